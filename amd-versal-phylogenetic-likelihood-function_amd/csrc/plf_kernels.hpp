@@ -1,0 +1,34 @@
+// plf_kernels.hpp -- launchers of the fused PLF kernels (internal to libplfx).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace plfx {
+
+// Self-resetting workspace for the in-kernel scaler-sum reduction: one 64-bit
+// word, bits [44,64) count the blocks that have arrived, bits [0,44) hold the
+// partial sum.  The last block to arrive writes the total and resets the word.
+constexpr int kTicketShift = 44;
+
+struct DnaArgs {
+  const void *x1, *x2;
+  void *x3;
+  const void *EV, *left, *right;
+  const int32_t *wgt;       // may be null (weights = 1)
+  uint8_t *scaler;          // may be null
+  int64_t *scaler_sum;      // may be null
+  unsigned long long *ws;   // ticket word (needed iff scaler_sum)
+  int64_t n;
+};
+
+// Fused DNA (4 states x 4 Gamma categories) inner-node update.
+// Returns the hipError_t of the launch.
+hipError_t launch_plf_dna_f32(const DnaArgs &a, int max_blocks, hipStream_t s);
+hipError_t launch_plf_dna_f64(const DnaArgs &a, int max_blocks, hipStream_t s);
+
+// sum_j scaler[j]*wgt[j] (host_mem.cpp:384-388), self-resetting ws as above.
+hipError_t launch_scaler_sum(const uint8_t *scaler, const int32_t *wgt, int64_t n,
+                             int64_t *out, unsigned long long *ws, int max_blocks,
+                             hipStream_t s);
+
+}  // namespace plfx

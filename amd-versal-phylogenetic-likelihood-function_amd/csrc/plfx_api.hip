@@ -1,0 +1,279 @@
+// plfx_api.hip -- the C ABI of include/plfx.h over the HIP kernels.
+//
+// Replaces the reference host's XRT layer (app/src/host_mem.cpp:108-157
+// kernel/bo/run setup, :283-394 run loop) and its CPU entry point plf()
+// (app/src/plf.h:1-5).  No C++ exception crosses this boundary; every entry
+// point returns a plfx_status.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/plfx.h"
+#include "plf_kernels.hpp"
+#include "testbench.hpp"
+
+struct plfx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int max_blocks = 2048;            // grid cap for the grid-stride kernels
+  unsigned long long *ws = nullptr; // ticket reduction words (2 x u64), zeroed once
+  // grow-only staging for the synchronous host entry points
+  void *d_buf = nullptr;
+  size_t d_cap = 0;
+  std::string err;
+};
+
+namespace {
+
+int fail(plfx_ctx *ctx, int code, const char *fmt, ...) {
+  if (ctx) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    ctx->err = buf;
+  }
+  return code;
+}
+
+int hip_fail(plfx_ctx *ctx, hipError_t e, const char *what) {
+  return fail(ctx, PLFX_ERR_HIP, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+#define PLFX_HIP(ctx, call)                          \
+  do {                                               \
+    hipError_t e_ = (call);                          \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+  } while (0)
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// NULL is the HIP null stream, as in every HIP API; pass plfx_ctx_stream(ctx)
+// to run on the context's own stream.
+hipStream_t pick(plfx_ctx *, void *stream) { return reinterpret_cast<hipStream_t>(stream); }
+
+int check_dev_args(plfx_ctx *ctx, const void *x1, const void *x2, const void *x3, const void *EV,
+                   int64_t n, const void *left, const void *right) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (n < 0) return fail(ctx, PLFX_ERR_INVALID, "n < 0 (%lld)", (long long)n);
+  if (n == 0) return PLFX_OK;
+  if (!x1 || !x2 || !x3 || !EV || !left || !right)
+    return fail(ctx, PLFX_ERR_INVALID, "null CLV/matrix pointer");
+  if (!aligned16(x1) || !aligned16(x2) || !aligned16(x3))
+    return fail(ctx, PLFX_ERR_INVALID, "CLV pointers must be 16-byte aligned");
+  if (x3 == x1 || x3 == x2) return fail(ctx, PLFX_ERR_INVALID, "x3 may not alias x1/x2");
+  return PLFX_OK;
+}
+
+template <typename T>
+int plf_dev(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int64_t n, const T *left,
+            const T *right, const int32_t *wgt, uint8_t *scaler, int64_t *scaler_sum,
+            void *stream) {
+  int rc = check_dev_args(ctx, x1, x2, x3, EV, n, left, right);
+  if (rc != PLFX_OK) return rc;
+  hipStream_t s = pick(ctx, stream);
+  if (n == 0) {
+    if (scaler_sum) PLFX_HIP(ctx, hipMemsetAsync(scaler_sum, 0, sizeof(int64_t), s));
+    return PLFX_OK;
+  }
+  plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, ctx->ws, n};
+  hipError_t e = sizeof(T) == 4 ? plfx::launch_plf_dna_f32(a, ctx->max_blocks, s)
+                                : plfx::launch_plf_dna_f64(a, ctx->max_blocks, s);
+  if (e != hipSuccess) return hip_fail(ctx, e, "plf_dna launch");
+  return PLFX_OK;
+}
+
+int ensure_dbuf(plfx_ctx *ctx, size_t bytes) {
+  if (bytes <= ctx->d_cap) return PLFX_OK;
+  if (ctx->d_buf) {
+    PLFX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    PLFX_HIP(ctx, hipFree(ctx->d_buf));
+    ctx->d_buf = nullptr;
+    ctx->d_cap = 0;
+  }
+  hipError_t e = hipMalloc(&ctx->d_buf, bytes);
+  if (e != hipSuccess) return fail(ctx, PLFX_ERR_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  ctx->d_cap = bytes;
+  return PLFX_OK;
+}
+
+size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// plf()-shaped synchronous host entry: H2D -> fused kernel -> D2H
+// (the reference's hm / msm / mh regions, host_mem.cpp:293-318).
+template <typename T>
+int plf_host(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int n, const T *left,
+             const T *right, const int *wgt, int *scalerIncrement) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (n < 0) return fail(ctx, PLFX_ERR_INVALID, "n < 0 (%d)", n);
+  if (n > 0 && (!x1 || !x2 || !x3 || !EV || !left || !right))
+    return fail(ctx, PLFX_ERR_INVALID, "null argument");
+  const size_t clv = (size_t)n * 16 * sizeof(T);
+  const size_t o_x1 = 0, o_x2 = round_up(clv, 256), o_x3 = o_x2 + round_up(clv, 256);
+  const size_t o_mat = o_x3 + round_up(clv, 256);  // EV 16 | left 64 | right 64
+  const size_t o_wgt = o_mat + round_up(144 * sizeof(T), 256);
+  const size_t o_sum = o_wgt + round_up((size_t)n * sizeof(int32_t), 256);
+  const size_t total = o_sum + 256;
+  int rc = ensure_dbuf(ctx, total);
+  if (rc != PLFX_OK) return rc;
+  char *d = static_cast<char *>(ctx->d_buf);
+  hipStream_t s = ctx->stream;
+  if (n > 0) {
+    PLFX_HIP(ctx, hipMemcpyAsync(d + o_x1, x1, clv, hipMemcpyHostToDevice, s));
+    PLFX_HIP(ctx, hipMemcpyAsync(d + o_x2, x2, clv, hipMemcpyHostToDevice, s));
+    PLFX_HIP(ctx, hipMemcpyAsync(d + o_mat, EV, 16 * sizeof(T), hipMemcpyHostToDevice, s));
+    PLFX_HIP(ctx, hipMemcpyAsync(d + o_mat + 16 * sizeof(T), left, 64 * sizeof(T), hipMemcpyHostToDevice, s));
+    PLFX_HIP(ctx, hipMemcpyAsync(d + o_mat + 80 * sizeof(T), right, 64 * sizeof(T), hipMemcpyHostToDevice, s));
+    if (wgt) PLFX_HIP(ctx, hipMemcpyAsync(d + o_wgt, wgt, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  }
+  const T *dm = reinterpret_cast<const T *>(d + o_mat);
+  rc = plf_dev<T>(ctx, reinterpret_cast<const T *>(d + o_x1), reinterpret_cast<const T *>(d + o_x2),
+                  reinterpret_cast<T *>(d + o_x3), dm, n, dm + 16, dm + 80,
+                  wgt ? reinterpret_cast<const int32_t *>(d + o_wgt) : nullptr, nullptr,
+                  reinterpret_cast<int64_t *>(d + o_sum), s);
+  if (rc != PLFX_OK) return rc;
+  int64_t sum = 0;
+  if (n > 0) PLFX_HIP(ctx, hipMemcpyAsync(x3, d + o_x3, clv, hipMemcpyDeviceToHost, s));
+  PLFX_HIP(ctx, hipMemcpyAsync(&sum, d + o_sum, sizeof sum, hipMemcpyDeviceToHost, s));
+  PLFX_HIP(ctx, hipStreamSynchronize(s));
+  if (scalerIncrement) *scalerIncrement = (int)sum;
+  return PLFX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int plfx_get_version(void) { return PLFX_VERSION; }
+
+int plfx_ctx_create(int device, plfx_ctx **out) {
+  if (!out) return PLFX_ERR_INVALID;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+    return PLFX_ERR_NODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return PLFX_ERR_NODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return PLFX_ERR_NODEV;
+  plfx_ctx *ctx = new (std::nothrow) plfx_ctx();
+  if (!ctx) return PLFX_ERR_NOMEM;
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return PLFX_ERR_HIP;
+  }
+  // Grid cap: enough resident 256-thread blocks to fill every CU a few times.
+  ctx->max_blocks = prop.multiProcessorCount * 8;
+  if (const char *env = std::getenv("PLFX_MAX_BLOCKS")) {
+    int v = std::atoi(env);
+    if (v > 0) ctx->max_blocks = v;
+  }
+  if (hipMalloc(reinterpret_cast<void **>(&ctx->ws), 2 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemsetAsync(ctx->ws, 0, 2 * sizeof(unsigned long long), ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return PLFX_ERR_HIP;
+  }
+  *out = ctx;
+  return PLFX_OK;
+}
+
+int plfx_ctx_destroy(plfx_ctx *ctx) {
+  if (!ctx) return PLFX_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->d_buf) (void)hipFree(ctx->d_buf);
+  if (ctx->ws) (void)hipFree(ctx->ws);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return PLFX_OK;
+}
+
+const char *plfx_last_error(const plfx_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void *plfx_ctx_stream(plfx_ctx *ctx) { return ctx ? reinterpret_cast<void *>(ctx->stream) : nullptr; }
+
+int plfx_ctx_device(const plfx_ctx *ctx) { return ctx ? ctx->device : -1; }
+
+int plfx_ctx_synchronize(plfx_ctx *ctx) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return PLFX_OK;
+}
+
+int plfx_plf_f32(plfx_ctx *ctx, const float *x1, const float *x2, float *x3, const float *EV, int n,
+                 const float *left, const float *right, const int *wgt, int *scalerIncrement) {
+  return plf_host<float>(ctx, x1, x2, x3, EV, n, left, right, wgt, scalerIncrement);
+}
+
+int plfx_plf_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *x3, const double *EV,
+                 int n, const double *left, const double *right, const int *wgt,
+                 int *scalerIncrement) {
+  return plf_host<double>(ctx, x1, x2, x3, EV, n, left, right, wgt, scalerIncrement);
+}
+
+int plfx_plf_dev_f32(plfx_ctx *ctx, const float *x1, const float *x2, float *x3, const float *EV,
+                     int64_t n, const float *left, const float *right, const int32_t *wgt,
+                     uint8_t *scaler, int64_t *scaler_sum, void *stream) {
+  return plf_dev<float>(ctx, x1, x2, x3, EV, n, left, right, wgt, scaler, scaler_sum, stream);
+}
+
+int plfx_plf_dev_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *x3,
+                     const double *EV, int64_t n, const double *left, const double *right,
+                     const int32_t *wgt, uint8_t *scaler, int64_t *scaler_sum, void *stream) {
+  return plf_dev<double>(ctx, x1, x2, x3, EV, n, left, right, wgt, scaler, scaler_sum, stream);
+}
+
+int plfx_instance_run(plfx_ctx *ctx, const void *in_left, const void *in_right, void *out_clv,
+                      uint8_t *out_scaler, uint32_t alignment_sites, uint32_t window_size,
+                      int layout, int dtype, void *stream) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (layout != PLFX_LAYOUT_COMBINED && layout != PLFX_LAYOUT_SEPARATE)
+    return fail(ctx, PLFX_ERR_INVALID, "bad layout %d", layout);
+  if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if (window_size % 16 != 0) return fail(ctx, PLFX_ERR_INVALID, "window_size %u not a multiple of 16", window_size);
+  if (!in_left || !in_right) return fail(ctx, PLFX_ERR_INVALID, "null instance buffer");
+  // Header words: in_left = [EV | P_L] (mm2sleft reads mem[0], mem[1..4]);
+  // in_right = [EV | P_R] (COMBINED, mem[1..4]) or [P_R] (SEPARATE, mem[0..3]).
+  const size_t es = dtype == PLFX_F32 ? 4 : 8;
+  const char *L = static_cast<const char *>(in_left);
+  const char *R = static_cast<const char *>(in_right);
+  const size_t rhdr = layout == PLFX_LAYOUT_COMBINED ? 80 : 64;
+  const void *EV = L;
+  const void *left = L + 16 * es;
+  const void *x1 = L + 80 * es;
+  const void *right = R + (rhdr - 64) * es;
+  const void *x2 = R + rhdr * es;
+  if (dtype == PLFX_F32)
+    return plf_dev<float>(ctx, (const float *)x1, (const float *)x2, (float *)out_clv,
+                          (const float *)EV, alignment_sites, (const float *)left,
+                          (const float *)right, nullptr, out_scaler, nullptr, stream);
+  return plf_dev<double>(ctx, (const double *)x1, (const double *)x2, (double *)out_clv,
+                         (const double *)EV, alignment_sites, (const double *)left,
+                         (const double *)right, nullptr, out_scaler, nullptr, stream);
+}
+
+int plfx_scaler_sum(plfx_ctx *ctx, const uint8_t *scaler, const int32_t *wgt, int64_t n,
+                    int64_t *out_sum, void *stream) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (!out_sum || n < 0 || (n > 0 && !scaler)) return fail(ctx, PLFX_ERR_INVALID, "bad scaler_sum args");
+  hipStream_t s = pick(ctx, stream);
+  if (n == 0) {
+    PLFX_HIP(ctx, hipMemsetAsync(out_sum, 0, sizeof(int64_t), s));
+    return PLFX_OK;
+  }
+  hipError_t e = plfx::launch_scaler_sum(scaler, wgt, n, out_sum, ctx->ws, ctx->max_blocks, s);
+  if (e != hipSuccess) return hip_fail(ctx, e, "scaler_sum launch");
+  return PLFX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,303 @@
+"""plfx -- Python binding of libplfx.so (include/plfx.h), the MI355X PLF engine.
+
+The binding mirrors the reference's interfaces for the PLF hot path:
+
+* ``plf(x1_start, x2_start, x3_start, EV, n, left, right, wgt)`` -- the
+  reference CPU entry point ``plf()`` (/root/reference/app/src/plf.h:1-5):
+  same argument order and meaning; the ``int& scalerIncrement`` out-argument
+  becomes the return value.  Runs on the GPU through ``plfx_plf_f32/f64``.
+* ``plf_dev(...)`` -- the same update on device-resident torch tensors,
+  asynchronous on a HIP stream (``plfx_plf_dev_f32/f64``); optional per-site
+  scaler bytes (the s2mm char output, hls/src/s2mm_memDNAwindowComb.cpp:97) and
+  weighted scaler sum (host_mem.cpp:384-388).
+* ``instance_run(...)`` -- the accelerator instance-buffer contract
+  (host_mem.cpp:123-157): packed [EV|P_L|CLV_L] / [EV|P_R|CLV_R] or [P_R|CLV_R].
+* ``Testbench`` / ``pack_instance`` -- testbench_info sizing
+  (app/src/include.h:150-266) and packing (host_mem.cpp:221-243).
+
+There is no CPU fallback: if libplfx.so or a gfx950 device is missing every
+call raises ``PlfxError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "libplfx.so"
+
+OK = 0
+ERR_INVALID, ERR_HIP, ERR_NOMEM, ERR_NODEV, ERR_UNSUPPORTED = -1, -2, -3, -4, -5
+LAYOUT_COMBINED, LAYOUT_SEPARATE = 0, 1
+AIE_STREAM, AIE_WINDOW = 0, 1
+F32, F64 = 0, 1
+
+# symbols declared by include/plfx.h (checked by tests/test_abi.py)
+EXPORTS = (
+    "plfx_ctx_create", "plfx_ctx_destroy", "plfx_last_error", "plfx_get_version",
+    "plfx_ctx_stream", "plfx_ctx_device", "plfx_ctx_synchronize",
+    "plfx_plf_f32", "plfx_plf_f64", "plfx_plf_dev_f32", "plfx_plf_dev_f64",
+    "plfx_instance_run", "plfx_scaler_sum",
+    "plfx_tb_alignments_per_instance", "plfx_tb_alignments_padding",
+    "plfx_tb_instance_site_offset", "plfx_tb_elements_per_instance",
+    "plfx_tb_instance_elements_left", "plfx_tb_instance_elements_right",
+    "plfx_tb_instance_elements_out",
+    "plfx_tb_instance_active_elements_left", "plfx_tb_instance_active_elements_right",
+    "plfx_tb_num_windows_per_instance", "plfx_pack_instance",
+)
+
+
+class PlfxError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__(f"plfx error {code}: {msg}")
+        self.code = code
+
+
+class _TB(C.Structure):
+    _fields_ = [("alignment_sites", C.c_uint64), ("parallel_instances", C.c_uint32),
+                ("window_size", C.c_uint32), ("layout", C.c_int32), ("aie_type", C.c_int32)]
+
+
+_lib = None
+
+
+def load():
+    """Load libplfx.so.  torch is imported first (when present) so that the
+    library binds to the same HIP runtime instance as torch's allocations."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401  -- share torch's libamdhip64
+    except ImportError:
+        pass
+    if not LIB_PATH.exists():
+        raise PlfxError(ERR_UNSUPPORTED, f"{LIB_PATH} not built (run __graft_entry__.build())")
+    L = C.CDLL(str(LIB_PATH))
+    vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int
+    L.plfx_ctx_create.argtypes = [i32, C.POINTER(vp)]
+    L.plfx_ctx_destroy.argtypes = [vp]
+    L.plfx_last_error.argtypes = [vp]
+    L.plfx_last_error.restype = C.c_char_p
+    L.plfx_ctx_stream.argtypes = [vp]
+    L.plfx_ctx_stream.restype = vp
+    L.plfx_ctx_device.argtypes = [vp]
+    L.plfx_ctx_synchronize.argtypes = [vp]
+    for s in ("f32", "f64"):
+        getattr(L, f"plfx_plf_{s}").argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, C.POINTER(i32)]
+        getattr(L, f"plfx_plf_dev_{s}").argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
+    L.plfx_instance_run.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, C.c_uint32, i32, i32, vp]
+    L.plfx_scaler_sum.argtypes = [vp, vp, vp, i64, vp, vp]
+    tbp = C.POINTER(_TB)
+    for name in ("alignments_per_instance", "instance_site_offset",
+                 "instance_active_elements_left", "instance_active_elements_right"):
+        f = getattr(L, f"plfx_tb_{name}")
+        f.argtypes = [tbp, i32]
+        f.restype = C.c_uint64
+    for name in ("alignments_padding", "elements_per_instance", "instance_elements_left",
+                 "instance_elements_right", "instance_elements_out", "num_windows_per_instance"):
+        f = getattr(L, f"plfx_tb_{name}")
+        f.argtypes = [tbp]
+        f.restype = C.c_uint64
+    L.plfx_pack_instance.argtypes = [tbp, i32, i32, vp, vp, vp, vp, vp, vp, vp]
+    _lib = L
+    return L
+
+
+class Context:
+    """A libplfx context bound to one HIP device (replaces acap_info,
+    app/src/include.h:28-147)."""
+
+    def __init__(self, device: int = 0):
+        self._L = load()
+        h = C.c_void_p()
+        rc = self._L.plfx_ctx_create(int(device), C.byref(h))
+        if rc != OK:
+            raise PlfxError(rc, f"plfx_ctx_create(device={device}) failed "
+                                "(no gfx950 device visible?)")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.plfx_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def stream(self):
+        return self._L.plfx_ctx_stream(self.h)
+
+    def synchronize(self):
+        self._check(self._L.plfx_ctx_synchronize(self.h))
+
+    def _check(self, rc):
+        if rc != OK:
+            raise PlfxError(rc, self._L.plfx_last_error(self.h).decode(errors="replace"))
+
+    # -- (1) plf() drop-in on host arrays ----------------------------------
+    def plf(self, x1_start, x2_start, x3_start, EV, n, left, right, wgt=None):
+        """plf(x1, x2, x3, EV, n, left, right, wgt) -> scalerIncrement.
+
+        numpy float32 or float64 arrays, x3_start written in place."""
+        dt = np.asarray(x1_start).dtype
+        if dt not in (np.float32, np.float64):
+            raise PlfxError(ERR_INVALID, f"unsupported dtype {dt}")
+        arrs = [x1_start, x2_start, x3_start, EV, left, right]
+        for a in arrs:
+            if not (isinstance(a, np.ndarray) and a.dtype == dt and a.flags.c_contiguous):
+                raise PlfxError(ERR_INVALID, "arrays must be C-contiguous numpy arrays of one dtype")
+        n = int(n)
+        if x1_start.size < 16 * n or x2_start.size < 16 * n or x3_start.size < 16 * n:
+            raise PlfxError(ERR_INVALID, "CLV arrays shorter than 16*n")
+        if EV.size < 16 or left.size < 64 or right.size < 64:
+            raise PlfxError(ERR_INVALID, "EV needs 16, left/right 64 values")
+        w = None
+        if wgt is not None:
+            w = np.ascontiguousarray(wgt, dtype=np.int32)
+            if w.size < n:
+                raise PlfxError(ERR_INVALID, "wgt shorter than n")
+        inc = C.c_int(0)
+        fn = self._L.plfx_plf_f32 if dt == np.float32 else self._L.plfx_plf_f64
+        p = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        self._check(fn(self.h, p(x1_start), p(x2_start), p(x3_start), p(EV), n, p(left), p(right),
+                       p(w), C.byref(inc)))
+        return inc.value
+
+    # -- (2) device-resident hot path ---------------------------------------
+    def plf_dev(self, x1, x2, x3, EV, left, right, wgt=None, scaler=None, scaler_sum=None,
+                n=None, stream=None):
+        """Fused PLF on torch device tensors (float32/float64, contiguous).
+
+        Asynchronous on `stream` (a torch.cuda.Stream, a raw hipStream_t int,
+        or None = torch's current stream)."""
+        import torch
+
+        dt = x1.dtype
+        if dt not in (torch.float32, torch.float64):
+            raise PlfxError(ERR_INVALID, f"unsupported dtype {dt}")
+        for t in (x1, x2, x3, EV, left, right):
+            if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
+                raise PlfxError(ERR_INVALID, "tensors must be contiguous device tensors of one dtype")
+        if n is None:
+            n = x1.numel() // 16
+        n = int(n)
+        if min(x1.numel(), x2.numel(), x3.numel()) < 16 * n:
+            raise PlfxError(ERR_INVALID, "CLV tensors shorter than 16*n")
+        if EV.numel() < 16 or left.numel() < 64 or right.numel() < 64:
+            raise PlfxError(ERR_INVALID, "EV needs 16, left/right 64 values")
+        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n or not wgt.is_cuda):
+            raise PlfxError(ERR_INVALID, "wgt must be an int32 device tensor of >= n elements")
+        if scaler is not None and (scaler.dtype != torch.uint8 or scaler.numel() < n):
+            raise PlfxError(ERR_INVALID, "scaler must be a uint8 device tensor of >= n elements")
+        if scaler_sum is not None and (scaler_sum.dtype != torch.int64 or scaler_sum.numel() < 1):
+            raise PlfxError(ERR_INVALID, "scaler_sum must be an int64 device tensor")
+        fn = self._L.plfx_plf_dev_f32 if dt == torch.float32 else self._L.plfx_plf_dev_f64
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        self._check(fn(self.h, p(x1), p(x2), p(x3), p(EV), n, p(left), p(right), p(wgt),
+                       p(scaler), p(scaler_sum), _stream_handle(stream)))
+
+    # -- (3) instance-buffer contract --------------------------------------
+    def instance_run(self, in_left, in_right, out_clv, out_scaler, alignment_sites, window_size,
+                     layout, stream=None):
+        import torch
+
+        dt = in_left.dtype
+        if dt not in (torch.float32, torch.float64) or in_right.dtype != dt or out_clv.dtype != dt:
+            raise PlfxError(ERR_INVALID, "instance buffers must share a float dtype")
+        hdr_r = 80 if layout == LAYOUT_COMBINED else 64
+        n = int(alignment_sites)
+        if in_left.numel() < 80 + 16 * n or in_right.numel() < hdr_r + 16 * n or \
+                out_clv.numel() < 16 * n:
+            raise PlfxError(ERR_INVALID, "instance buffers too small for alignment_sites")
+        if out_scaler is not None and (out_scaler.dtype != torch.uint8 or out_scaler.numel() < n):
+            raise PlfxError(ERR_INVALID, "out_scaler must be uint8 with >= alignment_sites bytes")
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        self._check(self._L.plfx_instance_run(self.h, p(in_left), p(in_right), p(out_clv),
+                                              p(out_scaler), n, int(window_size), int(layout),
+                                              F32 if dt == torch.float32 else F64,
+                                              _stream_handle(stream)))
+
+    # -- (4) scaler reduction ----------------------------------------------
+    def scaler_sum(self, scaler, wgt, out_sum, n=None, stream=None):
+        import torch
+
+        if n is None:
+            n = scaler.numel()
+        if scaler.dtype != torch.uint8 or out_sum.dtype != torch.int64:
+            raise PlfxError(ERR_INVALID, "scaler uint8, out_sum int64")
+        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n):
+            raise PlfxError(ERR_INVALID, "wgt int32 with >= n elements")
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        self._check(self._L.plfx_scaler_sum(self.h, p(scaler), p(wgt), int(n), p(out_sum),
+                                            _stream_handle(stream)))
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return C.c_void_p(stream)
+    return C.c_void_p(stream.cuda_stream)
+
+
+_default_ctx = None
+
+
+def default_context():
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+def plf(x1_start, x2_start, x3_start, EV, n, left, right, wgt=None):
+    """Module-level drop-in for the reference plf() (app/src/plf.h:1-5) on the
+    default context.  Returns scalerIncrement."""
+    return default_context().plf(x1_start, x2_start, x3_start, EV, n, left, right, wgt)
+
+
+class Testbench:
+    """testbench_info (app/src/include.h:150-266) via the C ABI (64-bit)."""
+
+    def __init__(self, alignment_sites, parallel_instances=1, window_size=1024,
+                 layout=LAYOUT_SEPARATE, aie_type=AIE_WINDOW):
+        self._L = load()
+        self.t = _TB(int(alignment_sites), int(parallel_instances), int(window_size), int(layout),
+                     int(aie_type))
+
+    def __getattr__(self, name):
+        f = getattr(self._L, f"plfx_tb_{name}", None)
+        if f is None:
+            raise AttributeError(name)
+        if len(f.argtypes) == 2:
+            return lambda k=-1: int(f(C.byref(self.t), int(k)))
+        return lambda: int(f(C.byref(self.t)))
+
+    def pack_instance(self, k, EV, left, right, x1, x2):
+        dt = np.asarray(x1).dtype
+        L = np.empty(self.instance_elements_left(), dt)
+        R = np.empty(self.instance_elements_right(), dt)
+        keep = [np.ascontiguousarray(a, dt) for a in (EV, left, right, x1, x2)]
+        rc = self._L.plfx_pack_instance(C.byref(self.t), int(k), F32 if dt == np.float32 else F64,
+                                        *[a.ctypes.data_as(C.c_void_p) for a in keep],
+                                        L.ctypes.data_as(C.c_void_p), R.ctypes.data_as(C.c_void_p))
+        if rc != OK:
+            raise PlfxError(rc, "plfx_pack_instance failed")
+        return L, R

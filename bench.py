@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""bench.py -- PLF sites/s (4-state DNA, fp64) on 1..8 MI355X + % HBM roofline.
+
+Workload (BASELINE.json configs[1]): one inner-node PLF update
+(app/src/plf.cpp:19-65 semantics: two 4x4 P x child-CLV matvecs per Gamma
+category, element-wise product, EV back-transform, underflow rescale, per-site
+scaler byte and weighted scaler sum) over 2^20 sites in fp64 per GPU per step.
+A step is one launch of the fused kernel over one node's CLVs, inputs already
+resident in HBM.  Steps rotate over R independent buffer sets (R x 389 MiB >
+the 256 MiB Infinity Cache) so every step streams from HBM.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank evaluates
+its own independent inner nodes (the reference's instance split over sites /
+nodes, include.h:181-195) with no data-path collective: weak scaling.  After
+the timed region one RCCL all-reduce combines the per-rank scaler totals.
+
+Prints ONE JSON line on rank 0 (driver contract), with
+  roofline:      algorithmic bytes per launch / average launch duration
+                 (HIP events on the launch stream) against 8 TB/s; `traffic`
+                 = HBM bytes per launch from the committed rocprofv3 PMC pass
+                 (profiles/), or null;
+  cpu_baseline:  the oracle's OpenMP f64 port on this host's cores over a
+                 bounded sample (plus the single-thread port and the reference
+                 plf() itself at its own -O0 flags as extra fields).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "amd-versal-phylogenetic-likelihood-function_amd"
+sys.path.insert(0, str(PKG))
+
+METRIC = "PLF sites/sec (4-state DNA, fp64) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SEED = 20250117
+
+
+def bytes_per_site(dtype_bytes):
+    # read x1, x2 (16 values each), write x3 (16 values), write 1 scaler byte,
+    # read 4-byte wgt (the kernel computes the weighted scaler sum)
+    return 3 * 16 * dtype_bytes + 1 + 4
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--sites", type=int, default=1 << 20)
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--buffer-sets", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0,
+                    help="wall seconds per CPU-baseline variant (bounded sample)")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(n_sites, seconds):
+    """Oracle (CPU restatement of plf()) timed on this host: OpenMP f64 over
+    up to 16 threads (the primary number), 1-thread f64, and the reference's
+    own plf() (f32, its -O0 host flags) when oracle/_ref is present."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+
+    import oracle as O
+
+    threads = min(16, os.cpu_count() or 1)
+    d = O.gen_hostmem(n_sites, np.float64, SEED)
+    out = (np.empty(16 * n_sites, np.float64), np.empty(n_sites, np.uint8))
+
+    def timed(fn, sites):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return reps * sites / el, reps
+
+    mt, reps_mt = timed(lambda: O.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"],
+                                      threads=threads, out=out), n_sites)
+    n1 = min(n_sites, 1 << 18)
+    s1 = {k: (v[:16 * n1] if k in ("x1", "x2") else v) for k, v in d.items()}
+    out1 = (np.empty(16 * n1, np.float64), np.empty(n1, np.uint8))
+    st, _ = timed(lambda: O.plf(s1["x1"], s1["x2"], s1["EV"], s1["left"], s1["right"], s1["wgt"][:n1],
+                                out=out1), n1)
+    res = {"value": mt, "unit": "sites/s", "cores": threads, "kind": "port",
+           "sample": f"{reps_mt} x {n_sites} sites, f64, host_mem input protocol, "
+                     f"OpenMP static split, ~{seconds:.0f}s wall",
+           "single_thread_port_f64": st}
+    if O.ref_lib("O0") is not None:
+        f = O.gen_hostmem(1 << 16, np.float32, SEED)
+        rt, _ = timed(lambda: O.ref_plf(f["x1"], f["x2"], f["EV"], f["left"], f["right"], f["wgt"]),
+                      1 << 16)
+        res["reference_plf_O0_f32_1thread"] = rt
+    return res
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world:
+        sys.exit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    import plfx
+
+    ctx = plfx.Context(local)
+    tdt = torch.float64 if a.dtype == "f64" else torch.float32
+    esz = 8 if a.dtype == "f64" else 4
+    n = a.sites
+    R = max(1, a.buffer_sets)
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED + rank)
+    EV = torch.rand(16, dtype=tdt, device=dev, generator=g)
+    left = torch.rand(64, dtype=tdt, device=dev, generator=g)
+    right = torch.rand(64, dtype=tdt, device=dev, generator=g)
+    sets = []
+    for _ in range(R):
+        x1 = torch.rand(n * 16, dtype=tdt, device=dev, generator=g)
+        x1.view(-1, 16)[0::4] *= 1e-12  # host_mem.cpp:200-202: every 4th site underflows
+        x2 = torch.rand(n * 16, dtype=tdt, device=dev, generator=g)
+        sets.append(dict(x1=x1, x2=x2, x3=torch.empty_like(x1),
+                         wgt=torch.ones(n, dtype=torch.int32, device=dev),
+                         sc=torch.empty(n, dtype=torch.uint8, device=dev),
+                         s=torch.zeros(1, dtype=torch.int64, device=dev)))
+    stream = torch.cuda.Stream(dev)          # dedicated launch stream; events on it
+    sh = stream.cuda_stream
+    torch.cuda.synchronize(dev)
+
+    def step(i):
+        b = sets[i % R]
+        ctx.plf_dev(b["x1"], b["x2"], b["x3"], EV, left, right, b["wgt"], b["sc"], b["s"], stream=sh)
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for i in range(a.steps):
+        step(a.warmup + i)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    dev_ms = e0.elapsed_time(e1)
+
+    # correctness spot check of the last step's scaler total (n/4 sites scale)
+    last = sets[(a.warmup + a.steps - 1) % R]
+    expect = (n + 3) // 4
+    tot = torch.stack([last["s"][0], torch.tensor(expect, device=dev, dtype=torch.int64)])
+    t = torch.tensor([wall_ms, dev_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)      # max over ranks
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)    # one RCCL all-reduce of scaler totals
+    wall_ms, dev_ms = float(t[0]), float(t[1])
+    check_ok = int(tot[0]) == int(tot[1])
+
+    if rank == 0:
+        per_launch_ms = dev_ms / a.steps
+        bps = bytes_per_site(esz)
+        achieved = bps * n / (per_launch_ms * 1e-3) / 1e9
+        traffic = None
+        tp = Path(a.traffic_json)
+        if tp.exists():
+            try:
+                tj = json.loads(tp.read_text())
+                if tj.get("sites") == n and tj.get("dtype") == a.dtype:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except (ValueError, OSError):
+                traffic = None
+        value = world * n * a.steps / (wall_ms * 1e-3)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "sites/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": wall_ms / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic (torch.rand U[0,1) CLVs/P/EV, left CLV x1e-12 on every 4th site, wgt=1)",
+            "config": {
+                "workload": "DNA 4-state x 4 Gamma cats, 1 inner node per GPU per step, "
+                            f"{n} sites, {a.dtype} (BASELINE configs[1])",
+                "sites_per_gpu_per_step": n,
+                "nodes_per_gpu_per_step": 1,
+                "buffer_sets": R,
+                "parallelism": f"independent nodes x{world} (replicas, no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "bytes_per_site": bps,
+                "kernel_avg_us": per_launch_ms * 1e3,
+            },
+            "check": "ok" if check_ok else "SCALER_SUM_MISMATCH",
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if not check_ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

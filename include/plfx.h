@@ -1,0 +1,166 @@
+/*
+ * plfx.h -- C ABI of the MI355X-native PLF engine (libplfx.so).
+ *
+ * This is the drop-in boundary.  It replaces the two interfaces through which
+ * the reference drives its PLF hot path:
+ *
+ *   (1) the CPU entry point  void plf(float* x1_start, float* x2_start,
+ *       float* x3_start, float* EV, const int n, float* left, float* right,
+ *       int* wgt, int& scalerIncrement)
+ *       -- /root/reference/app/src/plf.h:1-5, defined app/src/plf.cpp:8-68,
+ *       called from app/src/host_mem.cpp:418;
+ *   (2) the XRT accelerator contract of app/src/host_mem.cpp:108-157,283-394:
+ *       per instance an `in_left` bo = [EV16 | P_L64 | CLV_L], an `in_right`
+ *       bo = [EV16 | P_R64 | CLV_R] (COMBINED) or [P_R64 | CLV_R] (SEPARATE),
+ *       an `out` bo (CLV) and an `out_scaler` bo (char per site), with kernel
+ *       arguments mm2sleft/mm2sright(mem, alignment_sites, window_size)
+ *       (hls/src/mm2sleft_memDNAwindowComb.cpp:16) and
+ *       s2mm(mem, scalerIncrement, alignment_sites, window_size)
+ *       (hls/src/s2mm_memDNAwindowComb.cpp:20), and the host-side scaler
+ *       reduction sum_j scaler[j]*wgt[j] (host_mem.cpp:384-388).
+ *
+ * Data layout (identical to the reference): a site is S*C values stored
+ * site-major as x[site*16 + cat*4 + state] for DNA (4 Gamma categories x 4
+ * states, plf.cpp:21-23); P matrices are left[cat*16 + k*4 + l] (row-major
+ * P_c, plf.cpp:37-38); EV is EV[k*4 + l] (plf.cpp:47).
+ *
+ * Semantics (plf.cpp:19-65): for every site and category
+ *   ump_L[k] = sum_l x1[c*4+l]*left[c*16+k*4+l]   (same for right/x2)
+ *   x3[c*4+l] = sum_k (ump_L[k]*ump_R[k]) * EV[4k+l]
+ * then if every |x3| of the site is < 2^-32 (strict; NaN never scales), all
+ * values of the site are multiplied by 2^32, the per-site scaler byte is 1
+ * and wgt[site] is added to the scaler increment.  Arithmetic is IEEE with
+ * no FMA contraction and the reference's accumulation order, so the f32
+ * entry points reproduce the reference bit-for-bit and f64 reproduces the
+ * double instantiation of the same loop bit-for-bit.
+ *
+ * All functions return PLFX_OK (0) or a negative plfx_status; they never
+ * throw.  plfx_last_error() gives a message for the last failure on a
+ * context.  `stream` arguments are hipStream_t values passed as void* (NULL =
+ * the HIP null stream, as everywhere in HIP; plfx_ctx_stream() gives the
+ * context's own non-blocking stream).  Device pointers must come from the same HIP
+ * device as the context; CLV pointers must be 16-byte aligned.  A context
+ * may be used from one host thread at a time; distinct contexts are
+ * independent.  No allocation happens per call after warm-up (the host
+ * entry points keep grow-only staging buffers in the context).
+ */
+#ifndef PLFX_H
+#define PLFX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PLFX_VERSION 10000 /* 1.0.0 */
+
+typedef enum {
+  PLFX_OK = 0,
+  PLFX_ERR_INVALID = -1,     /* bad argument (null pointer, size, alignment) */
+  PLFX_ERR_HIP = -2,         /* HIP runtime failure; see plfx_last_error()   */
+  PLFX_ERR_NOMEM = -3,       /* device allocation failed                      */
+  PLFX_ERR_NODEV = -4,       /* no such HIP device / not a gfx950 device      */
+  PLFX_ERR_UNSUPPORTED = -5  /* states/categories combination not built       */
+} plfx_status;
+
+/* Instance-buffer header layout: app/src/include.h:20 (COMBINED, SEPARATE). */
+typedef enum { PLFX_LAYOUT_COMBINED = 0, PLFX_LAYOUT_SEPARATE = 1 } plfx_layout;
+/* AIE transport of the reference: app/src/include.h:21 (STREAM, WINDOW).
+ * Only affects buffer sizing (padding); the GPU needs neither. */
+typedef enum { PLFX_AIE_STREAM = 0, PLFX_AIE_WINDOW = 1 } plfx_aie;
+typedef enum { PLFX_F32 = 0, PLFX_F64 = 1 } plfx_dtype;
+
+typedef struct plfx_ctx plfx_ctx;
+
+/* ---- context ----------------------------------------------------------- */
+/* Replaces acap_info (app/src/include.h:28-147): binds a HIP device and owns
+ * a non-blocking stream, the scaler-sum workspace and host staging buffers. */
+int plfx_ctx_create(int device, plfx_ctx **ctx);
+int plfx_ctx_destroy(plfx_ctx *ctx);
+const char *plfx_last_error(const plfx_ctx *ctx);
+int plfx_get_version(void);
+/* The context's stream (hipStream_t) and device ordinal. */
+void *plfx_ctx_stream(plfx_ctx *ctx);
+int plfx_ctx_device(const plfx_ctx *ctx);
+/* Synchronise the context's stream. */
+int plfx_ctx_synchronize(plfx_ctx *ctx);
+
+/* ---- (1) drop-in for plf(): host arrays, synchronous -------------------- */
+/* Same argument order and meaning as plf() (app/src/plf.h:1-5); `int&` is
+ * `int*`.  Copies to the device, runs the fused kernel, copies back.
+ * wgt may be NULL (= all ones). */
+int plfx_plf_f32(plfx_ctx *ctx, const float *x1_start, const float *x2_start,
+                 float *x3_start, const float *EV, int n, const float *left,
+                 const float *right, const int *wgt, int *scalerIncrement);
+int plfx_plf_f64(plfx_ctx *ctx, const double *x1_start, const double *x2_start,
+                 double *x3_start, const double *EV, int n, const double *left,
+                 const double *right, const int *wgt, int *scalerIncrement);
+
+/* ---- (2) the hot path on device-resident CLVs, asynchronous ------------- */
+/* All pointers are device pointers.  wgt, scaler (uint8 per site, the s2mm
+ * char output) and scaler_sum (int64, = sum scaler*wgt, wgt NULL => 1) are
+ * each optional (NULL = not produced / not read).  n may be 0. */
+int plfx_plf_dev_f32(plfx_ctx *ctx, const float *x1, const float *x2, float *x3,
+                     const float *EV, int64_t n, const float *left,
+                     const float *right, const int32_t *wgt, uint8_t *scaler,
+                     int64_t *scaler_sum, void *stream);
+int plfx_plf_dev_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *x3,
+                     const double *EV, int64_t n, const double *left,
+                     const double *right, const int32_t *wgt, uint8_t *scaler,
+                     int64_t *scaler_sum, void *stream);
+
+/* ---- (3) the accelerator instance-buffer contract ----------------------- */
+/* in_left/in_right/out_clv/out_scaler: device buffers exactly as the
+ * reference packs them (host_mem.cpp:221-243): in_left = [EV 16 | P_L 64 |
+ * CLV_L], in_right = [EV 16 | P_R 64 | CLV_R] (COMBINED) or [P_R 64 | CLV_R]
+ * (SEPARATE); element type `dtype`.  Writes alignment_sites CLVs to out_clv
+ * and alignment_sites scaler bytes to out_scaler (never the window padding,
+ * SURVEY Q4/Q5).  window_size (bytes of an AIE window, a multiple of 16; 0
+ * for stream configs) is validated for sizing parity but not needed by the
+ * kernel. */
+int plfx_instance_run(plfx_ctx *ctx, const void *in_left, const void *in_right,
+                      void *out_clv, uint8_t *out_scaler, uint32_t alignment_sites,
+                      uint32_t window_size, int layout, int dtype, void *stream);
+
+/* ---- (4) scaler reduction (host_mem.cpp:384-388) on the device ---------- */
+/* out_sum (device int64) = sum_j scaler[j] * (wgt ? wgt[j] : 1). */
+int plfx_scaler_sum(plfx_ctx *ctx, const uint8_t *scaler, const int32_t *wgt,
+                    int64_t n, int64_t *out_sum, void *stream);
+
+/* ---- (5) instance sizing: testbench_info (app/src/include.h:150-266) ---- */
+/* 64-bit throughout.  `instance` < 0 means "no instance" where the
+ * reference has an overload without one. */
+typedef struct {
+  uint64_t alignment_sites;
+  uint32_t parallel_instances;
+  uint32_t window_size;  /* bytes, AIE window (include.h:155) */
+  int32_t layout;        /* plfx_layout */
+  int32_t aie_type;      /* plfx_aie */
+} plfx_testbench;
+
+uint64_t plfx_tb_alignments_per_instance(const plfx_testbench *tb, int instance);
+uint64_t plfx_tb_alignments_padding(const plfx_testbench *tb);
+uint64_t plfx_tb_instance_site_offset(const plfx_testbench *tb, int instance);
+uint64_t plfx_tb_elements_per_instance(const plfx_testbench *tb);
+uint64_t plfx_tb_instance_elements_left(const plfx_testbench *tb);
+uint64_t plfx_tb_instance_elements_right(const plfx_testbench *tb);
+uint64_t plfx_tb_instance_elements_out(const plfx_testbench *tb);
+uint64_t plfx_tb_instance_active_elements_left(const plfx_testbench *tb, int instance);
+uint64_t plfx_tb_instance_active_elements_right(const plfx_testbench *tb, int instance);
+uint64_t plfx_tb_num_windows_per_instance(const plfx_testbench *tb);
+
+/* Host packing of one instance's input buffers (host_mem.cpp:221-243) into
+ * caller-provided host arrays of instance_elements_{left,right} elements of
+ * `dtype`; padding is zero-filled. */
+int plfx_pack_instance(const plfx_testbench *tb, int instance, int dtype,
+                       const void *EV, const void *left, const void *right,
+                       const void *x1_all, const void *x2_all, void *out_left,
+                       void *out_right);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* PLFX_H */

@@ -1,0 +1,461 @@
+"""CPU oracle for the PLF hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker / the timed CPU baseline.
+The product (``libplfx.so``, its HIP kernels, the C++ host driver and the
+``plfx`` Python binding) never imports, links or calls anything here.
+
+Contents
+--------
+* ctypes bindings to ``liboracle.so`` (``plf_oracle.c``): the clean-room
+  restatement of ``plf()`` (/root/reference/app/src/plf.cpp:8-68) in float and
+  double, a generic S-state/C-category form, the host_mem input protocol
+  (/root/reference/app/src/host_mem.cpp:179-209) and the scaler reduction
+  (host_mem.cpp:384-388).
+* ctypes bindings to the reference's own ``plf()`` built into ``oracle/_ref``
+  from /root/reference/app/src/plf.cpp (oracle/Makefile), used to pin the
+  restatement.
+* ``testbench_*``: the instance sizing/partition arithmetic of
+  ``testbench_info`` (/root/reference/app/src/include.h:150-266).
+* ``pack_instance``: the per-instance input buffers of host_mem.cpp:221-243.
+* ``mm2s_lane_streams`` / ``s2mm``: the PL data movers
+  (hls/src/mm2sleft_memDNAwindowComb.cpp:16-100, mm2sright_*,
+  mm2sleft_memDNAwindowSep.cpp:16-95, mm2sright_memDNAwindowSep.cpp:16-88,
+  mm2sleft_memDNAstreamComb.cpp:16-116, transpose.cpp:6-24,
+  s2mm_memDNAwindowComb.cpp:20-101), restated over numpy so that the
+  AIE test vectors in aie/data pin the packing.
+* ``parse_aie_kat``: reads the reference's AIE golden vectors
+  (aie/data/golden{0..3}.txt and their stimuli).
+
+Parity status: the float path is pinned (reference binary + AIE goldens +
+committed fixtures).  Double, protein (S=20), tree sweep and lnL are
+extensions the reference does not have: parity unpinned beyond being the same
+loop as the pinned float path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB_PATH = ORACLE_DIR / "liboracle.so"
+REF_O0 = ORACLE_DIR / "_ref" / "libplfref_O0.so"
+REF_O3 = ORACLE_DIR / "_ref" / "libplfref_O3.so"
+
+TWO_TO_32 = 4294967296.0
+MINLIKELIHOOD = 1.0 / TWO_TO_32
+SEED = 20250117
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+
+_lib = None
+_refs: dict = {}
+
+
+def build():
+    """Compile liboracle.so (and oracle/_ref when /root/reference exists)."""
+    import subprocess
+
+    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(LIB_PATH))
+        for sfx, fp in (("f32", _f32p), ("f64", _f64p)):
+            f = getattr(L, f"plfo_plf_{sfx}")
+            f.argtypes = [fp, fp, fp, fp, C.c_longlong, fp, fp, C.c_void_p,
+                          C.POINTER(C.c_int), C.c_void_p]
+            f.restype = None
+            f = getattr(L, f"plfo_plf_{sfx}_omp")
+            f.argtypes = [fp, fp, fp, fp, C.c_longlong, fp, fp, C.c_void_p,
+                          C.POINTER(C.c_int), C.c_void_p, C.c_int]
+            f.restype = None
+            f = getattr(L, f"plfo_plf_gen_{sfx}")
+            f.argtypes = [C.c_int, C.c_int, fp, fp, fp, fp, C.c_longlong, fp, fp,
+                          C.c_void_p, C.POINTER(C.c_longlong), C.c_void_p]
+            f.restype = None
+            f = getattr(L, f"plfo_gen_hostmem_{sfx}")
+            f.argtypes = [C.c_uint32, C.c_longlong, fp, fp, fp, fp, fp, C.c_void_p]
+            f.restype = None
+        L.plfo_scaler_sum.argtypes = [_u8p, C.c_void_p, C.c_longlong]
+        L.plfo_scaler_sum.restype = C.c_longlong
+        L.plfo_mt_draws.argtypes = [C.c_uint32, C.c_longlong, C.c_void_p, C.c_void_p]
+        L.plfo_mt_draws.restype = None
+        _lib = L
+    return _lib
+
+
+def ref_lib(opt: str = "O0"):
+    """The reference plf() itself (oracle/_ref), or None if it was not built."""
+    if opt not in _refs:
+        p = REF_O0 if opt == "O0" else REF_O3
+        if not p.exists():
+            _refs[opt] = None
+        else:
+            L = C.CDLL(str(p))
+            L.plfref_plf.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, _f32p,
+                                     _f32p, _i32p]
+            L.plfref_plf.restype = C.c_int
+            _refs[opt] = L
+    return _refs[opt]
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _sfx(dtype):
+    return "f32" if np.dtype(dtype) == np.float32 else "f64"
+
+
+# --------------------------------------------------------------------------
+# plf() and friends
+# --------------------------------------------------------------------------
+def plf(x1, x2, EV, left, right, wgt=None, n=None, threads=0, out=None):
+    """Restated plf(): returns (x3, scaler_bytes, scalerIncrement).
+
+    threads > 0 uses the OpenMP variant (identical results); `out` may supply
+    preallocated (x3, scaler) arrays."""
+    dt = x1.dtype
+    if n is None:
+        n = x1.size // 16
+    if out is not None:
+        x3, sc = out
+    else:
+        x3 = np.empty(n * 16, dtype=dt)
+        sc = np.empty(n, dtype=np.uint8)
+    inc = C.c_int(0)
+    L = lib()
+    if wgt is not None:
+        wgt = np.ascontiguousarray(wgt, dtype=np.int32)
+    if threads > 0:
+        getattr(L, f"plfo_plf_{_sfx(dt)}_omp")(x1, x2, x3, EV, n, left, right,
+                                              _ptr(wgt), C.byref(inc), _ptr(sc), threads)
+    else:
+        getattr(L, f"plfo_plf_{_sfx(dt)}")(x1, x2, x3, EV, n, left, right,
+                                          _ptr(wgt), C.byref(inc), _ptr(sc))
+    return x3, sc, inc.value
+
+
+def plf_generic(S, Ccat, x1, x2, EV, left, right, wgt=None):
+    """Generic S-state / C-category restatement (protein S=20): unpinned
+    extension; identical to plf() for S=C=4."""
+    dt = x1.dtype
+    V = S * Ccat
+    n = x1.size // V
+    x3 = np.empty(n * V, dtype=dt)
+    sc = np.empty(n, dtype=np.uint8)
+    inc = C.c_longlong(0)
+    if wgt is not None:
+        wgt = np.ascontiguousarray(wgt, dtype=np.int32)
+    getattr(lib(), f"plfo_plf_gen_{_sfx(dt)}")(S, Ccat, x1, x2, x3, EV, n, left, right,
+                                               _ptr(wgt), C.byref(inc), _ptr(sc))
+    return x3, sc, inc.value
+
+
+def ref_plf(x1, x2, EV, left, right, wgt, opt="O0"):
+    """Run the reference plf() (float only).  Returns (x3, scalerIncrement)."""
+    L = ref_lib(opt)
+    if L is None:
+        raise FileNotFoundError("oracle/_ref was not built (no /root/reference here)")
+    n = x1.size // 16
+    x3 = np.zeros(n * 16, dtype=np.float32)
+    inc = L.plfref_plf(x1.copy(), x2.copy(), x3, EV.copy(), n, left.copy(), right.copy(),
+                       np.ascontiguousarray(wgt, dtype=np.int32).copy())
+    return x3, inc
+
+
+def scaler_sum(scaler, wgt=None):
+    return lib().plfo_scaler_sum(np.ascontiguousarray(scaler, dtype=np.uint8),
+                                 _ptr(None if wgt is None else np.ascontiguousarray(wgt, np.int32)),
+                                 scaler.size)
+
+
+def gen_hostmem(n, dtype=np.float32, seed=SEED):
+    """host_mem.cpp:179-209 input protocol with a fixed seed (the reference uses
+    std::random_device; Q8).  Returns dict(EV, left, right, x1, x2, wgt)."""
+    dt = np.dtype(dtype)
+    ev = np.empty(16, dt)
+    left = np.empty(64, dt)
+    right = np.empty(64, dt)
+    x1 = np.empty(16 * n, dt)
+    x2 = np.empty(16 * n, dt)
+    wgt = np.empty(n, np.int32)
+    getattr(lib(), f"plfo_gen_hostmem_{_sfx(dt)}")(seed, n, ev, left, right, x1, x2,
+                                                   _ptr(wgt))
+    return dict(EV=ev, left=left, right=right, x1=x1, x2=x2, wgt=wgt)
+
+
+def mt_draws(seed, count):
+    a = np.empty(count, np.uint32)
+    d = np.empty(count, np.float64)
+    lib().plfo_mt_draws(seed, count, _ptr(a), _ptr(d))
+    return a, d
+
+
+# --------------------------------------------------------------------------
+# testbench_info sizing (include.h:150-266), COMBINED=0 / SEPARATE=1,
+# STREAM=0 / WINDOW=1 as in include.h:20-21.
+# --------------------------------------------------------------------------
+COMBINED, SEPARATE = 0, 1
+STREAM, WINDOW = 0, 1
+
+
+class Testbench:
+    def __init__(self, alignment_sites, parallel_instances=1, window_size=1024,
+                 layout=SEPARATE, aie_type=WINDOW, plf_calls=1):
+        self.alignment_sites = int(alignment_sites)
+        self.parallel_instances = int(parallel_instances)
+        self.window_size = int(window_size)
+        self.input_layout = layout
+        self.aie_type = aie_type
+        self.plf_calls = plf_calls
+        self.elements_per_alignment = 16
+
+    def alignments_per_window(self):
+        return self.window_size >> 4
+
+    def alignments_per_instance(self, k=None):
+        n0 = int(math.ceil(self.alignment_sites / self.parallel_instances))
+        if k is None:
+            return n0
+        return n0 - (k == self.parallel_instances - 1) * self.alignments_padding()
+
+    def alignments_padding(self):
+        return self.alignments_per_instance() * self.parallel_instances - self.alignment_sites
+
+    def alignmentelements_per_instance(self, k):
+        return self.alignments_per_instance(k) * 16
+
+    def num_windows_per_instance(self):
+        apw = self.alignments_per_window()
+        full = self.alignments_per_instance() // apw
+        rem = self.alignments_per_instance() - full * apw
+        return full + (rem > 0)
+
+    def stream_padding(self):
+        return self.alignment_sites & 1
+
+    def elements_per_instance(self):
+        if self.aie_type == STREAM:
+            r = self.alignments_per_instance() + self.stream_padding()
+        else:
+            r = self.num_windows_per_instance() * self.alignments_per_window()
+        return r * 16
+
+    def header_left(self):
+        return 5 * 16
+
+    def header_right(self):
+        return 4 * 16 if self.input_layout == SEPARATE else 5 * 16
+
+    def instance_elements_left(self):
+        return self.elements_per_instance() + self.header_left()
+
+    def instance_elements_right(self):
+        return self.elements_per_instance() + self.header_right()
+
+    def instance_elements_out(self):
+        return self.elements_per_instance()
+
+    def instance_active_elements_left(self, k):
+        return self.alignmentelements_per_instance(k) + self.header_left()
+
+    def instance_active_elements_right(self, k):
+        return self.alignmentelements_per_instance(k) + self.header_right()
+
+    def instance_site_offset(self, k):
+        # host_mem.cpp:229 / :290-291: offsets use instance 0's size
+        return k * self.alignments_per_instance(0)
+
+
+def pack_instance(tb: Testbench, k, EV, left, right, x1, x2, fill=0.0):
+    """Per-instance input buffers of host_mem.cpp:221-243 (whole padded
+    device buffers; the reference leaves the padded tail uninitialised, Q5:
+    here it is `fill`)."""
+    dt = x1.dtype
+    L = np.full(tb.instance_elements_left(), fill, dtype=dt)
+    R = np.full(tb.instance_elements_right(), fill, dtype=dt)
+    off = tb.instance_site_offset(k) * 16
+    cnt = tb.alignmentelements_per_instance(k)
+    L[0:16] = EV
+    L[16:80] = left
+    L[80:80 + cnt] = x1[off:off + cnt]
+    if tb.input_layout == COMBINED:
+        R[0:16] = EV
+        R[16:80] = right
+        R[80:80 + cnt] = x2[off:off + cnt]
+    else:
+        R[0:64] = right
+        R[64:64 + cnt] = x2[off:off + cnt]
+    return L, R
+
+
+def transpose4(word16):
+    """transpose.cpp:6-24: element i*4+j -> j*4+i."""
+    return np.asarray(word16).reshape(4, 4).T.reshape(16).copy()
+
+
+def mm2s_lane_streams(mem, alignment_sites, window_size, side, layout, aie="window"):
+    """Emulate mm2sleft/mm2sright (mem variants): returns a list of 4 lane
+    streams, each an (beats, 4) array of 128-bit beats (4 floats).
+
+    side: "left" | "right"; layout: COMBINED | SEPARATE; aie: "window"|"stream".
+    For SEPARATE the EV and branch matrices go to side streams; they are
+    returned as extra keys in a dict in that case.
+    """
+    mem = np.asarray(mem)
+    words = lambda i: mem[16 * i:16 * i + 16]  # noqa: E731 -- one 512-bit word
+    has_ev = not (side == "right" and layout == SEPARATE)
+    ev = words(0) if has_ev else None
+    pbase = 1 if has_ev else 0
+    branch = [transpose4(words(pbase + c)) for c in range(4)]
+    dbase = pbase + 4
+    lanes = [[] for _ in range(4)]
+    side_ev, side_br = [], [[] for _ in range(4)]
+    ev_rows = None
+    if ev is not None:
+        if side == "left":
+            ev_rows = [ev[0:4], ev[4:8]]          # mm2sleft Comb:34-35
+        else:
+            ev_rows = [ev[8:12], ev[12:16]]       # mm2sright Comb: bottom half
+    if aie == "stream":
+        pad = alignment_sites & 1
+        hdr = np.zeros(4, dtype=np.float32)
+        hdr[0] = np.float32(alignment_sites + pad)
+        for c in range(4):
+            lanes[c].append(hdr)
+            for r in ev_rows:
+                lanes[c].append(r)
+            for j in range(4):
+                lanes[c].append(branch[c][4 * j:4 * j + 4])
+        for i in range(alignment_sites):
+            w = words(dbase + i)
+            for c in range(4):
+                lanes[c].append(w[4 * c:4 * c + 4])
+        if pad:
+            for c in range(4):
+                lanes[c].append(np.zeros(4, dtype=mem.dtype))
+        return [np.array(x) for x in lanes]
+    apw = window_size >> 4
+    nfull = alignment_sites // apw
+    nwin = nfull + (alignment_sites - nfull * apw > 0)
+    for w in range(nwin):
+        if layout == COMBINED:
+            for c in range(4):
+                for r in ev_rows:
+                    lanes[c].append(r)
+                for j in range(4):
+                    lanes[c].append(branch[c][4 * j:4 * j + 4])
+        else:
+            for j in range(4):
+                if ev is not None:
+                    side_ev.append(ev[4 * j:4 * j + 4])
+                for c in range(4):
+                    side_br[c].append(branch[c][4 * j:4 * j + 4])
+        for i in range(apw):
+            wd = words(dbase + apw * w + i)
+            for c in range(4):
+                lanes[c].append(wd[4 * c:4 * c + 4])
+    out = [np.array(x) for x in lanes]
+    if layout == SEPARATE:
+        return dict(data=out, ev=np.array(side_ev) if side_ev else None,
+                    branch=[np.array(b) for b in side_br])
+    return out
+
+
+def s2mm(lane_out, alignment_sites, window_size):
+    """Emulate s2mm (s2mm_memDNAwindowComb.cpp:20-101): 4 lane output streams
+    of (beats,4) -> (CLV words for every padded slot, scaler byte per slot)."""
+    apw = window_size >> 4
+    nfull = alignment_sites // apw
+    nwin = nfull + (alignment_sites - nfull * apw > 0)
+    slots = nwin * apw
+    dt = lane_out[0].dtype
+    mem = np.empty((slots, 16), dtype=dt)
+    sc = np.zeros(slots, dtype=np.uint8)
+    for s in range(slots):
+        x3 = np.concatenate([lane_out[c][s] for c in range(4)]).astype(dt)
+        keep = np.all(np.abs(x3.astype(np.float64)) < MINLIKELIHOOD)
+        if keep and s < alignment_sites:
+            x3 = (x3.astype(np.float64) * TWO_TO_32).astype(dt)
+            sc[s] = 1
+        mem[s] = x3
+    return mem.reshape(-1), sc
+
+
+def aie_lane_compute(data_left, data_right, branch_left, branch_right, ev):
+    """AIE lane arithmetic (mmul_branch x2 -> combine -> ev;
+    aie/src/128x9DNAwindow8192Comb/kernels/{mmul_branch,combine,ev}.cpp):
+    out = ((x . B_L) * (y . B_R)) . EV with B = P^T as streamed.  float64 here
+    (used only as a numpy cross-check of the goldens)."""
+    a = data_left.astype(np.float64) @ branch_left.astype(np.float64)
+    b = data_right.astype(np.float64) @ branch_right.astype(np.float64)
+    return (a * b) @ ev.astype(np.float64)
+
+
+# --------------------------------------------------------------------------
+# AIE golden vectors (aie/data), the reference's own known-answer test.
+# --------------------------------------------------------------------------
+def _read_rows(path):
+    rows = []
+    for line in Path(path).read_text().splitlines():
+        line = line.strip()
+        if line:
+            rows.append([float(t) for t in line.split()])
+    return np.array(rows, dtype=np.float32)
+
+
+def parse_aie_kat(data_dir="/root/reference/aie/data"):
+    """Parse the AIE stimuli + goldens into plf() inputs for one site.
+
+    Returns dict(EV, left, right, x1, x2, golden) (float32), where
+    left[c*16+k*4+l] = B_c[l][k] (inputbranchleft_c holds P_c^T, the matrix the
+    AIE multiplies by) and golden[c*4+l] = golden_c row."""
+    d = Path(data_dir)
+    EV = _read_rows(d / "inputEV0.txt").reshape(16)
+    left = np.empty(64, np.float32)
+    right = np.empty(64, np.float32)
+    x1 = np.empty(16, np.float32)
+    x2 = np.empty(16, np.float32)
+    golden = np.empty(16, np.float32)
+    extras = {}
+    for c in range(4):
+        BL = _read_rows(d / f"inputbranchleft{c}.txt")
+        BR = _read_rows(d / f"inputbranchright{c}.txt")
+        left[c * 16:(c + 1) * 16] = BL.T.reshape(16)
+        right[c * 16:(c + 1) * 16] = BR.T.reshape(16)
+        dl = _read_rows(d / f"inputdataleft{c}.txt")
+        dr = _read_rows(d / f"inputdataright{c}.txt")
+        g = _read_rows(d / f"golden{c}.txt")
+        assert (dl == dl[0]).all() and (dr == dr[0]).all() and (g == g[0]).all()
+        x1[c * 4:(c + 1) * 4] = dl[0]
+        x2[c * 4:(c + 1) * 4] = dr[0]
+        golden[c * 4:(c + 1) * 4] = g[0]
+        extras[f"golden_rows{c}"] = len(g)
+        extras[f"combinedevleft{c}"] = _read_rows(d / f"inputcombinedevleft{c}.txt")
+        extras[f"combinedevright{c}"] = _read_rows(d / f"inputcombinedevright{c}.txt")
+        extras[f"stream_combinedevleft{c}"] = _read_rows(d / "stream" / f"inputcombinedevleft{c}.txt")
+        extras[f"stream_combinedevright{c}"] = _read_rows(d / "stream" / f"inputcombinedevright{c}.txt")
+    return dict(EV=EV, left=left, right=right, x1=x1, x2=x2, golden=golden, **extras)
+
+
+def compare_rel(a, b, scale=None):
+    """max |a-b| / max(|b|) style relative error used by the fp64 tests."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    if scale is None:
+        scale = np.maximum(np.abs(b), np.finfo(np.float64).tiny)
+    return float(np.max(np.abs(a - b) / scale)) if a.size else 0.0
