@@ -1,0 +1,377 @@
+// plf_dna.hpp -- device code of the fused DNA PLF kernel (shared by
+// plf_kernels.hip and the tuning harness tools/tune_plf.hip).
+//
+// Semantics: app/src/plf.cpp:19-65 (+ s2mm scaler byte,
+// hls/src/s2mm_memDNAwindowComb.cpp:70-97, and the weighted scaler sum,
+// app/src/host_mem.cpp:384-388).  See plf_kernels.hip for the mapping.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace plfx {
+namespace dev {
+
+constexpr int kBlock = 256;  // 4 waves
+constexpr int kWavesPerBlock = kBlock / 64;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+template <typename T>
+struct Num;
+template <>
+struct Num<float> {
+  __device__ static constexpr float two32() { return 4294967296.0f; }
+  __device__ static constexpr float minlik() { return 2.3283064365386963e-10f; }  // 2^-32
+  __device__ static inline float abs(float x) { return __builtin_fabsf(x); }
+  template <bool NT>
+  __device__ static inline void load4(const float *p, float (&v)[4]) {
+    f32x4 a;
+    if constexpr (NT) a = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
+    else a = *reinterpret_cast<const f32x4 *>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+  __device__ static inline void store4_nt(float *p, const float (&v)[4]) {
+    f32x4 a = {v[0], v[1], v[2], v[3]};
+    __builtin_nontemporal_store(a, reinterpret_cast<f32x4 *>(p));
+  }
+};
+template <>
+struct Num<double> {
+  __device__ static constexpr double two32() { return 4294967296.0; }
+  __device__ static constexpr double minlik() { return 1.0 / 4294967296.0; }
+  __device__ static inline double abs(double x) { return __builtin_fabs(x); }
+  template <bool NT>
+  __device__ static inline void load4(const double *p, double (&v)[4]) {
+    f64x2 a, b;
+    if constexpr (NT) {
+      a = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(p));
+      b = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(p) + 1);
+    } else {
+      a = reinterpret_cast<const f64x2 *>(p)[0];
+      b = reinterpret_cast<const f64x2 *>(p)[1];
+    }
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+  }
+  __device__ static inline void store4_nt(double *p, const double (&v)[4]) {
+    f64x2 a = {v[0], v[1]};
+    f64x2 b = {v[2], v[3]};
+    __builtin_nontemporal_store(a, reinterpret_cast<f64x2 *>(p));
+    __builtin_nontemporal_store(b, reinterpret_cast<f64x2 *>(p) + 1);
+  }
+};
+
+// Cross-block sum without a memset launch and without a serialised fan-in.
+// Workspace (kWsWords int64, zero at rest, restored to zero by the last
+// arrivals): slot[s] at ws[s*16] (one 128-B line each, s = blockIdx % kSlots)
+// and top at ws[kSlots*16].  Every add carries its own arrival count:
+// word += kTick + partial, so after A arrivals word = A*kTick + sum and the
+// count decodes as round(word / kTick) whenever |any partial sum| < kTick/2.
+// Each block makes ONE returned atomic on its slot; the last arrival of a slot
+// makes ONE returned atomic on top; the last arrival there knows the total.
+// Two dependent round trips instead of a count+sum+acquire chain, and at most
+// ceil(G/kSlots) arrivals serialise on a word (~12 ns each, MI355X_MICROARCH.md
+// row fanin).  Precondition: sum |wgt| < 2^40 (the reference's own
+// scalerIncrement is an int).
+constexpr int kSlots = 32;
+constexpr int kWsWords = (kSlots + 1) * 16;
+constexpr long long kTick = 1ll << 41;
+
+__device__ __forceinline__ long long decode_count(long long word) {
+  return (word + (kTick >> 1)) >> 41;  // floor((word + kTick/2) / kTick)
+}
+
+__device__ inline void block_ticket_sum(long long v, unsigned long long *wsu, int64_t *out) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __shared__ long long part[kWavesPerBlock];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  long long *ws = reinterpret_cast<long long *>(wsu);
+  const long long G = gridDim.x;
+  const long long slot = blockIdx.x % kSlots;
+  const long long nslots = G < kSlots ? G : kSlots;
+  const long long arrivals = (G - slot + kSlots - 1) / kSlots;
+  long long tot = 0;
+#pragma unroll
+  for (int i = 0; i < kWavesPerBlock; i++) tot += part[i];
+  const long long old = __hip_atomic_fetch_add(ws + slot * 16, kTick + tot, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+  if (decode_count(old) != arrivals - 1) return;
+  const long long slot_sum = old + kTick + tot - arrivals * kTick;
+  __hip_atomic_store(ws + slot * 16, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long told = __hip_atomic_fetch_add(ws + kSlots * 16, kTick + slot_sum, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+  if (decode_count(told) != nslots - 1) return;
+  *out = (int64_t)(told + kTick + slot_sum - nslots * kTick);
+  __hip_atomic_store(ws + kSlots * 16, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Swap 64-bit values between adjacent lanes with DPP quad_perm patterns:
+// dpp_even(x) = x of lane (l & ~1), dpp_odd(x) = x of lane (l | 1).
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const long long b = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), kCtrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), kCtrl, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kQuadEven = 0 | (0 << 2) | (2 << 4) | (2 << 6);  // quad_perm [0,0,2,2]
+constexpr int kQuadOdd = 1 | (1 << 2) | (3 << 4) | (3 << 6);   // quad_perm [1,1,3,3]
+
+// One site-category (4 values of x1, 4 of x2) -> 4 values of x3, before the
+// scale test.  plf.cpp:31-50: ump from +0.0 ascending l, product per k, x3 from
+// +0.0 ascending k.
+template <typename T>
+__device__ __forceinline__ void site_cat(const T (&a)[4], const T (&b)[4], const T (&PL)[16],
+                                         const T (&PR)[16], const T (&E)[16], T (&o)[4]) {
+  T p[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    T u1 = T(0), u2 = T(0);
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      u1 += a[l] * PL[k * 4 + l];
+      u2 += b[l] * PR[k * 4 + l];
+    }
+    p[k] = u1 * u2;
+  }
+#pragma unroll
+  for (int l = 0; l < 4; l++) o[l] = T(0);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+#pragma unroll
+    for (int l = 0; l < 4; l++) o[l] += p[k] * E[4 * k + l];
+  }
+}
+
+// Knobs: U = 16-site wave steps per loop trip (bytes in flight per lane =
+// 2*U*4*sizeof(T)); NT = non-temporal CLV loads; kSum = produce the weighted
+// scaler sum; kMinWaves = __launch_bounds__ occupancy hint (waves per SIMD).
+template <typename T, int U, bool kSum, bool NT, int kMinWaves>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
+               const T *__restrict__ EV, const T *__restrict__ left,
+               const T *__restrict__ right, const int32_t *__restrict__ wgt,
+               uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+               int64_t *scaler_sum) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 3;     // Gamma category owned by this lane
+  const int q = lane >> 2;    // site slot within a 16-site wave step
+  const int nib = lane & 60;  // bit offset of this site's nibble in the ballot
+
+  T PL[16], PR[16], E[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    PL[i] = left[c * 16 + i];  // left[c*16 + k*4 + l]
+    PR[i] = right[c * 16 + i];
+    E[i] = EV[i];  // uniform: scalar loads
+  }
+  const T m = Num<T>::minlik();
+
+  long long acc = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  const int64_t nfull = n - (16 * U - 1);  // base < nfull  <=>  whole step in range
+
+  int64_t base = wave * 16 * U;
+  // full steps: no bounds checks, every load of the step issued up front
+  for (; base < nfull; base += stride) {
+    T a[U][4], b[U][4];
+    int w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      Num<T>::template load4<NT>(x1 + site * 16 + c * 4, a[u]);
+      Num<T>::template load4<NT>(x2 + site * 16 + c * 4, b[u]);
+      if (kSum) w[u] = wgt ? wgt[site] : 1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      T o[4];
+      site_cat<T>(a[u], b[u], PL, PR, E, o);
+      const bool small = (Num<T>::abs(o[0]) < m) && (Num<T>::abs(o[1]) < m) &&
+                         (Num<T>::abs(o[2]) < m) && (Num<T>::abs(o[3]) < m);
+      const unsigned long long mask = __ballot(small);
+      const bool sc = ((mask >> nib) & 0xFull) == 0xFull;
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const T s = o[l] * Num<T>::two32();  // exact: power-of-two scaling
+        o[l] = sc ? s : o[l];
+      }
+      Num<T>::store4_nt(x3 + site * 16 + c * 4, o);
+      if (c == 0) {
+        if (scaler) scaler[site] = (uint8_t)sc;
+      }
+      if (kSum) acc += (c == 0 && sc) ? (long long)w[u] : 0ll;
+    }
+  }
+  // tail (at most one partial step per wave)
+  if (base < n) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      const bool valid = site < n;
+      T a[4] = {T(0), T(0), T(0), T(0)}, b[4] = {T(0), T(0), T(0), T(0)};
+      if (valid) {
+        Num<T>::template load4<false>(x1 + site * 16 + c * 4, a);
+        Num<T>::template load4<false>(x2 + site * 16 + c * 4, b);
+      }
+      T o[4];
+      site_cat<T>(a, b, PL, PR, E, o);
+      const bool small = valid && (Num<T>::abs(o[0]) < m) && (Num<T>::abs(o[1]) < m) &&
+                         (Num<T>::abs(o[2]) < m) && (Num<T>::abs(o[3]) < m);
+      const unsigned long long mask = __ballot(small);
+      const bool sc = ((mask >> nib) & 0xFull) == 0xFull;
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const T s = o[l] * Num<T>::two32();
+        o[l] = sc ? s : o[l];
+      }
+      if (valid) {
+        Num<T>::store4_nt(x3 + site * 16 + c * 4, o);
+        if (c == 0) {
+          if (scaler) scaler[site] = (uint8_t)sc;
+          if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+        }
+      }
+    }
+  }
+  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
+// f64 DNA kernel, lane-pair mapping: every wave memory instruction touches one
+// contiguous 1 KiB (lane l <-> bytes 16l..16l+15 of an 8-site block), i.e. lane
+// l holds states {2h, 2h+1} (h = l&1) of category c = (l>>1)&3 of site l>>3.
+// The two lanes of a pair rebuild the category's 4 states with DPP, each
+// computes ump/prod for two of the four k (k = 2h, 2h+1), the pair swaps the
+// products with DPP, and each lane produces its two output states -- every
+// value with exactly plf()'s operation order (ascending l, then ascending k,
+// from +0.0).  Per site: 16 lanes x 16 B per child, 8 lanes per site, the
+// site's 16-value scale test is one byte of the wave ballot.
+template <int U, bool kSum, int kMinWaves>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_f64_pair_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                        double *__restrict__ x3, const double *__restrict__ EV,
+                        const double *__restrict__ left, const double *__restrict__ right,
+                        const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                        unsigned long long *ws, int64_t *scaler_sum) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 1;          // which half of the category's states / k range
+  const int c = (lane >> 1) & 3;   // Gamma category
+  const int g = lane >> 3;         // site within the 8-site block of one instruction
+  const int sh = lane & 56;        // bit offset of this site's byte in the ballot
+
+  double PL[2][4], PR[2][4], E[4][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      PL[kk][l] = left[c * 16 + (2 * h + kk) * 4 + l];
+      PR[kk][l] = right[c * 16 + (2 * h + kk) * 4 + l];
+    }
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int t = 0; t < 2; t++) E[k][t] = EV[4 * k + 2 * h + t];
+  const double m = Num<double>::minlik();
+
+  long long acc = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  const int64_t nfull = n - (16 * U - 1);
+
+  // one 8-site block: loads are done by the caller
+  auto body = [&](const f64x2 a, const f64x2 b, int64_t site0, bool valid, int w) {
+    // rebuild the 4 states of x1_c / x2_c in every lane of the pair
+    const double a0 = dpp_f64<kQuadEven>(a.x), a1 = dpp_f64<kQuadEven>(a.y);
+    const double a2 = dpp_f64<kQuadOdd>(a.x), a3 = dpp_f64<kQuadOdd>(a.y);
+    const double b0 = dpp_f64<kQuadEven>(b.x), b1 = dpp_f64<kQuadEven>(b.y);
+    const double b2 = dpp_f64<kQuadOdd>(b.x), b3 = dpp_f64<kQuadOdd>(b.y);
+    double pm[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+      double u1 = 0.0, u2 = 0.0;
+      u1 += a0 * PL[kk][0]; u1 += a1 * PL[kk][1]; u1 += a2 * PL[kk][2]; u1 += a3 * PL[kk][3];
+      u2 += b0 * PR[kk][0]; u2 += b1 * PR[kk][1]; u2 += b2 * PR[kk][2]; u2 += b3 * PR[kk][3];
+      pm[kk] = u1 * u2;
+    }
+    const double p0 = dpp_f64<kQuadEven>(pm[0]), p1 = dpp_f64<kQuadEven>(pm[1]);
+    const double p2 = dpp_f64<kQuadOdd>(pm[0]), p3 = dpp_f64<kQuadOdd>(pm[1]);
+    double o[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      double x = 0.0;
+      x += p0 * E[0][t]; x += p1 * E[1][t]; x += p2 * E[2][t]; x += p3 * E[3][t];
+      o[t] = x;
+    }
+    const bool small = valid && (__builtin_fabs(o[0]) < m) && (__builtin_fabs(o[1]) < m);
+    const unsigned long long mask = __ballot(small);
+    const bool sc = ((mask >> sh) & 0xFFull) == 0xFFull;
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const double s = o[t] * Num<double>::two32();
+      o[t] = sc ? s : o[t];
+    }
+    if (valid) {
+      f64x2 ov = {o[0], o[1]};
+      __builtin_nontemporal_store(ov, reinterpret_cast<f64x2 *>(x3 + site0 * 16) + lane);
+      if ((lane & 7) == 0) {
+        if (scaler) scaler[site0 + g] = (uint8_t)sc;
+        if (kSum && sc) acc += w;
+      }
+    }
+  };
+
+  int64_t base = wave * 16 * U;
+  for (; base < nfull; base += stride) {
+    f64x2 a[U][2], b[U][2];
+    int w[U][2];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int64_t site0 = base + u * 16 + j * 8;
+        a[u][j] = reinterpret_cast<const f64x2 *>(x1 + site0 * 16)[lane];
+        b[u][j] = reinterpret_cast<const f64x2 *>(x2 + site0 * 16)[lane];
+        if (kSum) w[u][j] = wgt ? wgt[site0 + g] : 1;
+      }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) body(a[u][j], b[u][j], base + u * 16 + j * 8, true, kSum ? w[u][j] : 0);
+  }
+  if (base < n) {  // tail: at most one partial step per wave
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int64_t site0 = base + u * 16 + j * 8;
+        const bool valid = site0 + g < n;
+        f64x2 a = {0.0, 0.0}, b = {0.0, 0.0};
+        int w = 0;
+        if (valid) {
+          a = reinterpret_cast<const f64x2 *>(x1 + site0 * 16)[lane];
+          b = reinterpret_cast<const f64x2 *>(x2 + site0 * 16)[lane];
+          if (kSum) w = wgt ? wgt[site0 + g] : 1;
+        }
+        body(a, b, site0, valid, w);
+      }
+  }
+  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
+__global__ void __launch_bounds__(kBlock)
+scaler_sum_kernel(const uint8_t *__restrict__ scaler, const int32_t *__restrict__ wgt, int64_t n,
+                  unsigned long long *ws, int64_t *out) {
+  long long acc = 0;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n; j += stride)
+    acc += (long long)scaler[j] * (wgt ? (long long)wgt[j] : 1ll);
+  block_ticket_sum(acc, ws, out);
+}
+
+}  // namespace dev
+}  // namespace plfx

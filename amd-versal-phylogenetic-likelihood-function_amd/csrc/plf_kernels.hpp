@@ -5,10 +5,9 @@
 
 namespace plfx {
 
-// Self-resetting workspace for the in-kernel scaler-sum reduction: one 64-bit
-// word, bits [44,64) count the blocks that have arrived, bits [0,44) hold the
-// partial sum.  The last block to arrive writes the total and resets the word.
-constexpr int kTicketShift = 44;
+// Self-resetting workspace of the in-kernel scaler-sum reduction
+// (plf_dna.hpp block_ticket_sum): kWsWords 64-bit words, zero at rest.
+constexpr int kWsWords = (32 + 1) * 16;
 
 struct DnaArgs {
   const void *x1, *x2;

@@ -20,8 +20,8 @@
 struct plfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  int max_blocks = 2048;            // grid cap for the grid-stride kernels
-  unsigned long long *ws = nullptr; // ticket reduction words (2 x u64), zeroed once
+  int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
+  unsigned long long *ws = nullptr; // ticket reduction words (plfx::kWsWords u64), zeroed once
   // grow-only staging for the synchronous host entry points
   void *d_buf = nullptr;
   size_t d_cap = 0;
@@ -169,14 +169,15 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
     delete ctx;
     return PLFX_ERR_HIP;
   }
-  // Grid cap: enough resident 256-thread blocks to fill every CU a few times.
-  ctx->max_blocks = prop.multiProcessorCount * 8;
+  // Grid cap: 0 = as many blocks as are co-resident (occupancy x CUs);
+  // PLFX_MAX_BLOCKS overrides it for experiments.
   if (const char *env = std::getenv("PLFX_MAX_BLOCKS")) {
     int v = std::atoi(env);
     if (v > 0) ctx->max_blocks = v;
   }
-  if (hipMalloc(reinterpret_cast<void **>(&ctx->ws), 2 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemsetAsync(ctx->ws, 0, 2 * sizeof(unsigned long long), ctx->stream) != hipSuccess ||
+  const size_t ws_bytes = plfx::kWsWords * sizeof(unsigned long long);
+  if (hipMalloc(reinterpret_cast<void **>(&ctx->ws), ws_bytes) != hipSuccess ||
+      hipMemsetAsync(ctx->ws, 0, ws_bytes, ctx->stream) != hipSuccess ||
       hipStreamSynchronize(ctx->stream) != hipSuccess) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     (void)hipStreamDestroy(ctx->stream);
