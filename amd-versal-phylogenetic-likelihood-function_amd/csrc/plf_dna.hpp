@@ -251,7 +251,13 @@ plf_dna_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict
 // value with exactly plf()'s operation order (ascending l, then ascending k,
 // from +0.0).  Per site: 16 lanes x 16 B per child, 8 lanes per site, the
 // site's 16-value scale test is one byte of the wave ballot.
-template <int U, bool kSum, int kMinWaves>
+template <bool NT>
+__device__ __forceinline__ f64x2 ld16(const f64x2 *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <int U, bool kSum, int kMinWaves, bool NTL = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_f64_pair_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                         double *__restrict__ x3, const double *__restrict__ EV,
@@ -334,8 +340,8 @@ plf_dna_f64_pair_kernel(const double *__restrict__ x1, const double *__restrict_
 #pragma unroll
       for (int j = 0; j < 2; j++) {
         const int64_t site0 = base + u * 16 + j * 8;
-        a[u][j] = reinterpret_cast<const f64x2 *>(x1 + site0 * 16)[lane];
-        b[u][j] = reinterpret_cast<const f64x2 *>(x2 + site0 * 16)[lane];
+        a[u][j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(x1 + site0 * 16) + lane);
+        b[u][j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
         if (kSum) w[u][j] = wgt ? wgt[site0 + g] : 1;
       }
 #pragma unroll

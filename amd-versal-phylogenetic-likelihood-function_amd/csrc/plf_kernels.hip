@@ -42,10 +42,12 @@ using dev::kWavesPerBlock;
 static_assert(kWsWords == dev::kWsWords, "workspace size mismatch");
 
 // Tuned on MI355X (tools/tune_plf.hip, profiles/r01_tune.log):
-// f64 lane-pair kernel, 2 x 16-site steps per trip, grid = 2 x resident blocks.
+// f64 lane-pair kernel, 2 x 16-site steps per trip, non-temporal CLV loads
+// and stores, grid = resident blocks.
 constexpr int kU64 = 2, kU32 = 4;
-constexpr int kGridMul64 = 2, kGridMul32 = 1;
+constexpr int kGridMul64 = 1, kGridMul32 = 1;
 constexpr bool kNt = false;
+constexpr bool kNtl64 = true;
 constexpr int kMinWaves = 1;
 
 // Co-resident 256-thread blocks of `kernel` on the current device (cached per
@@ -83,7 +85,7 @@ hipError_t launch_dna_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
 template <int U, bool kSum>
 hipError_t launch_pair_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
   static int cache = 0;
-  auto kernel = &dev::plf_dna_f64_pair_kernel<U, kSum, kMinWaves>;
+  auto kernel = &dev::plf_dna_f64_pair_kernel<U, kSum, kMinWaves, kNtl64>;
   const int64_t sites_per_block = (int64_t)kWavesPerBlock * 16 * U;
   int64_t blocks = (a.n + sites_per_block - 1) / sites_per_block;
   const int64_t cap =

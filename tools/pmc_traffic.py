@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 PMC CSVs (FETCH_SIZE pass, WRITE_SIZE pass) into HBM bytes
+per launch of the PLF kernel, corrected as MI355X_MICROARCH.md section HBM
+prescribes: counters are in KiB (x1024); on gfx950 FETCH_SIZE reports exactly
+half of the bytes of a wide (16 B/lane) coalesced streaming read (x2);
+WRITE_SIZE reads 16-B/lane streaming stores exactly.
+
+usage: tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON --sites N --dtype f64
+"""
+import argparse
+import csv
+import json
+import statistics as st
+
+
+def med(path, name, kernel):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if r["Counter_Name"] == name and kernel in r["Kernel_Name"]]
+    if not vals:
+        raise SystemExit(f"no {name} rows for {kernel} in {path}")
+    return st.median(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("out")
+    ap.add_argument("--sites", type=int, default=1 << 20)
+    ap.add_argument("--dtype", default="f64")
+    ap.add_argument("--kernel", default="plf_dna_f64_pair_kernel")
+    a = ap.parse_args()
+    f, nf = med(a.fetch, "FETCH_SIZE", a.kernel)
+    w, nw = med(a.write, "WRITE_SIZE", a.kernel)
+    fetch_b = f * 1024 * 2
+    write_b = w * 1024
+    esz = 8 if a.dtype == "f64" else 4
+    alg_read = a.sites * (2 * 16 * esz + 4)
+    alg_write = a.sites * (16 * esz + 1)
+    rec = {
+        "kernel": a.kernel, "sites": a.sites, "dtype": a.dtype,
+        "dispatches": {"fetch_pass": nf, "write_pass": nw},
+        "FETCH_SIZE_KiB_median": f, "WRITE_SIZE_KiB_median": w,
+        "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
+        "hbm_bytes_per_launch": fetch_b + write_b,
+        "algorithmic_bytes_per_launch": alg_read + alg_write,
+        "traffic_over_algorithmic": (fetch_b + write_b) / (alg_read + alg_write),
+        "correction": "FETCH_SIZE x1024 x2 (gfx950 half-count on 16-B/lane streaming reads), "
+                      "WRITE_SIZE x1024 (MI355X_MICROARCH.md, HBM section)",
+    }
+    json.dump(rec, open(a.out, "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()

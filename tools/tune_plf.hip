@@ -65,6 +65,35 @@ __global__ void __launch_bounds__(256) stream3_sitepattern(const double *__restr
   if (kScaler && acc == 12345678) *out = acc;
 }
 
+// 2R+1W stream, V 16-B vectors per lane per trip, optional nt loads
+template <int V, bool NTL, bool NTS>
+__global__ void __launch_bounds__(256) stream3v(const double *__restrict__ a, const double *__restrict__ b,
+                                                double *__restrict__ c, int64_t n2) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const d2 *A = (const d2 *)a; const d2 *B = (const d2 *)b; d2 *C = (d2 *)c;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * V;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x * V + threadIdx.x; i < n2; i += stride) {
+    d2 x[V], y[V];
+#pragma unroll
+    for (int v = 0; v < V; v++) {
+      if (NTL) { x[v] = __builtin_nontemporal_load(A + i + v * 256); y[v] = __builtin_nontemporal_load(B + i + v * 256); }
+      else { x[v] = A[i + v * 256]; y[v] = B[i + v * 256]; }
+    }
+#pragma unroll
+    for (int v = 0; v < V; v++) {
+      if (NTS) __builtin_nontemporal_store(x[v] + y[v], C + i + v * 256);
+      else C[i + v * 256] = x[v] + y[v];
+    }
+  }
+}
+// 1R+1W copy (the guide's float4-copy calibration point)
+__global__ void __launch_bounds__(256) copy1(const double *__restrict__ a, double *__restrict__ c, int64_t n2) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const d2 *A = (const d2 *)a; d2 *C = (d2 *)c;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += (int64_t)gridDim.x * blockDim.x)
+    C[i] = A[i];
+}
+
 struct Set { double *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
 
 int main(int argc, char **argv) {
@@ -95,6 +124,12 @@ int main(int argc, char **argv) {
   vs.push_back({"stream3 (2R+1W, 384 B/site)", [&](const Set &s) {
     stream3<<<CUs * 8, 256>>>(s.x1, s.x2, s.x3, n * 8); }, {}});
 
+  vs.push_back({"copy 1R+1W (256 B/site) grid 8/CU", [&](const Set &s) {
+    copy1<<<CUs * 8, 256>>>(s.x1, s.x3, n * 8); }, {}});
+#define ADD_S3(V, NTL, NTS, GPC) vs.push_back({"stream3 V=" #V " ntl=" #NTL " nts=" #NTS " grid " #GPC "/CU", [&](const Set &s) { \
+    stream3v<V, NTL, NTS><<<CUs * GPC, 256>>>(s.x1, s.x2, s.x3, n * 8); }, {}});
+  ADD_S3(2, false, true, 8) ADD_S3(1, true, true, 8) ADD_S3(2, true, true, 8) ADD_S3(2, true, true, 4)
+  ADD_S3(4, true, true, 4) ADD_S3(2, true, true, 16)
   vs.push_back({"stream3 site pattern (384 B/site)", [&](const Set &s) {
     stream3_sitepattern<false><<<CUs * 4, 256>>>(s.x1, s.x2, s.x3, s.wgt, s.sc, n, s.sum); }, {}});
   vs.push_back({"stream3 site pattern + scaler byte + wgt", [&](const Set &s) {
@@ -114,24 +149,24 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
                          s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
   }
-#define ADD_PAIR(U, MW, GM, SUM)                                                                   \
+#define ADD_PAIR(U, MW, GM, SUM) ADD_PAIRN(U, MW, GM, SUM, false)
+#define ADD_PAIRN(U, MW, GM, SUM, NTL)                                                             \
   {                                                                                                \
-    auto k = &plf_dna_f64_pair_kernel<U, SUM, MW>;                                                 \
+    auto k = &plf_dna_f64_pair_kernel<U, SUM, MW, NTL>;                                                 \
     int res = occ((const void *)k) * CUs;                                                          \
     int64_t need = (n + 64 * U - 1) / (64 * U);                                                    \
     int64_t grid = GM > 0 ? std::min<int64_t>(need, (int64_t)res * GM) : need;                     \
-    char nm[160]; snprintf(nm, sizeof nm, "pair U=%d minw=%d sum=%d occ=%d/CU grid=%lld%s", U, MW, SUM, \
+    char nm[160]; snprintf(nm, sizeof nm, "pair U=%d minw=%d sum=%d ntl=%d occ=%d/CU grid=%lld%s", U, MW, SUM, NTL, \
                            occ((const void *)k), (long long)grid, GM > 0 ? "" : " (uncapped)");   \
     vs.push_back({nm, [=](const Set &s) {                                                          \
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
                          s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
   }
-  ADD_PAIR(1, 1, 1, true) ADD_PAIR(1, 1, 2, true) ADD_PAIR(1, 1, 0, true) ADD_PAIR(1, 1, 1, false)
-  ADD_PAIR(2, 1, 1, true) ADD_PAIR(2, 1, 2, true) ADD_PAIR(2, 1, 1, false)
-  ADD_PAIR(4, 1, 1, true) ADD_PAIR(4, 1, 0, true)
-  ADD_PLF(1, false, 1, 1) ADD_PLFS(1, false, 1, 1, false) ADD_PLF(1, false, 1, 0)
-  ADD_PLF(2, false, 1, 1) ADD_PLFS(2, false, 1, 1, false)
-  ADD_PLF(4, false, 1, 1) ADD_PLFS(4, false, 1, 1, false)
+  ADD_PAIR(2, 1, 2, true) ADD_PAIR(2, 1, 2, false)
+  ADD_PAIRN(1, 1, 1, true, true) ADD_PAIRN(1, 1, 2, true, true) ADD_PAIRN(1, 1, 4, true, true)
+  ADD_PAIRN(2, 1, 1, true, true) ADD_PAIRN(2, 1, 2, true, true) ADD_PAIRN(2, 1, 4, true, true)
+  ADD_PAIRN(2, 1, 2, false, true) ADD_PAIRN(4, 1, 1, true, true) ADD_PAIRN(4, 1, 2, true, true)
+
 
   for (int round = 0; round < rounds; round++) {
     for (auto &v : vs) {
@@ -149,7 +184,7 @@ int main(int argc, char **argv) {
          rounds, R, n * 389.0 / 1048576);
   for (auto &v : vs) {
     std::sort(v.us.begin(), v.us.end());
-    const double bytes = ((v.name.rfind("stream3", 0) == 0 && v.name.find("wgt") == std::string::npos) ? 384.0 : 389.0) * n;
+    const double bytes = (v.name.rfind("copy", 0) == 0 ? 256.0 : (v.name.rfind("stream3", 0) == 0 && v.name.find("wgt") == std::string::npos) ? 384.0 : 389.0) * n;
     printf("%-62s median %8.2f us  min %8.2f us  %7.0f GB/s  %5.1f%% of 8 TB/s  %6.2f Gsites/s\n",
            v.name.c_str(), v.us[v.us.size() / 2], v.us[0], bytes / (v.us[v.us.size() / 2] * 1e-6) / 1e9,
            100.0 * bytes / (v.us[v.us.size() / 2] * 1e-6) / 8e12, n / (v.us[v.us.size() / 2] * 1e-6) / 1e9);
