@@ -45,6 +45,22 @@ def bytes_per_site(dtype_bytes):
     return 3 * 16 * dtype_bytes + 1 + 4
 
 
+def combine_ranks(wall_ms, dev_ms, got_sum, expect_sum, device, world):
+    """Cross-rank reduction of one bench run: MAX of the timed-region wall and
+    device times (the driver contract) and ONE all-reduce (RCCL on GPUs, gloo in
+    the CPU tests) of the scaler totals.  Returns (wall_ms, dev_ms, check_ok)."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([wall_ms, dev_ms], dtype=torch.float64, device=device)
+    tot = torch.stack([got_sum.to(device=device, dtype=torch.int64).reshape(()),
+                       torch.tensor(expect_sum, dtype=torch.int64, device=device)])
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    return float(t[0]), float(t[1]), int(tot[0]) == int(tot[1])
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -193,16 +209,10 @@ def main():
     dev_ms = e0.elapsed_time(e1)
 
     # correctness spot check: every buffer set's last scaler total is n/4
-    # (every 4th site underflows and wgt = 1)
+    # (every 4th site underflows and wgt = 1); max-over-ranks timing
     expect = (n + 3) // 4
     got = torch.stack([b["s"][0] for b in sets]).sum()
-    tot = torch.stack([got, torch.tensor(expect * R, device=dev, dtype=torch.int64)])
-    t = torch.tensor([wall_ms, dev_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)      # max over ranks
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)    # one RCCL all-reduce of scaler totals
-    wall_ms, dev_ms = float(t[0]), float(t[1])
-    check_ok = int(tot[0]) == int(tot[1])
+    wall_ms, dev_ms, check_ok = combine_ranks(wall_ms, dev_ms, got, expect * R, dev, world)
 
     if rank == 0:
         per_launch_ms = dev_ms / a.steps

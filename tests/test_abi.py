@@ -98,3 +98,18 @@ def test_pack_instance_matches_oracle(oracle, dtype, layout, P, W):
         L, R = t.pack_instance(k, d["EV"], d["left"], d["right"], d["x1"], d["x2"])
         oL, oR = oracle.pack_instance(o, k, d["EV"], d["left"], d["right"], d["x1"], d["x2"])
         assert np.array_equal(L, oL) and np.array_equal(R, oR)
+
+
+def build_dropin(tmp_dir):
+    exe = Path(tmp_dir) / "dropin_main"
+    src = ROOT / "tests" / "dropin_main.cpp"
+    r = subprocess.run(["g++", "-O1", "-std=c++17", f"-I{ROOT / 'include'}", str(src), "-o", str(exe),
+                        f"-L{PKG / 'plfx'}", "-lplfx", f"-Wl,-rpath,{PKG / 'plfx'}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_dropin_header_compiles(tmp_path):
+    """include/plfx_plf.hpp provides plf() with the reference's signature."""
+    assert build_dropin(tmp_path).exists()

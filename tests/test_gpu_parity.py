@@ -268,3 +268,27 @@ def test_host_driver_end_to_end(oracle, tmp_path):
             assert np.array_equal(bits(got), bits(e3))
             assert np.array_equal(sc, esc) and inc == einc
         assert "GPU PLF kernel" in r.stdout
+
+
+def test_dropin_header_reference_call(tmp_path):
+    """A C++ call site written exactly like host_mem.cpp:418, compiled against
+    include/plfx_plf.hpp, reproduces the reference fixture bit for bit."""
+    from test_abi import build_dropin
+
+    g = golden("hostmem_f32_n1000.npz")
+    n = 1000
+    inp = tmp_path / "in.bin"
+    with open(inp, "wb") as f:
+        f.write(np.int32(n).tobytes())
+        for k in ("EV", "left", "right", "x1", "x2"):
+            f.write(np.ascontiguousarray(g[k], np.float32).tobytes())
+        f.write(np.ascontiguousarray(g["wgt"], np.int32).tobytes())
+    exe = build_dropin(tmp_path)
+    out = tmp_path / "out.bin"
+    r = subprocess.run([str(exe), str(inp), str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    raw = np.fromfile(out, dtype=np.uint8)
+    x3 = raw[:64 * n].view(np.float32)
+    inc = int(raw[64 * n:].view(np.int32)[0])
+    assert np.array_equal(bits(x3), bits(g["x3"]))
+    assert inc == int(g["scalerIncrement"])
