@@ -104,7 +104,7 @@ __device__ inline void block_ticket_sum(long long v, unsigned long long *wsu, in
   const long long told = __hip_atomic_fetch_add(ws + kSlots * 16, kTick + slot_sum, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
   if (decode_count(told) != nslots - 1) return;
-  *out = (int64_t)(told + kTick + slot_sum - nslots * kTick);
+  if (out) *out = (int64_t)(told + kTick + slot_sum - nslots * kTick);
   __hip_atomic_store(ws + kSlots * 16, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -149,13 +149,13 @@ __device__ __forceinline__ void site_cat(const T (&a)[4], const T (&b)[4], const
 // Knobs: U = 16-site wave steps per loop trip (bytes in flight per lane =
 // 2*U*4*sizeof(T)); NT = non-temporal CLV loads; kSum = produce the weighted
 // scaler sum; kMinWaves = __launch_bounds__ occupancy hint (waves per SIMD).
-template <typename T, int U, bool kSum, bool NT, int kMinWaves>
-__global__ void __launch_bounds__(kBlock, kMinWaves)
-plf_dna_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
-               const T *__restrict__ EV, const T *__restrict__ left,
-               const T *__restrict__ right, const int32_t *__restrict__ wgt,
-               uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
-               int64_t *scaler_sum) {
+template <typename T, int U, bool kSum, bool NT>
+__device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *__restrict__ x2,
+                                             T *__restrict__ x3, const T *__restrict__ EV,
+                                             const T *__restrict__ left, const T *__restrict__ right,
+                                             const int32_t *__restrict__ wgt,
+                                             uint8_t *__restrict__ scaler, int64_t n,
+                                             unsigned long long *ws, int64_t *scaler_sum) {
   const int lane = threadIdx.x & 63;
   const int c = lane & 3;     // Gamma category owned by this lane
   const int q = lane >> 2;    // site slot within a 16-site wave step
@@ -242,6 +242,16 @@ plf_dna_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
 
+template <typename T, int U, bool kSum, bool NT, int kMinWaves>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
+               const T *__restrict__ EV, const T *__restrict__ left,
+               const T *__restrict__ right, const int32_t *__restrict__ wgt,
+               uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+               int64_t *scaler_sum) {
+  dna_cat_body<T, U, kSum, NT>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum);
+}
+
 // f64 DNA kernel, lane-pair mapping: every wave memory instruction touches one
 // contiguous 1 KiB (lane l <-> bytes 16l..16l+15 of an 8-site block), i.e. lane
 // l holds states {2h, 2h+1} (h = l&1) of category c = (l>>1)&3 of site l>>3.
@@ -257,13 +267,16 @@ __device__ __forceinline__ f64x2 ld16(const f64x2 *p) {
   else return *p;
 }
 
-template <int U, bool kSum, int kMinWaves, bool NTL = false>
-__global__ void __launch_bounds__(kBlock, kMinWaves)
-plf_dna_f64_pair_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
-                        double *__restrict__ x3, const double *__restrict__ EV,
-                        const double *__restrict__ left, const double *__restrict__ right,
-                        const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                        unsigned long long *ws, int64_t *scaler_sum) {
+template <int U, bool kSum, bool NTL>
+__device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
+                                              const double *__restrict__ x2,
+                                              double *__restrict__ x3,
+                                              const double *__restrict__ EV,
+                                              const double *__restrict__ left,
+                                              const double *__restrict__ right,
+                                              const int32_t *__restrict__ wgt,
+                                              uint8_t *__restrict__ scaler, int64_t n,
+                                              unsigned long long *ws, int64_t *scaler_sum) {
   const int lane = threadIdx.x & 63;
   const int h = lane & 1;          // which half of the category's states / k range
   const int c = (lane >> 1) & 3;   // Gamma category
@@ -367,6 +380,54 @@ plf_dna_f64_pair_kernel(const double *__restrict__ x1, const double *__restrict_
       }
   }
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
+template <int U, bool kSum, int kMinWaves, bool NTL = false>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_f64_pair_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                        double *__restrict__ x3, const double *__restrict__ EV,
+                        const double *__restrict__ left, const double *__restrict__ right,
+                        const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                        unsigned long long *ws, int64_t *scaler_sum) {
+  dna_pair_body<U, kSum, NTL>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum);
+}
+
+// Batched inner-node updates: one launch evaluates gridDim.y <= kMaxBatch
+// independent nodes (a tree level, or a shard of independent nodes) that share
+// EV, n and wgt; node = blockIdx.y.  The descriptors travel by value in the
+// kernel arguments (no staging copy, graph-capture safe) and are read through
+// the scalar cache.  Each node has its own kWsWords of scaler-sum workspace.
+struct NodeDesc {
+  const void *x1, *x2;
+  void *x3;
+  const void *left, *right;
+  uint8_t *scaler;      // may be null
+  int64_t *scaler_sum;  // may be null
+};
+constexpr int kMaxBatch = 32;
+struct NodeBatch {
+  NodeDesc d[kMaxBatch];
+};
+
+template <int U, bool kSum, int kMinWaves, bool NTL = false>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_f64_pair_batch_kernel(const NodeBatch nodes, const double *__restrict__ EV,
+                              const int32_t *__restrict__ wgt, int64_t n,
+                              unsigned long long *ws) {
+  const NodeDesc &d = nodes.d[blockIdx.y];
+  dna_pair_body<U, kSum, NTL>((const double *)d.x1, (const double *)d.x2, (double *)d.x3, EV,
+                              (const double *)d.left, (const double *)d.right, wgt, d.scaler, n,
+                              ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum);
+}
+
+template <typename T, int U, bool kSum, bool NT, int kMinWaves>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_batch_kernel(const NodeBatch nodes, const T *__restrict__ EV,
+                     const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
+  const NodeDesc &d = nodes.d[blockIdx.y];
+  dna_cat_body<T, U, kSum, NT>((const T *)d.x1, (const T *)d.x2, (T *)d.x3, EV, (const T *)d.left,
+                               (const T *)d.right, wgt, d.scaler, n,
+                               ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum);
 }
 
 __global__ void __launch_bounds__(kBlock)

@@ -1,4 +1,4 @@
-// plf_kernels.hip -- fused PLF inner-node update for CDNA4 (gfx950).
+// plf_kernels.hip -- launchers of the fused PLF kernels for CDNA4 (gfx950).
 //
 // One kernel replaces the reference's whole accelerator pipeline for one PLF
 // call: the PL input movers (hls/src/mm2sleft_memDNAwindowComb.cpp:16-100,
@@ -7,32 +7,19 @@
 // output mover with the underflow test/rescale and the char scaler
 // (hls/src/s2mm_memDNAwindowComb.cpp:45-99), plus the host's weighted scaler
 // reduction (app/src/host_mem.cpp:384-388).  Arithmetic follows the CPU
-// definition plf() (app/src/plf.cpp:19-65) operation for operation.
+// definition plf() (app/src/plf.cpp:19-65) operation for operation.  The
+// device code and its mapping are documented in plf_dna.hpp / DESIGN.md.
 //
-// Mapping (DNA, S=4 states, C=4 Gamma categories, V=16 values per site):
-//   * 4 consecutive lanes own one site, lane c = category c (the reference's
-//     4 AIE lanes, aie/src/128x9DNAwindow8192Comb/graph.h:34-46); a wave covers
-//     16 sites per step and issues U steps of loads before computing.
-//   * lane c streams its 4 states of x1 and x2 with 16-byte loads (the 4 lanes
-//     of a site read one contiguous 64/128-byte site record, the wave one
-//     contiguous 1/2 KiB block) and writes its 4 results with non-temporal
-//     16-byte stores.
-//   * P_L[c], P_R[c] (16 values each) live in VGPRs for the whole grid-stride
-//     loop; EV is wave-uniform and sits in SGPRs (scalar loads).
-//   * per-site scale test: each lane tests its 4 values, a wave ballot gives a
-//     64-bit mask, and the site's nibble == 0xF decides; the rescale is a
-//     select (no divergent branch).  Lane c==0 writes the site's scaler byte
-//     and accumulates wgt into a register; one 64-bit atomic per block feeds a
-//     self-resetting ticket reduction, so no memset launch is needed per call.
-//   * no FMA contraction (-ffp-contract=off) and the reference's ascending
-//     accumulation order from +0.0: bit-exact against plf() in f32 and against
-//     its double instantiation in f64.
-//   * grid = resident blocks (occupancy x CUs) x kGridWaves, grid-stride loop.
+// Grids: grid-stride kernels launch at most the co-resident block count
+// (occupancy x CUs) times a tuned multiplier; batched launches spread those
+// blocks over the batch's nodes (blockIdx.y = node).
 #include <hip/hip_runtime.h>
+
 #include <cstdint>
 
 #include "plf_dna.hpp"
 #include "plf_kernels.hpp"
+#include "plf_lnl.hpp"
 
 namespace plfx {
 namespace {
@@ -40,6 +27,8 @@ namespace {
 using dev::kBlock;
 using dev::kWavesPerBlock;
 static_assert(kWsWords == dev::kWsWords, "workspace size mismatch");
+static_assert(kMaxBatch == dev::kMaxBatch, "batch size mismatch");
+static_assert(sizeof(NodeDescH) == sizeof(dev::NodeDesc), "node descriptor mismatch");
 
 // Tuned on MI355X (tools/tune_plf.hip, profiles/r01_tune.log):
 // f64 lane-pair kernel, 2 x 16-site steps per trip, non-temporal CLV loads
@@ -51,7 +40,7 @@ constexpr bool kNtl64 = true;
 constexpr int kMinWaves = 1;
 
 // Co-resident 256-thread blocks of `kernel` on the current device (cached per
-// kernel; the grid-stride kernels launch at most this many).
+// kernel instantiation by the caller).
 int resident_blocks(const void *kernel, int &cache) {
   if (!cache) {
     int dev = 0, per_cu = 0;
@@ -66,48 +55,126 @@ int resident_blocks(const void *kernel, int &cache) {
   return cache;
 }
 
-template <typename T, int U, bool kSum>
-hipError_t launch_dna_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  static int cache = 0;
-  auto kernel = &dev::plf_dna_kernel<T, U, kSum, kNt, kMinWaves>;
-  const int64_t sites_per_block = (int64_t)kWavesPerBlock * 16 * U;
-  int64_t blocks = (a.n + sites_per_block - 1) / sites_per_block;
-  const int64_t cap =
-      max_blocks > 0 ? max_blocks : (int64_t)kGridMul32 * resident_blocks((const void *)kernel, cache);
+// blocks along x for `count` nodes of n sites each
+int64_t grid_x(const void *kernel, int &cache, int grid_mul, int64_t n, int sites_per_block,
+               int count, int max_blocks) {
+  int64_t blocks = (n + sites_per_block - 1) / sites_per_block;
+  const int64_t resident = (int64_t)grid_mul * resident_blocks(kernel, cache);
+  const int64_t cap = max_blocks > 0 ? max_blocks : (resident + count - 1) / count;
   if (blocks > cap) blocks = cap;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const T *)a.x1,
+  return blocks < 1 ? 1 : blocks;
+}
+
+template <typename T, bool kSum>
+hipError_t launch_cat(const DnaArgs &a, int max_blocks, hipStream_t s) {
+  static int cache = 0;
+  auto kernel = &dev::plf_dna_kernel<T, kU32, kSum, kNt, kMinWaves>;
+  const int64_t gx = grid_x((const void *)kernel, cache, kGridMul32, a.n, kWavesPerBlock * 16 * kU32,
+                            1, max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
                      (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,
                      (const T *)a.right, a.wgt, a.scaler, a.n, a.ws, a.scaler_sum);
   return hipGetLastError();
 }
 
-template <int U, bool kSum>
-hipError_t launch_pair_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
+template <bool kSum>
+hipError_t launch_pair(const DnaArgs &a, int max_blocks, hipStream_t s) {
   static int cache = 0;
-  auto kernel = &dev::plf_dna_f64_pair_kernel<U, kSum, kMinWaves, kNtl64>;
-  const int64_t sites_per_block = (int64_t)kWavesPerBlock * 16 * U;
-  int64_t blocks = (a.n + sites_per_block - 1) / sites_per_block;
-  const int64_t cap =
-      max_blocks > 0 ? max_blocks : (int64_t)kGridMul64 * resident_blocks((const void *)kernel, cache);
-  if (blocks > cap) blocks = cap;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const double *)a.x1,
+  auto kernel = &dev::plf_dna_f64_pair_kernel<kU64, kSum, kMinWaves, kNtl64>;
+  const int64_t gx = grid_x((const void *)kernel, cache, kGridMul64, a.n, kWavesPerBlock * 16 * kU64,
+                            1, max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV,
                      (const double *)a.left, (const double *)a.right, a.wgt, a.scaler, a.n, a.ws,
                      a.scaler_sum);
   return hipGetLastError();
 }
 
+template <bool kSum>
+hipError_t launch_pair_batch(const dev::NodeBatch &b, int count, const double *EV,
+                             const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                             hipStream_t s) {
+  static int cache = 0;
+  auto kernel = &dev::plf_dna_f64_pair_batch_kernel<kU64, kSum, kMinWaves, kNtl64>;
+  const int64_t gx = grid_x((const void *)kernel, cache, kGridMul64, n, kWavesPerBlock * 16 * kU64,
+                            count, max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt, n,
+                     ws);
+  return hipGetLastError();
+}
+
+template <typename T, bool kSum>
+hipError_t launch_cat_batch(const dev::NodeBatch &b, int count, const T *EV, const int32_t *wgt,
+                            int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s) {
+  static int cache = 0;
+  auto kernel = &dev::plf_dna_batch_kernel<T, kU32, kSum, kNt, kMinWaves>;
+  const int64_t gx = grid_x((const void *)kernel, cache, kGridMul32, n, kWavesPerBlock * 16 * kU32,
+                            count, max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt, n,
+                     ws);
+  return hipGetLastError();
+}
+
+template <typename T, int S, int C>
+hipError_t launch_lnl_t(const T *x, int64_t n, const double *catw, const double *freq,
+                        const int32_t *wgt, const int64_t *sums, int nsums, double *partials,
+                        unsigned long long *ticket, double *out, double *site_lnl, hipStream_t s) {
+  static int cache = 0;
+  auto kernel = &dev::root_lnl_kernel<T, S, C>;
+  int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * (64 / C), 1, 0);
+  if (gx > kLnlMaxGrid) gx = kLnlMaxGrid;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, x, n, catw, freq, wgt, sums,
+                     nsums, partials, ticket, out, site_lnl);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_plf_dna_f32(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  return a.scaler_sum ? launch_dna_t<float, kU32, true>(a, max_blocks, s)
-                      : launch_dna_t<float, kU32, false>(a, max_blocks, s);
+  return a.scaler_sum ? launch_cat<float, true>(a, max_blocks, s)
+                      : launch_cat<float, false>(a, max_blocks, s);
 }
+
 hipError_t launch_plf_dna_f64(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  return a.scaler_sum ? launch_pair_t<kU64, true>(a, max_blocks, s)
-                      : launch_pair_t<kU64, false>(a, max_blocks, s);
+  return a.scaler_sum ? launch_pair<true>(a, max_blocks, s) : launch_pair<false>(a, max_blocks, s);
+}
+
+hipError_t launch_plf_dna_batch(int dtype, const NodeDescH *nodes, int count, const void *EV,
+                                const int32_t *wgt, int64_t n, unsigned long long *ws,
+                                int max_blocks, hipStream_t s) {
+  if (count < 1 || count > kMaxBatch) return hipErrorInvalidValue;
+  dev::NodeBatch b{};
+  bool any_sum = false;
+  for (int i = 0; i < count; i++) {
+    b.d[i] = dev::NodeDesc{nodes[i].x1, nodes[i].x2, nodes[i].x3, nodes[i].left, nodes[i].right,
+                           nodes[i].scaler, nodes[i].scaler_sum};
+    any_sum |= nodes[i].scaler_sum != nullptr;
+  }
+  if (dtype == 1)
+    return any_sum ? launch_pair_batch<true>(b, count, (const double *)EV, wgt, n, ws, max_blocks, s)
+                   : launch_pair_batch<false>(b, count, (const double *)EV, wgt, n, ws, max_blocks, s);
+  return any_sum
+             ? launch_cat_batch<float, true>(b, count, (const float *)EV, wgt, n, ws, max_blocks, s)
+             : launch_cat_batch<float, false>(b, count, (const float *)EV, wgt, n, ws, max_blocks, s);
+}
+
+hipError_t launch_root_lnl(int dtype, int states, const void *x, int64_t n, const double *catw,
+                           const double *freq, const int32_t *wgt, const int64_t *scaler_sums,
+                           int nsums, double *partials, unsigned long long *ticket, double *out,
+                           double *site_lnl, hipStream_t s) {
+  if (states == 4 && dtype == 1)
+    return launch_lnl_t<double, 4, 4>((const double *)x, n, catw, freq, wgt, scaler_sums, nsums,
+                                      partials, ticket, out, site_lnl, s);
+  if (states == 4 && dtype == 0)
+    return launch_lnl_t<float, 4, 4>((const float *)x, n, catw, freq, wgt, scaler_sums, nsums,
+                                     partials, ticket, out, site_lnl, s);
+  if (states == 20 && dtype == 1)
+    return launch_lnl_t<double, 20, 4>((const double *)x, n, catw, freq, wgt, scaler_sums, nsums,
+                                       partials, ticket, out, site_lnl, s);
+  if (states == 20 && dtype == 0)
+    return launch_lnl_t<float, 20, 4>((const float *)x, n, catw, freq, wgt, scaler_sums, nsums,
+                                      partials, ticket, out, site_lnl, s);
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_scaler_sum(const uint8_t *scaler, const int32_t *wgt, int64_t n, int64_t *out,

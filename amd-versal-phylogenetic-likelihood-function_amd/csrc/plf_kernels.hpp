@@ -26,6 +26,26 @@ hipError_t launch_plf_dna_f32(const DnaArgs &a, int max_blocks, hipStream_t s);
 hipError_t launch_plf_dna_f64(const DnaArgs &a, int max_blocks, hipStream_t s);
 
 // sum_j scaler[j]*wgt[j] (host_mem.cpp:384-388), self-resetting ws as above.
+// Batched nodes (<= kMaxBatch per launch) sharing EV, n, wgt.  dtype: 0 f32, 1 f64.
+struct NodeDescH {
+  const void *x1, *x2;
+  void *x3;
+  const void *left, *right;
+  uint8_t *scaler;
+  int64_t *scaler_sum;
+};
+constexpr int kMaxBatch = 32;
+hipError_t launch_plf_dna_batch(int dtype, const NodeDescH *nodes, int count, const void *EV,
+                                const int32_t *wgt, int64_t n, unsigned long long *ws,
+                                int max_blocks, hipStream_t s);
+
+// Root log-likelihood; partials: >= kLnlMaxGrid doubles; ticket: 1 u64 (zero at rest).
+constexpr int kLnlMaxGrid = 4096;
+hipError_t launch_root_lnl(int dtype, int states, const void *x, int64_t n, const double *catw,
+                           const double *freq, const int32_t *wgt, const int64_t *scaler_sums,
+                           int nsums, double *partials, unsigned long long *ticket, double *out,
+                           double *site_lnl, hipStream_t s);
+
 hipError_t launch_scaler_sum(const uint8_t *scaler, const int32_t *wgt, int64_t n,
                              int64_t *out, unsigned long long *ws, int max_blocks,
                              hipStream_t s);

@@ -10,8 +10,10 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/plfx.h"
 #include "plf_kernels.hpp"
@@ -21,7 +23,9 @@ struct plfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
-  unsigned long long *ws = nullptr; // ticket reduction words (plfx::kWsWords u64), zeroed once
+  unsigned long long *ws = nullptr; // ticket reduction words (kMaxBatch x kWsWords u64), zero at rest
+  double *lnl_partials = nullptr;   // kLnlMaxGrid doubles
+  unsigned long long *lnl_ticket = nullptr;
   // grow-only staging for the synchronous host entry points
   void *d_buf = nullptr;
   size_t d_cap = 0;
@@ -175,11 +179,16 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
     int v = std::atoi(env);
     if (v > 0) ctx->max_blocks = v;
   }
-  const size_t ws_bytes = plfx::kWsWords * sizeof(unsigned long long);
+  const size_t ws_bytes = (size_t)plfx::kMaxBatch * plfx::kWsWords * sizeof(unsigned long long);
   if (hipMalloc(reinterpret_cast<void **>(&ctx->ws), ws_bytes) != hipSuccess ||
       hipMemsetAsync(ctx->ws, 0, ws_bytes, ctx->stream) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void **>(&ctx->lnl_partials), plfx::kLnlMaxGrid * sizeof(double)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void **>(&ctx->lnl_ticket), sizeof(unsigned long long)) != hipSuccess ||
+      hipMemsetAsync(ctx->lnl_ticket, 0, sizeof(unsigned long long), ctx->stream) != hipSuccess ||
       hipStreamSynchronize(ctx->stream) != hipSuccess) {
     if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->lnl_partials) (void)hipFree(ctx->lnl_partials);
+    if (ctx->lnl_ticket) (void)hipFree(ctx->lnl_ticket);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return PLFX_ERR_HIP;
@@ -194,6 +203,8 @@ int plfx_ctx_destroy(plfx_ctx *ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->d_buf) (void)hipFree(ctx->d_buf);
   if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->lnl_partials) (void)hipFree(ctx->lnl_partials);
+  if (ctx->lnl_ticket) (void)hipFree(ctx->lnl_ticket);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return PLFX_OK;
@@ -261,6 +272,103 @@ int plfx_instance_run(plfx_ctx *ctx, const void *in_left, const void *in_right, 
   return plf_dev<double>(ctx, (const double *)x1, (const double *)x2, (double *)out_clv,
                          (const double *)EV, alignment_sites, (const double *)left,
                          (const double *)right, nullptr, out_scaler, nullptr, stream);
+}
+
+int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *nodes, int count,
+                       const void *EV, int64_t n, const int32_t *wgt, void *stream) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if (states != 4) return fail(ctx, PLFX_ERR_UNSUPPORTED, "batched nodes: states=%d not built", states);
+  if (count < 0 || n < 0 || (count > 0 && (!nodes || !EV)))
+    return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
+  hipStream_t s = pick(ctx, stream);
+  for (int i = 0; i < count; i++) {
+    int rc = check_dev_args(ctx, nodes[i].x1, nodes[i].x2, nodes[i].x3, EV, n, nodes[i].left,
+                            nodes[i].right);
+    if (rc != PLFX_OK) return rc;
+    if (n == 0 && nodes[i].scaler_sum)
+      PLFX_HIP(ctx, hipMemsetAsync(nodes[i].scaler_sum, 0, sizeof(int64_t), s));
+  }
+  if (n == 0) return PLFX_OK;
+  for (int i = 0; i < count; i += plfx::kMaxBatch) {
+    const int c = std::min(plfx::kMaxBatch, count - i);
+    hipError_t e = plfx::launch_plf_dna_batch(
+        dtype, reinterpret_cast<const plfx::NodeDescH *>(nodes + i), c, EV, wgt, n, ctx->ws,
+        ctx->max_blocks, s);
+    if (e != hipSuccess) return hip_fail(ctx, e, "plf batch launch");
+  }
+  return PLFX_OK;
+}
+
+int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
+                  void *const *clv, int nslots, const void *pmats, int npmats, const void *EV,
+                  int64_t n, const int32_t *wgt, uint8_t *const *scalers, int64_t *scaler_sums,
+                  void *stream) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (states != 4) return fail(ctx, PLFX_ERR_UNSUPPORTED, "traverse: states=%d not built", states);
+  if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if (nops < 0 || (nops > 0 && (!ops || !clv || !pmats || !EV)))
+    return fail(ctx, PLFX_ERR_INVALID, "bad traverse arguments");
+  const size_t es = dtype == PLFX_F32 ? 4 : 8;
+  const size_t mat = (size_t)states * states * 4;  // C*S*S values per matrix
+  // dependency levels: RAW on children, WAR/WAW on the parent slot
+  std::vector<int> level(nops, 0), slot_write(nslots, -1), slot_read(nslots, -1);
+  int nlev = 0;
+  for (int j = 0; j < nops; j++) {
+    const plfx_trav_op &o = ops[j];
+    if (o.parent < 0 || o.parent >= nslots || o.child1 < 0 || o.child1 >= nslots || o.child2 < 0 ||
+        o.child2 >= nslots || o.pmat < 0 || o.pmat >= npmats)
+      return fail(ctx, PLFX_ERR_INVALID, "op %d: slot/pmat index out of range", j);
+    if (o.parent == o.child1 || o.parent == o.child2)
+      return fail(ctx, PLFX_ERR_INVALID, "op %d: parent slot aliases a child", j);
+    int lv = 0;
+    for (int sl : {o.child1, o.child2})
+      if (slot_write[sl] >= 0) lv = std::max(lv, slot_write[sl] + 1);
+    if (slot_write[o.parent] >= 0) lv = std::max(lv, slot_write[o.parent] + 1);
+    if (slot_read[o.parent] >= 0) lv = std::max(lv, slot_read[o.parent] + 1);
+    level[j] = lv;
+    slot_write[o.parent] = lv;
+    for (int sl : {o.child1, o.child2}) slot_read[sl] = std::max(slot_read[sl], lv);
+    nlev = std::max(nlev, lv + 1);
+  }
+  hipStream_t s = pick(ctx, stream);
+  std::vector<plfx_node> batch;
+  for (int lv = 0; lv < nlev; lv++) {
+    batch.clear();
+    for (int j = 0; j < nops; j++) {
+      if (level[j] != lv) continue;
+      const plfx_trav_op &o = ops[j];
+      const char *pm = static_cast<const char *>(pmats);
+      batch.push_back(plfx_node{clv[o.child1], clv[o.child2], clv[o.parent],
+                                pm + (size_t)(2 * o.pmat) * mat * es,
+                                pm + (size_t)(2 * o.pmat + 1) * mat * es,
+                                scalers ? scalers[j] : nullptr,
+                                scaler_sums ? scaler_sums + j : nullptr});
+    }
+    int rc = plfx_plf_batch_dev(ctx, dtype, states, batch.data(), (int)batch.size(), EV, n, wgt, s);
+    if (rc != PLFX_OK) return rc;
+  }
+  return PLFX_OK;
+}
+
+int plfx_root_lnl(plfx_ctx *ctx, int dtype, int states, const void *x, int64_t n,
+                  const double *catw, const double *freq, const int32_t *wgt,
+                  const int64_t *scaler_sums, int nsums, double *out_lnl, double *site_lnl,
+                  void *stream) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if (states != 4 && states != 20) return fail(ctx, PLFX_ERR_UNSUPPORTED, "lnl: states=%d", states);
+  if (!out_lnl || n < 0 || (n > 0 && !x) || nsums < 0 || (nsums > 0 && !scaler_sums))
+    return fail(ctx, PLFX_ERR_INVALID, "bad root_lnl arguments");
+  hipStream_t s = pick(ctx, stream);
+  if (n == 0) {
+    PLFX_HIP(ctx, hipMemsetAsync(out_lnl, 0, sizeof(double), s));
+    if (nsums == 0) return PLFX_OK;
+  }
+  hipError_t e = plfx::launch_root_lnl(dtype, states, x, n, catw, freq, wgt, scaler_sums, nsums,
+                                       ctx->lnl_partials, ctx->lnl_ticket, out_lnl, site_lnl, s);
+  if (e != hipSuccess) return hip_fail(ctx, e, "root_lnl launch");
+  return PLFX_OK;
 }
 
 int plfx_scaler_sum(plfx_ctx *ctx, const uint8_t *scaler, const int32_t *wgt, int64_t n,

@@ -47,6 +47,7 @@ EXPORTS = (
     "plfx_tb_instance_elements_out",
     "plfx_tb_instance_active_elements_left", "plfx_tb_instance_active_elements_right",
     "plfx_tb_num_windows_per_instance", "plfx_pack_instance",
+    "plfx_plf_batch_dev", "plfx_traverse", "plfx_root_lnl",
 )
 
 
@@ -54,6 +55,18 @@ class PlfxError(RuntimeError):
     def __init__(self, code, msg=""):
         super().__init__(f"plfx error {code}: {msg}")
         self.code = code
+
+
+class Node(C.Structure):
+    """plfx_node: one inner-node update (all device pointers)."""
+    _fields_ = [("x1", C.c_void_p), ("x2", C.c_void_p), ("x3", C.c_void_p),
+                ("left", C.c_void_p), ("right", C.c_void_p), ("scaler", C.c_void_p),
+                ("scaler_sum", C.c_void_p)]
+
+
+class TravOp(C.Structure):
+    _fields_ = [("parent", C.c_int32), ("child1", C.c_int32), ("child2", C.c_int32),
+                ("pmat", C.c_int32)]
 
 
 class _TB(C.Structure):
@@ -103,6 +116,10 @@ def load():
         f.argtypes = [tbp]
         f.restype = C.c_uint64
     L.plfx_pack_instance.argtypes = [tbp, i32, i32, vp, vp, vp, vp, vp, vp, vp]
+    L.plfx_plf_batch_dev.argtypes = [vp, i32, i32, C.POINTER(Node), i32, vp, i64, vp, vp]
+    L.plfx_traverse.argtypes = [vp, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp), i32, vp, i32,
+                                vp, i64, vp, C.POINTER(vp), vp, vp]
+    L.plfx_root_lnl.argtypes = [vp, i32, i32, vp, i64, vp, vp, vp, vp, i32, vp, vp, vp]
     _lib = L
     return L
 
@@ -253,6 +270,80 @@ class Context:
                                               p(out_scaler), n, int(window_size), int(layout),
                                               F32 if dt == torch.float32 else F64,
                                               _stream_handle(stream)))
+
+    # -- (6) batched nodes / traversal ---------------------------------------
+    def plf_batch_dev(self, nodes, EV, n, wgt=None, stream=None):
+        """nodes: sequence of dicts with torch tensors x1, x2, x3, left, right and
+        optional scaler (uint8[n]), scaler_sum (int64[1]); all one float dtype,
+        all sharing EV, n (sites) and wgt."""
+        import torch
+
+        dt = EV.dtype
+        arr = (Node * len(nodes))()
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        for i, nd in enumerate(nodes):
+            for k in ("x1", "x2", "x3"):
+                t = nd[k]
+                if t.dtype != dt or t.numel() < 16 * n or not t.is_contiguous():
+                    raise PlfxError(ERR_INVALID, f"node {i}: {k} must be contiguous {dt} >= 16*n")
+            for k in ("left", "right"):
+                if nd[k].dtype != dt or nd[k].numel() < 64:
+                    raise PlfxError(ERR_INVALID, f"node {i}: {k} needs 64 values")
+            arr[i] = Node(ptr(nd["x1"]), ptr(nd["x2"]), ptr(nd["x3"]), ptr(nd["left"]),
+                          ptr(nd["right"]), ptr(nd.get("scaler")), ptr(nd.get("scaler_sum")))
+        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n):
+            raise PlfxError(ERR_INVALID, "wgt must be int32 with >= n elements")
+        self._check(self._L.plfx_plf_batch_dev(self.h, F32 if dt == torch.float32 else F64, 4, arr,
+                                               len(nodes), C.c_void_p(EV.data_ptr()), int(n),
+                                               C.c_void_p(ptr(wgt)), _stream_handle(stream)))
+
+    def traverse(self, ops, clv, pmats, EV, n, wgt=None, scalers=None, scaler_sums=None,
+                 stream=None):
+        """Run a post-order traversal descriptor.  ops: (nops, 4) int array of
+        [parent, child1, child2, pmat]; clv: list of torch CLV tensors (slots);
+        pmats: tensor of 2*npmat matrices (64 values each for DNA)."""
+        import torch
+
+        ops = np.ascontiguousarray(ops, dtype=np.int32).reshape(-1, 4)
+        nops = ops.shape[0]
+        dt = EV.dtype
+        for t in clv:
+            if t.dtype != dt or t.numel() < 16 * n or not t.is_contiguous():
+                raise PlfxError(ERR_INVALID, "every CLV slot must be contiguous, same dtype, >= 16*n")
+        if pmats.dtype != dt or pmats.numel() % 128:
+            raise PlfxError(ERR_INVALID, "pmats must hold whole (left, right) pairs of 64 values")
+        if scaler_sums is not None and (scaler_sums.dtype != torch.int64 or scaler_sums.numel() < nops):
+            raise PlfxError(ERR_INVALID, "scaler_sums must be int64 with >= nops entries")
+        top = (TravOp * nops)(*[TravOp(*map(int, r)) for r in ops])
+        slots = (C.c_void_p * len(clv))(*[t.data_ptr() for t in clv])
+        sc = None
+        if scalers is not None:
+            sc = (C.c_void_p * nops)(*[None if t is None else t.data_ptr() for t in scalers])
+        self._check(self._L.plfx_traverse(
+            self.h, F32 if dt == torch.float32 else F64, 4, top, nops, slots, len(clv),
+            C.c_void_p(pmats.data_ptr()), pmats.numel() // 128, C.c_void_p(EV.data_ptr()), int(n),
+            C.c_void_p(None if wgt is None else wgt.data_ptr()), sc,
+            C.c_void_p(None if scaler_sums is None else scaler_sums.data_ptr()),
+            _stream_handle(stream)))
+
+    # -- (7) root log-likelihood --------------------------------------------
+    def root_lnl(self, x, n, out, catw=None, freq=None, wgt=None, scaler_sums=None,
+                 site_lnl=None, states=4, stream=None):
+        """Root lnL into `out` (float64 device tensor, 1 element); see plfx.h (7)."""
+        import torch
+
+        if out.dtype != torch.float64 or out.numel() < 1:
+            raise PlfxError(ERR_INVALID, "out must be a float64 device tensor")
+        if x.numel() < 4 * states * n:
+            raise PlfxError(ERR_INVALID, "x too small")
+        for t, k in ((catw, 4), (freq, states)):
+            if t is not None and (t.dtype != torch.float64 or t.numel() < k):
+                raise PlfxError(ERR_INVALID, "catw/freq must be float64 device tensors")
+        p = lambda t: C.c_void_p(None if t is None else t.data_ptr())  # noqa: E731
+        nsums = 0 if scaler_sums is None else scaler_sums.numel()
+        self._check(self._L.plfx_root_lnl(self.h, F32 if x.dtype == torch.float32 else F64, states,
+                                          p(x), int(n), p(catw), p(freq), p(wgt), p(scaler_sums),
+                                          nsums, p(out), p(site_lnl), _stream_handle(stream)))
 
     # -- (4) scaler reduction ----------------------------------------------
     def scaler_sum(self, scaler, wgt, out_sum, n=None, stream=None):

@@ -129,6 +129,56 @@ int plfx_instance_run(plfx_ctx *ctx, const void *in_left, const void *in_right,
 int plfx_scaler_sum(plfx_ctx *ctx, const uint8_t *scaler, const int32_t *wgt,
                     int64_t n, int64_t *out_sum, void *stream);
 
+/* ---- (6) many inner nodes per launch (extension: the reference evaluates
+ * one node per call; BASELINE configs 3 and 4) -------------------------- */
+/* One inner-node update: parent x3 from children x1, x2 with this node's P
+ * matrices (left/right: C*S*S values, layout of plf.cpp:37-38).  scaler
+ * (uint8 per site) and scaler_sum (int64) are optional per node. */
+typedef struct {
+  const void *x1, *x2;
+  void *x3;
+  const void *left, *right;
+  uint8_t *scaler;
+  int64_t *scaler_sum;
+} plfx_node;
+
+/* `count` independent nodes sharing EV, n and wgt; all device pointers, the
+ * `nodes` array itself is host memory (it travels in the kernel arguments, 32
+ * nodes per launch: graph-capture safe).  states must be 4 (DNA). */
+int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *nodes, int count,
+                       const void *EV, int64_t n, const int32_t *wgt, void *stream);
+
+/* A traversal descriptor (RAxML-style post-order list).  Op j computes CLV
+ * slot `parent` from slots `child1`, `child2` with the P-matrix pair `pmat`:
+ * left = pmats + (2*pmat)*C*S*S, right = pmats + (2*pmat+1)*C*S*S. */
+typedef struct {
+  int32_t parent, child1, child2, pmat;
+} plfx_trav_op;
+
+/* Executes `ops` in an order equivalent to the sequential one: ops are grouped
+ * into dependency levels (an op waits for the ops that write its children and
+ * for earlier readers/writers of its parent slot) and each level is issued as
+ * batched launches.  clv: host array of `nslots` device CLV pointers;
+ * scalers: host array of nops device uint8 pointers (or NULL / NULL entries);
+ * scaler_sums: device int64[nops] (or NULL): entry j = op j's scalerIncrement. */
+int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
+                  void *const *clv, int nslots, const void *pmats, int npmats, const void *EV,
+                  int64_t n, const int32_t *wgt, uint8_t *const *scalers, int64_t *scaler_sums,
+                  void *stream);
+
+/* ---- (7) root log-likelihood (extension) -- */
+/* lnL = sum_i wgt_i * log( sum_c catw[c] * sum_s freq[s] * x[i][c][s] )
+ *       + (sum_{j<nsums} scaler_sums[j]) * log(2^-32)
+ * x: device CLV of the root (n sites, states S in {4, 20}, 4 categories);
+ * catw (4), freq (S): device f64 arrays or NULL (uniform); wgt NULL = 1;
+ * scaler_sums: device int64[nsums] (the inner nodes' scalerIncrements).
+ * out_lnl: device double; site_lnl: optional device double[n] (log L_i
+ * without the scaling correction).  Deterministic (fixed reduction order). */
+int plfx_root_lnl(plfx_ctx *ctx, int dtype, int states, const void *x, int64_t n,
+                  const double *catw, const double *freq, const int32_t *wgt,
+                  const int64_t *scaler_sums, int nsums, double *out_lnl, double *site_lnl,
+                  void *stream);
+
 /* ---- (5) instance sizing: testbench_info (app/src/include.h:150-266) ---- */
 /* 64-bit throughout.  `instance` < 0 means "no instance" where the
  * reference has an overload without one. */

@@ -89,6 +89,15 @@ def lib():
             f = getattr(L, f"plfo_gen_hostmem_{sfx}")
             f.argtypes = [C.c_uint32, C.c_longlong, fp, fp, fp, fp, fp, C.c_void_p]
             f.restype = None
+        for sfx in ("f32", "f64"):
+            f = getattr(L, f"plfo_traverse_{sfx}")
+            f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                          C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p]
+            f.restype = None
+            f = getattr(L, f"plfo_root_lnl_{sfx}")
+            f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p,
+                          C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+            f.restype = C.c_double
         L.plfo_scaler_sum.argtypes = [_u8p, C.c_void_p, C.c_longlong]
         L.plfo_scaler_sum.restype = C.c_longlong
         L.plfo_mt_draws.argtypes = [C.c_uint32, C.c_longlong, C.c_void_p, C.c_void_p]
@@ -163,6 +172,58 @@ def plf_generic(S, Ccat, x1, x2, EV, left, right, wgt=None):
     getattr(lib(), f"plfo_plf_gen_{_sfx(dt)}")(S, Ccat, x1, x2, x3, EV, n, left, right,
                                                _ptr(wgt), C.byref(inc), _ptr(sc))
     return x3, sc, inc.value
+
+
+def traverse(S, Ccat, ops, clv, pmats, EV, n, wgt=None, want_scalers=False):
+    """Sequential traversal (extension, unpinned): ops = int32 array (nops, 4)
+    [parent, child1, child2, pmat]; clv = list of numpy CLVs (slots, written in
+    place); pmats = flat array of 2*npmat matrices (C*S*S each).
+    Returns (scaler_sums int64[nops], scalers list or None)."""
+    ops = np.ascontiguousarray(ops, dtype=np.int32).reshape(-1, 4)
+    nops = ops.shape[0]
+    dt = clv[0].dtype
+    ptrs = (C.c_void_p * len(clv))(*[a.ctypes.data_as(C.c_void_p) for a in clv])
+    sums = np.zeros(nops, np.int64)
+    scal = [np.zeros(n, np.uint8) for _ in range(nops)] if want_scalers else None
+    sptr = (C.c_void_p * nops)(*[a.ctypes.data_as(C.c_void_p) for a in scal]) if scal else None
+    w = None if wgt is None else np.ascontiguousarray(wgt, np.int32)
+    getattr(lib(), f"plfo_traverse_{_sfx(dt)}")(S, Ccat, ops.ctypes.data_as(C.c_void_p), nops, ptrs,
+                                               np.ascontiguousarray(pmats, dt).ctypes.data_as(C.c_void_p),
+                                               np.ascontiguousarray(EV, dt).ctypes.data_as(C.c_void_p),
+                                               n, _ptr(w), sptr, sums.ctypes.data_as(C.c_void_p))
+    return sums, scal
+
+
+def root_lnl(S, Ccat, x, n, catw=None, freq=None, wgt=None, scaler_sums=None, site=False):
+    """Root log-likelihood (extension, unpinned):
+    sum_i wgt_i log(sum_c catw_c sum_s freq_s x[i,c,s]) + sum(scaler_sums)*log(2^-32)."""
+    dt = x.dtype
+    sl = np.empty(n, np.float64) if site else None
+    ss = None if scaler_sums is None else np.ascontiguousarray(scaler_sums, np.int64)
+    cw = None if catw is None else np.ascontiguousarray(catw, np.float64)
+    fr = None if freq is None else np.ascontiguousarray(freq, np.float64)
+    w = None if wgt is None else np.ascontiguousarray(wgt, np.int32)
+    v = getattr(lib(), f"plfo_root_lnl_{_sfx(dt)}")(S, Ccat, x.ctypes.data_as(C.c_void_p), n,
+                                                    _ptr(cw), _ptr(fr), _ptr(w), _ptr(ss),
+                                                    0 if ss is None else ss.size, _ptr(sl))
+    return (v, sl) if site else v
+
+
+def balanced_tree_ops(ntips):
+    """Post-order ops of a balanced binary tree over `ntips` tips (power of 2):
+    slots 0..ntips-1 are tips, inner nodes get slots ntips.. in post-order
+    (level by level); op j uses P-matrix pair j.  Returns int32 (ntips-1, 4)."""
+    ops = []
+    level = list(range(ntips))
+    nxt = ntips
+    while len(level) > 1:
+        new = []
+        for i in range(0, len(level), 2):
+            ops.append((nxt, level[i], level[i + 1], len(ops)))
+            new.append(nxt)
+            nxt += 1
+        level = new
+    return np.array(ops, np.int32)
 
 
 def ref_plf(x1, x2, EV, left, right, wgt, opt="O0"):

@@ -258,3 +258,63 @@ void plfo_mt_draws(uint32_t seed, long long count, uint32_t *out32, double *outd
 
 PLFO_DEFINE_GEN_INPUTS(f32, float)
 PLFO_DEFINE_GEN_INPUTS(f64, double)
+
+/* ------------------------------------------------------------------------ */
+/* Tree traversal and root log-likelihood (extensions: the reference has no  */
+/* traversal or evaluate step, SURVEY F9 -- parity unpinned beyond reusing   */
+/* the pinned plf() loop).  Ops run strictly in list order (the sequential   */
+/* semantics the GPU's level-batched schedule must reproduce).               */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int parent, child1, child2, pmat;
+} plfo_trav_op;
+
+#define PLFO_DEFINE_TRAV(SUFFIX, T)                                                     \
+  void plfo_traverse_##SUFFIX(int S, int C, const plfo_trav_op *ops, int nops, T **clv,  \
+                              const T *pmats, const T *EV, long long n, const int *wgt,   \
+                              unsigned char **scalers, long long *scaler_sums) {          \
+    const long long mat = (long long)C * S * S;                                          \
+    int j;                                                                               \
+    for (j = 0; j < nops; j++) {                                                         \
+      const plfo_trav_op *o = &ops[j];                                                   \
+      long long inc = 0;                                                                 \
+      plfo_plf_gen_##SUFFIX(S, C, clv[o->child1], clv[o->child2], clv[o->parent], EV, n,  \
+                            pmats + (2LL * o->pmat) * mat, pmats + (2LL * o->pmat + 1) * mat, \
+                            wgt, &inc, scalers ? scalers[j] : 0);                        \
+      if (scaler_sums) scaler_sums[j] = inc;                                             \
+    }                                                                                    \
+  }
+
+PLFO_DEFINE_TRAV(f32, float)
+PLFO_DEFINE_TRAV(f64, double)
+
+/* lnL = sum_i wgt_i log(sum_c catw[c] sum_s freq[s] x[i][c][s])
+ *       + (sum of scaler_sums) * log(2^-32)           (sites in order) */
+#define PLFO_DEFINE_LNL(SUFFIX, T)                                                      \
+  double plfo_root_lnl_##SUFFIX(int S, int C, const T *x, long long n, const double *catw, \
+                                const double *freq, const int *wgt,                      \
+                                const long long *scaler_sums, int nsums,                 \
+                                double *site_lnl) {                                      \
+    double acc = 0.0;                                                                    \
+    long long i, nsc = 0;                                                                \
+    int c, s;                                                                            \
+    for (i = 0; i < n; i++) {                                                            \
+      double L = 0.0;                                                                    \
+      for (c = 0; c < C; c++) {                                                          \
+        double t = 0.0;                                                                  \
+        for (s = 0; s < S; s++)                                                          \
+          t += (freq ? freq[s] : 1.0 / S) * (double)x[i * S * C + c * S + s];            \
+        L += (catw ? catw[c] : 1.0 / C) * t;                                             \
+      }                                                                                  \
+      {                                                                                  \
+        double l = log(L);                                                               \
+        if (site_lnl) site_lnl[i] = l;                                                   \
+        acc += (wgt ? (double)wgt[i] : 1.0) * l;                                         \
+      }                                                                                  \
+    }                                                                                    \
+    for (c = 0; c < nsums; c++) nsc += scaler_sums[c];                                   \
+    return acc + (double)nsc * (-32.0 * 0.69314718055994530942);                         \
+  }
+
+PLFO_DEFINE_LNL(f32, float)
+PLFO_DEFINE_LNL(f64, double)

@@ -1,0 +1,178 @@
+"""GPU tests of the multi-node extensions (BASELINE configs 3 and 4): batched
+independent nodes, traversal descriptors with level scheduling, and the root
+log-likelihood.  The reference has none of these: parity is
+against the oracle's sequential restatement built on the pinned plf() loop --
+"parity unpinned" beyond that.  Bar: CLVs and scaler sums bit-exact; lnL within
+1e-12 relative (device log() and a different, fixed summation order)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LNL_RTOL = 1e-12
+
+
+def bits(a):
+    a = np.asarray(a)
+    return a.view(np.uint32 if a.dtype == np.float32 else np.uint64)
+
+
+def dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("count", [1, 5, 32, 41])
+def test_batch_independent_nodes(ctx, oracle, dtype, count):
+    import torch
+
+    n = 3001
+    rng = np.random.default_rng(count)
+    d = oracle.gen_hostmem(n, dtype, 100 + count)
+    EV = d["EV"]
+    w = (rng.integers(0, 5, n)).astype(np.int32)
+    nodes, exp = [], []
+    for i in range(count):
+        x1 = (rng.random(16 * n) * (1e-12 if i % 3 == 0 else 1.0)).astype(dtype)
+        x2 = rng.random(16 * n).astype(dtype)
+        L = rng.random(64).astype(dtype)
+        R = rng.random(64).astype(dtype)
+        exp.append(oracle.plf(x1, x2, EV, L, R, w))
+        nodes.append(dict(x1=dev(x1), x2=dev(x2), x3=torch.empty(16 * n, dtype=dev(x1).dtype, device="cuda"),
+                          left=dev(L), right=dev(R),
+                          scaler=torch.empty(n, dtype=torch.uint8, device="cuda") if i % 2 == 0 else None,
+                          scaler_sum=torch.zeros(1, dtype=torch.int64, device="cuda") if i % 4 != 3 else None))
+    ctx.plf_batch_dev(nodes, dev(EV), n, dev(w))
+    torch.cuda.synchronize()
+    for i, (nd, (e3, esc, einc)) in enumerate(zip(nodes, exp)):
+        assert np.array_equal(bits(nd["x3"].cpu().numpy()), bits(e3)), i
+        if nd["scaler"] is not None:
+            assert np.array_equal(nd["scaler"].cpu().numpy(), esc), i
+        if nd["scaler_sum"] is not None:
+            assert int(nd["scaler_sum"].item()) == einc, i
+
+
+def _tree_case(oracle, ntips, n, dtype, seed):
+    rng = np.random.default_rng(seed)
+    ops = oracle.balanced_tree_ops(ntips)
+    nslots = ntips + ops.shape[0]
+    tips = [rng.random(16 * n).astype(dtype) for _ in range(ntips)]
+    pm = (rng.random(ops.shape[0] * 2 * 64) * 0.25).astype(dtype)   # P, EV x0.25
+    EV = (rng.random(16) * 0.25).astype(dtype)
+    wgt = rng.integers(1, 4, n).astype(np.int32)
+    return ops, nslots, tips, pm, EV, wgt
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_traverse_balanced_tree(ctx, oracle, dtype):
+    import torch
+
+    n = 2049
+    ops, nslots, tips, pm, EV, wgt = _tree_case(oracle, 16, n, dtype, 7)
+    clv_h = [t.copy() for t in tips] + [np.zeros(16 * n, dtype) for _ in range(nslots - 16)]
+    esums, escal = oracle.traverse(4, 4, ops, clv_h, pm, EV, n, wgt, want_scalers=True)
+    assert esums.sum() > 0  # deep levels underflow: the scaler path is exercised
+    clv = [dev(t) for t in tips] + [torch.zeros(16 * n, dtype=dev(tips[0]).dtype, device="cuda")
+                                    for _ in range(nslots - 16)]
+    sums = torch.zeros(ops.shape[0], dtype=torch.int64, device="cuda")
+    scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(ops.shape[0])]
+    ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums)
+    torch.cuda.synchronize()
+    for s in range(16, nslots):
+        assert np.array_equal(bits(clv[s].cpu().numpy()), bits(clv_h[s])), s
+    assert np.array_equal(sums.cpu().numpy(), esums)
+    for j in range(ops.shape[0]):
+        assert np.array_equal(scal[j].cpu().numpy(), escal[j])
+    # root lnL with model weights
+    catw = np.array([0.1, 0.2, 0.3, 0.4])
+    freq = np.array([0.3, 0.2, 0.25, 0.25])
+    root = nslots - 1
+    exp, esite = oracle.root_lnl(4, 4, clv_h[root], n, catw, freq, wgt, esums, site=True)
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    site = torch.zeros(n, dtype=torch.float64, device="cuda")
+    ctx.root_lnl(clv[root], n, out, dev(catw), dev(freq), dev(wgt), sums, site)
+    torch.cuda.synchronize()
+    got = float(out.item())
+    assert abs(got - exp) <= LNL_RTOL * abs(exp)
+    assert np.allclose(site.cpu().numpy(), esite, rtol=1e-14, atol=0)
+
+
+def test_traverse_slot_reuse_hazards(ctx, oracle):
+    """A caterpillar that recycles CLV slots (write-after-read and
+    write-after-write hazards): the level schedule must equal sequential order."""
+    import torch
+
+    n = 777
+    rng = np.random.default_rng(3)
+    tips = [rng.random(16 * n) for _ in range(5)]
+    # slots 0..4 tips, 5 and 6 scratch
+    ops = np.array([[5, 0, 1, 0], [6, 5, 2, 1], [5, 6, 3, 2], [6, 5, 4, 3], [5, 2, 3, 4],
+                    [0, 1, 4, 0]], np.int32)
+    pm = rng.random(5 * 128) * 0.5
+    EV = rng.random(16)
+    clv_h = [t.copy() for t in tips] + [np.zeros(16 * n), np.zeros(16 * n)]
+    esums, _ = oracle.traverse(4, 4, ops, clv_h, pm, EV, n)
+    clv = [dev(t) for t in tips] + [torch.zeros(16 * n, dtype=torch.float64, device="cuda") for _ in range(2)]
+    sums = torch.zeros(ops.shape[0], dtype=torch.int64, device="cuda")
+    ctx.traverse(ops, clv, dev(pm), dev(EV), n, None, None, sums)
+    torch.cuda.synchronize()
+    for s in range(7):
+        assert np.array_equal(bits(clv[s].cpu().numpy()), bits(clv_h[s])), s
+    assert np.array_equal(sums.cpu().numpy(), esums)
+
+
+def test_traverse_rejects_bad_ops(ctx):
+    import plfx
+    import torch
+
+    n = 16
+    clv = [torch.zeros(16 * n, dtype=torch.float64, device="cuda") for _ in range(3)]
+    pm = torch.zeros(128, dtype=torch.float64, device="cuda")
+    EV = torch.zeros(16, dtype=torch.float64, device="cuda")
+    for bad in ([[2, 0, 5, 0]], [[2, 0, 1, 1]], [[0, 0, 1, 0]]):
+        with pytest.raises(plfx.PlfxError):
+            ctx.traverse(np.array(bad, np.int32), clv, pm, EV, n)
+
+
+def test_tree64_full_size_window(ctx, oracle):
+    """BASELINE config 3 shape: 64-taxon balanced tree, 63 inner nodes, 2^20
+    sites, f64, on the GPU; sites are independent, so a 4096-site window is
+    checked bit-exactly against the oracle run on that window, and the full
+    root lnL against the oracle's lnL of the GPU's root CLV."""
+    import torch
+
+    n = 1 << 20
+    ntips = 64
+    ops = oracle.balanced_tree_ops(ntips)
+    nslots = ntips + ops.shape[0]
+    g = torch.Generator(device="cuda")
+    g.manual_seed(20250117)
+    clv = [torch.rand(16 * n, dtype=torch.float64, device="cuda", generator=g) for _ in range(ntips)]
+    clv += [torch.empty(16 * n, dtype=torch.float64, device="cuda") for _ in range(nslots - ntips)]
+    pm = torch.rand(ops.shape[0] * 128, dtype=torch.float64, device="cuda", generator=g) * 0.25
+    EV = torch.rand(16, dtype=torch.float64, device="cuda", generator=g) * 0.25
+    sums = torch.zeros(ops.shape[0], dtype=torch.int64, device="cuda")
+    scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(ops.shape[0])]
+    ctx.traverse(ops, clv, pm, EV, n, None, scal, sums)
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    ctx.root_lnl(clv[-1], n, out, scaler_sums=sums)
+    torch.cuda.synchronize()
+    # per-op sums equal the scaler bytes they summarise
+    gsums = sums.cpu().numpy()
+    for j in range(ops.shape[0]):
+        assert int(scal[j].sum().item()) == gsums[j]
+    assert gsums.sum() > 0
+    # window check
+    lo, m = 500_003, 4096
+    win = [t[16 * lo:16 * (lo + m)].cpu().numpy().copy() for t in clv[:ntips]]
+    win += [np.zeros(16 * m) for _ in range(nslots - ntips)]
+    esums, escal = oracle.traverse(4, 4, ops, win, pm.cpu().numpy(), EV.cpu().numpy(), m, want_scalers=True)
+    for s in range(ntips, nslots):
+        assert np.array_equal(bits(clv[s][16 * lo:16 * (lo + m)].cpu().numpy()), bits(win[s])), s
+    for j in range(ops.shape[0]):
+        assert np.array_equal(scal[j][lo:lo + m].cpu().numpy(), escal[j])
+    root = clv[-1].cpu().numpy()
+    exp = oracle.root_lnl(4, 4, root, n, scaler_sums=gsums)
+    assert abs(float(out.item()) - exp) <= LNL_RTOL * abs(exp)
