@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--sites", type=int, default=1 << 20)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--buffer-sets", type=int, default=4)
+    ap.add_argument("--workload", choices=["node", "tree64", "nodes64"], default="node",
+                    help="node: BASELINE configs[1] (headline); tree64: configs[2]; "
+                         "nodes64: the per-GPU shard of configs[3]")
     ap.add_argument("--launch", choices=["bound", "checked", "graph"], default="graph",
                     help="bound: pre-validated launcher per buffer set; checked: full "
                          "argument checks per call; graph: steps captured in one HIP graph")
@@ -120,6 +123,173 @@ def cpu_baseline(n_sites, seconds):
     return res
 
 
+class NodeWorkload:
+    """BASELINE configs[1]: one inner node of n sites per GPU per step, rotating
+    over R buffer sets (R x 389 MiB > the 256 MiB Infinity Cache)."""
+
+    def __init__(self, ctx, a, dev, g, tdt, esz):
+        import torch
+
+        n, R = a.sites, max(1, a.buffer_sets)
+        self.n, self.R = n, R
+        self.EV = torch.rand(16, dtype=tdt, device=dev, generator=g)
+        self.left = torch.rand(64, dtype=tdt, device=dev, generator=g)
+        self.right = torch.rand(64, dtype=tdt, device=dev, generator=g)
+        self.sets = []
+        for _ in range(R):
+            x1 = torch.rand(n * 16, dtype=tdt, device=dev, generator=g)
+            x1.view(-1, 16)[0::4] *= 1e-12  # host_mem.cpp:200-202: every 4th site underflows
+            x2 = torch.rand(n * 16, dtype=tdt, device=dev, generator=g)
+            self.sets.append(dict(x1=x1, x2=x2, x3=torch.empty_like(x1),
+                                  wgt=torch.ones(n, dtype=torch.int32, device=dev),
+                                  sc=torch.empty(n, dtype=torch.uint8, device=dev),
+                                  s=torch.zeros(1, dtype=torch.int64, device=dev)))
+        self.ctx, self.checked = ctx, a.launch == "checked"
+        self.bound = [ctx.bind_plf_dev(b["x1"], b["x2"], b["x3"], self.EV, self.left, self.right,
+                                       b["wgt"], b["sc"], b["s"]) for b in self.sets]
+        self.sites_per_step = n
+        self.bytes_per_step = bytes_per_site(esz) * n
+        self.bytes_per_site = bytes_per_site(esz)
+        self.config = {
+            "workload": f"DNA 4-state x 4 Gamma cats, 1 inner node per GPU per step, {n} sites, "
+                        f"{a.dtype} (BASELINE configs[1])",
+            "sites_per_gpu_per_step": n, "nodes_per_gpu_per_step": 1, "buffer_sets": R}
+
+    def step(self, i, sh):
+        if self.checked:
+            b = self.sets[i % self.R]
+            self.ctx.plf_dev(b["x1"], b["x2"], b["x3"], self.EV, self.left, self.right, b["wgt"],
+                             b["sc"], b["s"], stream=sh)
+        else:
+            self.bound[i % self.R](sh)
+
+    def check(self):
+        import torch
+
+        # every buffer set's last scaler total is n/4 (every 4th site, wgt = 1)
+        return torch.stack([b["s"][0] for b in self.sets]).sum(), self.R * ((self.n + 3) // 4)
+
+    def post(self, world, dev):
+        return {}
+
+
+class Tree64Workload:
+    """BASELINE configs[2]: post-order sweep of a 64-taxon balanced tree (63
+    inner nodes, levels of 32/16/8/4/2/1 nodes, one batched launch per level)
+    over n sites, then the root log-likelihood.  Tips dense U[0,1); P and EV
+    x0.25 so magnitudes stay bounded and deep levels underflow."""
+
+    def __init__(self, ctx, a, dev, g, tdt, esz):
+        import numpy as np
+        import torch
+
+        n = a.sites
+        ntips = 64
+        self.n, self.ctx = n, ctx
+        self.ops = np.array(_balanced_ops(ntips), np.int32)
+        nops = self.ops.shape[0]
+        self.clv = [torch.rand(16 * n, dtype=tdt, device=dev, generator=g) for _ in range(ntips)]
+        self.clv += [torch.empty(16 * n, dtype=tdt, device=dev) for _ in range(nops)]
+        self.pm = torch.rand(nops * 128, dtype=tdt, device=dev, generator=g) * 0.25
+        self.EV = torch.rand(16, dtype=tdt, device=dev, generator=g) * 0.25
+        self.wgt = torch.ones(n, dtype=torch.int32, device=dev)
+        self.sums = torch.zeros(nops, dtype=torch.int64, device=dev)
+        self.lnl = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.sites_per_step = nops * n
+        # per node: read x1, x2, write x3, read wgt (scaler sums, no bytes); + lnL read of the root
+        self.bytes_per_site = 3 * 16 * esz + 4
+        self.bytes_per_step = nops * self.bytes_per_site * n + (16 * esz + 4) * n
+        self.config = {
+            "workload": f"DNA 4-state, 64-taxon balanced tree post-order sweep (63 inner nodes, "
+                        f"6 level launches) + root lnL, {n} sites, {a.dtype} (BASELINE configs[2])",
+            "sites_per_gpu_per_step": self.sites_per_step, "nodes_per_gpu_per_step": nops}
+
+    def step(self, i, sh):
+        self.ctx.traverse(self.ops, self.clv, self.pm, self.EV, self.n, self.wgt, None, self.sums,
+                          stream=sh)
+        self.ctx.root_lnl(self.clv[-1], self.n, self.lnl, wgt=self.wgt, scaler_sums=self.sums,
+                          stream=sh)
+
+    def check(self):
+        import torch
+
+        ok = bool(torch.isfinite(self.lnl).all().item()) and int(self.sums.sum().item()) > 0
+        return torch.tensor(1 if ok else 0), 1
+
+    def post(self, world, dev):
+        return {"root_lnl_rank0": float(self.lnl.item()),
+                "scaler_events": int(self.sums.sum().item())}
+
+
+class Nodes64Workload:
+    """BASELINE configs[3] per-GPU shard: 512 independent inner nodes x n sites
+    over 8 GPUs = 64 nodes per GPU per step (two 32-node batched launches).  After
+    the timed region every rank evaluates the lnL of its nodes and ONE RCCL
+    all-reduce sums the lnL and scaler totals over ranks."""
+
+    def __init__(self, ctx, a, dev, g, tdt, esz):
+        import torch
+
+        n = a.sites
+        self.n, self.ctx, self.nn = n, ctx, 64
+        self.EV = torch.rand(16, dtype=tdt, device=dev, generator=g)
+        self.wgt = torch.ones(n, dtype=torch.int32, device=dev)
+        self.sums = torch.zeros(self.nn, dtype=torch.int64, device=dev)
+        self.nodes = []
+        for j in range(self.nn):
+            x1 = torch.rand(n * 16, dtype=tdt, device=dev, generator=g)
+            x1.view(-1, 16)[0::4] *= 1e-12
+            self.nodes.append(dict(
+                x1=x1, x2=torch.rand(n * 16, dtype=tdt, device=dev, generator=g),
+                x3=torch.empty(n * 16, dtype=tdt, device=dev),
+                left=torch.rand(64, dtype=tdt, device=dev, generator=g),
+                right=torch.rand(64, dtype=tdt, device=dev, generator=g),
+                scaler=torch.empty(n, dtype=torch.uint8, device=dev),
+                scaler_sum=self.sums[j:j + 1]))
+        self.sites_per_step = self.nn * n
+        self.bytes_per_site = bytes_per_site(esz)
+        self.bytes_per_step = self.nn * self.bytes_per_site * n
+        self.config = {
+            "workload": f"DNA 4-state, 512 independent inner nodes sharded 64 per GPU, {n} sites, "
+                        f"{a.dtype} (BASELINE configs[3]); lnL all-reduce after the timed region",
+            "sites_per_gpu_per_step": self.sites_per_step, "nodes_per_gpu_per_step": self.nn}
+
+    def step(self, i, sh):
+        self.ctx.plf_batch_dev(self.nodes[:32], self.EV, self.n, self.wgt, stream=sh)
+        self.ctx.plf_batch_dev(self.nodes[32:], self.EV, self.n, self.wgt, stream=sh)
+
+    def check(self):
+        return self.sums.sum(), self.nn * ((self.n + 3) // 4)
+
+    def post(self, world, dev):
+        import torch
+        import torch.distributed as dist
+
+        lnl = torch.zeros(self.nn, dtype=torch.float64, device=dev)
+        for j, nd in enumerate(self.nodes):
+            self.ctx.root_lnl(nd["x3"], self.n, lnl[j:j + 1], wgt=self.wgt,
+                              scaler_sums=self.sums[j:j + 1])
+        tot = torch.stack([lnl.sum(), self.sums.sum().to(torch.float64)])
+        if world > 1:
+            dist.all_reduce(tot, op=dist.ReduceOp.SUM)  # the one lnL all-reduce (RCCL over xGMI)
+        return {"lnl_all_nodes_all_ranks": float(tot[0]), "scaler_events_all_ranks": int(tot[1])}
+
+
+def _balanced_ops(ntips):
+    ops, level, nxt = [], list(range(ntips)), ntips
+    while len(level) > 1:
+        new = []
+        for i in range(0, len(level), 2):
+            ops.append((nxt, level[i], level[i + 1], len(ops)))
+            new.append(nxt)
+            nxt += 1
+        level = new
+    return ops
+
+
+WORKLOADS = {"node": NodeWorkload, "tree64": Tree64Workload, "nodes64": Nodes64Workload}
+
+
 def main():
     a = parse()
     import torch
@@ -144,50 +314,26 @@ def main():
     ctx = plfx.Context(local)
     tdt = torch.float64 if a.dtype == "f64" else torch.float32
     esz = 8 if a.dtype == "f64" else 4
-    n = a.sites
-    R = max(1, a.buffer_sets)
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
-    EV = torch.rand(16, dtype=tdt, device=dev, generator=g)
-    left = torch.rand(64, dtype=tdt, device=dev, generator=g)
-    right = torch.rand(64, dtype=tdt, device=dev, generator=g)
-    sets = []
-    for _ in range(R):
-        x1 = torch.rand(n * 16, dtype=tdt, device=dev, generator=g)
-        x1.view(-1, 16)[0::4] *= 1e-12  # host_mem.cpp:200-202: every 4th site underflows
-        x2 = torch.rand(n * 16, dtype=tdt, device=dev, generator=g)
-        sets.append(dict(x1=x1, x2=x2, x3=torch.empty_like(x1),
-                         wgt=torch.ones(n, dtype=torch.int32, device=dev),
-                         sc=torch.empty(n, dtype=torch.uint8, device=dev),
-                         s=torch.zeros(1, dtype=torch.int64, device=dev)))
+    wl = WORKLOADS[a.workload](ctx, a, dev, g, tdt, esz)
     stream = torch.cuda.Stream(dev)          # dedicated launch stream; events on it
     sh = stream.cuda_stream
     torch.cuda.synchronize(dev)
-    bound = [ctx.bind_plf_dev(b["x1"], b["x2"], b["x3"], EV, left, right, b["wgt"], b["sc"], b["s"])
-             for b in sets]
-    torch.cuda.synchronize(dev)
-
-    def step(i):
-        if a.launch == "checked":
-            b = sets[i % R]
-            ctx.plf_dev(b["x1"], b["x2"], b["x3"], EV, left, right, b["wgt"], b["sc"], b["s"],
-                        stream=sh)
-        else:
-            bound[i % R](sh)
 
     graph = None
     if a.launch == "graph":
-        for i in range(max(a.warmup, R)):
-            step(i)
+        for i in range(max(a.warmup, 4)):
+            wl.step(i, sh)
         torch.cuda.synchronize(dev)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=stream):
             for i in range(a.steps):
-                bound[(a.warmup + i) % R](stream.cuda_stream)
+                wl.step(a.warmup + i, stream.cuda_stream)
         torch.cuda.synchronize(dev)
 
     for i in range(a.warmup):
-        step(i)
+        wl.step(i, sh)
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
@@ -200,7 +346,7 @@ def main():
             graph.replay()
     else:
         for i in range(a.steps):
-            step(a.warmup + i)
+            wl.step(a.warmup + i, sh)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     barrier()
@@ -208,26 +354,26 @@ def main():
     wall_ms = (time.perf_counter() - t0) * 1e3
     dev_ms = e0.elapsed_time(e1)
 
-    # correctness spot check: every buffer set's last scaler total is n/4
-    # (every 4th site underflows and wgt = 1); max-over-ranks timing
-    expect = (n + 3) // 4
-    got = torch.stack([b["s"][0] for b in sets]).sum()
-    wall_ms, dev_ms, check_ok = combine_ranks(wall_ms, dev_ms, got, expect * R, dev, world)
+    got, expect = wl.check()
+    wall_ms, dev_ms, check_ok = combine_ranks(wall_ms, dev_ms, got, expect, dev, world)
+    extra = wl.post(world, dev)
 
     if rank == 0:
-        per_launch_ms = dev_ms / a.steps
-        bps = bytes_per_site(esz)
-        achieved = bps * n / (per_launch_ms * 1e-3) / 1e9
+        per_step_ms = dev_ms / a.steps
+        achieved = wl.bytes_per_step / (per_step_ms * 1e-3) / 1e9
         traffic = None
         tp = Path(a.traffic_json)
-        if tp.exists():
+        if a.workload == "node" and tp.exists():
             try:
                 tj = json.loads(tp.read_text())
-                if tj.get("sites") == n and tj.get("dtype") == a.dtype:
+                if tj.get("sites") == a.sites and tj.get("dtype") == a.dtype:
                     traffic = tj.get("hbm_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None
-        value = world * n * a.steps / (wall_ms * 1e-3)
+        value = world * wl.sites_per_step * a.steps / (wall_ms * 1e-3)
+        cfg = dict(wl.config)
+        cfg.update(parallelism=f"independent nodes x{world} (one process per GPU, no data-path "
+                               "collective)", launch=a.launch, **extra)
         out = {
             "metric": METRIC,
             "value": value,
@@ -241,15 +387,7 @@ def main():
             "vs_baseline": None,
             "dtype": a.dtype,
             "data": "synthetic (torch.rand U[0,1) CLVs/P/EV, left CLV x1e-12 on every 4th site, wgt=1)",
-            "config": {
-                "workload": "DNA 4-state x 4 Gamma cats, 1 inner node per GPU per step, "
-                            f"{n} sites, {a.dtype} (BASELINE configs[1])",
-                "sites_per_gpu_per_step": n,
-                "nodes_per_gpu_per_step": 1,
-                "buffer_sets": R,
-                "parallelism": f"independent nodes x{world} (replicas, no data-path collective)",
-                "launch": a.launch,
-            },
+            "config": cfg,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -257,13 +395,13 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "bytes_per_site": bps,
-                "kernel_avg_us": per_launch_ms * 1e3,
+                "bytes_per_site": wl.bytes_per_site,
+                "kernel_avg_us": per_step_ms * 1e3,
             },
-            "check": "ok" if check_ok else "SCALER_SUM_MISMATCH",
+            "check": "ok" if check_ok else "CHECK_FAILED",
         }
         if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(a.sites, a.cpu_seconds)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
