@@ -20,6 +20,7 @@
 #include "plf_dna.hpp"
 #include "plf_kernels.hpp"
 #include "plf_lnl.hpp"
+#include "plf_prot.hpp"
 
 namespace plfx {
 namespace {
@@ -128,7 +129,32 @@ hipError_t launch_lnl_t(const T *x, int64_t n, const double *catw, const double 
   return hipGetLastError();
 }
 
+template <typename T, bool kFma, bool kSum>
+hipError_t launch_prot_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
+  static int cache = 0;
+  auto kernel = &dev::plf_prot_kernel<T, kFma, kSum>;
+  const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
+                     (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,
+                     (const T *)a.right, a.wgt, a.scaler, a.n, a.ws, a.scaler_sum);
+  return hipGetLastError();
+}
+
+template <typename T, bool kFma>
+hipError_t launch_prot_s(const DnaArgs &a, int max_blocks, hipStream_t s) {
+  return a.scaler_sum ? launch_prot_t<T, kFma, true>(a, max_blocks, s)
+                      : launch_prot_t<T, kFma, false>(a, max_blocks, s);
+}
+
 }  // namespace
+
+hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s) {
+  if (dtype == 1)
+    return fma ? launch_prot_s<double, true>(a, max_blocks, s)
+               : launch_prot_s<double, false>(a, max_blocks, s);
+  return fma ? launch_prot_s<float, true>(a, max_blocks, s)
+             : launch_prot_s<float, false>(a, max_blocks, s);
+}
 
 hipError_t launch_plf_dna_f32(const DnaArgs &a, int max_blocks, hipStream_t s) {
   return a.scaler_sum ? launch_cat<float, true>(a, max_blocks, s)

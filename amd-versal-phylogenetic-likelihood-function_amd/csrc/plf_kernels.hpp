@@ -26,6 +26,9 @@ hipError_t launch_plf_dna_f32(const DnaArgs &a, int max_blocks, hipStream_t s);
 hipError_t launch_plf_dna_f64(const DnaArgs &a, int max_blocks, hipStream_t s);
 
 // sum_j scaler[j]*wgt[j] (host_mem.cpp:384-388), self-resetting ws as above.
+// Protein (S=20, C=4) kernel; fma selects fused multiply-add.
+hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s);
+
 // Batched nodes (<= kMaxBatch per launch) sharing EV, n, wgt.  dtype: 0 f32, 1 f64.
 struct NodeDescH {
   const void *x1, *x2;

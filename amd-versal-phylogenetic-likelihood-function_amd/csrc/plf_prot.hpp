@@ -1,0 +1,256 @@
+// plf_prot.hpp -- fused PLF inner-node update for S=20 states (protein) x C=4
+// Gamma categories (extension: the reference hard-wires DNA, SURVEY F9 /
+// BASELINE configs[4]).  Same loop as plf() (app/src/plf.cpp:19-65) with 4
+// replaced by 20: ump[k] = sum_l x[c][l]*P_c[k][l] (ascending l from +0.0),
+// prod[k] = umpL*umpR, x3[c][l] = sum_k prod[k]*EV[k][l] (ascending k from
+// +0.0), site scaled iff all 80 |x3| < 2^-32.
+//
+// Mapping: a 256-thread block owns 64 consecutive sites; wave w = category c,
+// lane = site.  Child tiles pass through LDS (coalesced global access, padded
+// conflict-free rows; lane = site directly on HBM re-read every line 4x and
+// thrashed L2).  The wave's category matrices P_L, P_R and EV (3 x 400 values)
+// stay resident in VGPRs for the whole kernel, spread over the 64 lanes (value
+// e lives in lane e%64 of register e/64: 7 registers per matrix), and every
+// use broadcasts one value with v_readlane at a compile-time lane -- no memory
+// latency in the inner loop.  (Measured alternatives, both at 14 % of the HBM
+// roofline: s_load from the scalar cache, which cannot hold 4 x 9.6 KB, and
+// LDS broadcasts, which move a full 1 KiB per ds_read_b128 and were each
+// waited on immediately.)  Each
+// lane keeps its 20 x1, 20 x2 and 20 running x3 values in VGPRs and streams
+// over k, accumulating x3 in plf()'s k order.  The 80-value scale test of a
+// site spans the 4 waves: each wave ballots its 20-value test, the 4 masks meet
+// in LDS and are ANDed.  The four waves of a block read the same contiguous
+// 64 x 640 B of each child, so HBM/L2 see whole lines.
+//
+// kFma=false: separate multiply and add in plf()'s order (bit-identical to the
+// oracle's generic restatement); kFma=true: fused multiply-add (one rounding
+// per term), half the VALU issue, within 1e-12 relative of it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <type_traits>
+
+#include "plf_dna.hpp"
+
+namespace plfx {
+namespace dev {
+
+template <typename T, bool kFma>
+__device__ __forceinline__ T madd(T a, T b, T c) {
+  if constexpr (kFma) return __builtin_fma(a, b, c);
+  else return c + a * b;
+}
+template <>
+__device__ __forceinline__ float madd<float, true>(float a, float b, float c) {
+  return __builtin_fmaf(a, b, c);
+}
+
+// Value e of a lane-distributed matrix (lane e%64 of register e/64), broadcast
+// to the wave; e is a compile-time constant after unrolling.
+template <typename T, int R>
+__device__ __forceinline__ T bcast(const T (&M)[R], int e) {
+  if constexpr (sizeof(T) == 8) {
+    const long long v = __builtin_bit_cast(long long, M[e >> 6]);
+    const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), e & 63);
+    const int hi = __builtin_amdgcn_readlane((int)(v >> 32), e & 63);
+    return __builtin_bit_cast(T, ((long long)hi << 32) | (unsigned int)lo);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, M[e >> 6]), e & 63));
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void load20(const T *__restrict__ p, T (&v)[20]) {
+  if constexpr (sizeof(T) == 8) {
+    const f64x2 *q = reinterpret_cast<const f64x2 *>(p);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const f64x2 t = __builtin_nontemporal_load(q + i);
+      v[2 * i] = t.x;
+      v[2 * i + 1] = t.y;
+    }
+  } else {
+    const f32x4 *q = reinterpret_cast<const f32x4 *>(p);
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const f32x4 t = __builtin_nontemporal_load(q + i);
+      v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store20(T *__restrict__ p, const T (&v)[20]) {
+  if constexpr (sizeof(T) == 8) {
+    f64x2 *q = reinterpret_cast<f64x2 *>(p);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      f64x2 t = {v[2 * i], v[2 * i + 1]};
+      __builtin_nontemporal_store(t, q + i);
+    }
+  } else {
+    f32x4 *q = reinterpret_cast<f32x4 *>(p);
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      f32x4 t = {v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+      __builtin_nontemporal_store(t, q + i);
+    }
+  }
+}
+
+// One 64-site tile of one child through LDS: the block's 256 threads load the
+// tile's 64 x 80 values with coalesced 16-B (non-temporal) loads and store them
+// at chunk (site*41 + chunk) -- one pad chunk per site makes every lane's
+// ds_read_b128 of its own (site, category) row bank-conflict-free.
+template <typename T>
+struct ProtTile {
+  static constexpr int kChunksPerSite = 80 * (int)sizeof(T) / 16;  // 40 (f64) / 20 (f32)
+  static constexpr int kStride = kChunksPerSite + 1;
+  static constexpr int kChunks = 64 * kChunksPerSite;
+  typedef typename std::conditional<sizeof(T) == 8, f64x2, f32x4>::type V;
+};
+
+template <typename T>
+__device__ __forceinline__ void tile_load(const T *__restrict__ g, int64_t base, int64_t n,
+                                          typename ProtTile<T>::V *lds) {
+  using PT = ProtTile<T>;
+  const typename PT::V *src = reinterpret_cast<const typename PT::V *>(g + base * 80);
+  const int64_t lim = (n - base) * PT::kChunksPerSite;  // chunks of valid sites
+#pragma unroll
+  for (int i = 0; i < PT::kChunks / kBlock; i++) {
+    const int j = threadIdx.x + i * kBlock;
+    const int s = j / PT::kChunksPerSite, q = j - s * PT::kChunksPerSite;
+    typename PT::V v = {};
+    if (j < lim) v = __builtin_nontemporal_load(src + j);
+    lds[s * PT::kStride + q] = v;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void tile_store(T *__restrict__ g, int64_t base, int64_t n,
+                                           const typename ProtTile<T>::V *lds) {
+  using PT = ProtTile<T>;
+  typename PT::V *dst = reinterpret_cast<typename PT::V *>(g + base * 80);
+  const int64_t lim = (n - base) * PT::kChunksPerSite;
+#pragma unroll
+  for (int i = 0; i < PT::kChunks / kBlock; i++) {
+    const int j = threadIdx.x + i * kBlock;
+    const int s = j / PT::kChunksPerSite, q = j - s * PT::kChunksPerSite;
+    if (j < lim) __builtin_nontemporal_store(lds[s * PT::kStride + q], dst + j);
+  }
+}
+
+// this lane's (site, category) row of 20 values <-> the LDS tile
+template <typename T>
+__device__ __forceinline__ void row_read(const typename ProtTile<T>::V *lds, int site, int c,
+                                         T (&v)[20]) {
+  using PT = ProtTile<T>;
+  const typename PT::V *r = lds + site * PT::kStride + c * (PT::kChunksPerSite / 4);
+  if constexpr (sizeof(T) == 8) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) { const f64x2 t = r[i]; v[2 * i] = t.x; v[2 * i + 1] = t.y; }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const f32x4 t = r[i];
+      v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void row_write(typename ProtTile<T>::V *lds, int site, int c,
+                                          const T (&v)[20]) {
+  using PT = ProtTile<T>;
+  typename PT::V *r = lds + site * PT::kStride + c * (PT::kChunksPerSite / 4);
+  if constexpr (sizeof(T) == 8) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) r[i] = f64x2{v[2 * i], v[2 * i + 1]};
+  } else {
+#pragma unroll
+    for (int i = 0; i < 5; i++) r[i] = f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+  }
+}
+
+// kAblate (tuning only, tools/tune_plf.hip): 0 = the kernel; 1 = skip the
+// arithmetic (o = a + b); 2 = skip the child-tile traffic (a, b synthesised).
+template <typename T, bool kFma, bool kSum, int kAblate = 0>
+__global__ void __launch_bounds__(kBlock)
+plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
+                const T *__restrict__ EV, const T *__restrict__ left, const T *__restrict__ right,
+                const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                unsigned long long *ws, int64_t *scaler_sum) {
+  constexpr int S = 20;
+  using PT = ProtTile<T>;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform category
+  const int lane = threadIdx.x & 63;
+  constexpr int R = (S * S + 63) / 64;  // registers per lane-distributed matrix
+  T ML[R], MR[R], ME[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int e = r * 64 + lane;
+    ML[r] = e < S * S ? left[c * S * S + e] : T(0);
+    MR[r] = e < S * S ? right[c * S * S + e] : T(0);
+    ME[r] = e < S * S ? EV[e] : T(0);
+  }
+  const T m = Num<T>::minlik();
+  __shared__ typename PT::V tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock];
+  long long acc = 0;
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+    const int64_t site = base + lane;
+    const bool valid = site < n;
+    T a[S], b[S], o[S];
+    if constexpr (kAblate == 2) {
+#pragma unroll
+      for (int l = 0; l < S; l++) { a[l] = T(site + l) * T(1e-3); b[l] = T(lane + l) * T(1e-3); }
+    } else {
+      tile_load<T>(x1, base, n, tile);
+      __syncthreads();
+      row_read<T>(tile, lane, c, a);
+      __syncthreads();
+      tile_load<T>(x2, base, n, tile);
+      __syncthreads();
+      row_read<T>(tile, lane, c, b);
+    }
+#pragma unroll
+    for (int l = 0; l < S; l++) o[l] = kAblate == 1 ? a[l] + b[l] : T(0);
+#pragma unroll
+    for (int k = 0; k < (kAblate == 1 ? 0 : S); k++) {
+      T u1 = T(0), u2 = T(0);
+#pragma unroll
+      for (int l = 0; l < S; l++) {
+        u1 = madd<T, kFma>(a[l], bcast<T>(ML, k * S + l), u1);
+        u2 = madd<T, kFma>(b[l], bcast<T>(MR, k * S + l), u2);
+      }
+      const T p = u1 * u2;
+#pragma unroll
+      for (int l = 0; l < S; l++) o[l] = madd<T, kFma>(p, bcast<T>(ME, k * S + l), o[l]);
+    }
+    bool small = valid;
+#pragma unroll
+    for (int l = 0; l < S; l++) small = small && (Num<T>::abs(o[l]) < m);
+    const unsigned long long mk = __ballot(small);
+    if (lane == 0) small_mask[c] = mk;
+    __syncthreads();  // also: every wave is done reading x2 from the tile
+    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+    const bool sc = (all >> lane) & 1ull;
+#pragma unroll
+    for (int l = 0; l < S; l++) {
+      const T sv = o[l] * Num<T>::two32();
+      o[l] = sc ? sv : o[l];
+    }
+    row_write<T>(tile, lane, c, o);
+    if (valid && c == 0) {
+      if (scaler) scaler[site] = (uint8_t)sc;
+      if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+    }
+    __syncthreads();
+    if constexpr (kAblate != 2) tile_store<T>(x3, base, n, tile);
+    __syncthreads();  // tile and small_mask are reused by the next trip
+  }
+  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
+}  // namespace dev
+}  // namespace plfx

@@ -245,6 +245,36 @@ int plfx_plf_dev_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *
   return plf_dev<double>(ctx, x1, x2, x3, EV, n, left, right, wgt, scaler, scaler_sum, stream);
 }
 
+int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void *x1,
+                     const void *x2, void *x3, const void *EV, int64_t n, const void *left,
+                     const void *right, const int32_t *wgt, uint8_t *scaler,
+                     int64_t *scaler_sum, void *stream) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if (flags & ~PLFX_FMA) return fail(ctx, PLFX_ERR_INVALID, "bad flags %d", flags);
+  if (states == 4) {
+    return dtype == PLFX_F32
+               ? plf_dev<float>(ctx, (const float *)x1, (const float *)x2, (float *)x3,
+                                (const float *)EV, n, (const float *)left, (const float *)right,
+                                wgt, scaler, scaler_sum, stream)
+               : plf_dev<double>(ctx, (const double *)x1, (const double *)x2, (double *)x3,
+                                 (const double *)EV, n, (const double *)left,
+                                 (const double *)right, wgt, scaler, scaler_sum, stream);
+  }
+  if (states != 20) return fail(ctx, PLFX_ERR_UNSUPPORTED, "states=%d not built (4, 20)", states);
+  int rc = check_dev_args(ctx, x1, x2, x3, EV, n, left, right);
+  if (rc != PLFX_OK) return rc;
+  hipStream_t s = pick(ctx, stream);
+  if (n == 0) {
+    if (scaler_sum) PLFX_HIP(ctx, hipMemsetAsync(scaler_sum, 0, sizeof(int64_t), s));
+    return PLFX_OK;
+  }
+  plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, ctx->ws, n};
+  hipError_t e = plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s);
+  if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot launch");
+  return PLFX_OK;
+}
+
 int plfx_instance_run(plfx_ctx *ctx, const void *in_left, const void *in_right, void *out_clv,
                       uint8_t *out_scaler, uint32_t alignment_sites, uint32_t window_size,
                       int layout, int dtype, void *stream) {

@@ -47,8 +47,9 @@ EXPORTS = (
     "plfx_tb_instance_elements_out",
     "plfx_tb_instance_active_elements_left", "plfx_tb_instance_active_elements_right",
     "plfx_tb_num_windows_per_instance", "plfx_pack_instance",
-    "plfx_plf_batch_dev", "plfx_traverse", "plfx_root_lnl",
+    "plfx_plf_batch_dev", "plfx_traverse", "plfx_root_lnl", "plfx_plf_dev_gen",
 )
+EXACT, FMA = 0, 1
 
 
 class PlfxError(RuntimeError):
@@ -116,6 +117,7 @@ def load():
         f.argtypes = [tbp]
         f.restype = C.c_uint64
     L.plfx_pack_instance.argtypes = [tbp, i32, i32, vp, vp, vp, vp, vp, vp, vp]
+    L.plfx_plf_dev_gen.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
     L.plfx_plf_batch_dev.argtypes = [vp, i32, i32, C.POINTER(Node), i32, vp, i64, vp, vp]
     L.plfx_traverse.argtypes = [vp, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp), i32, vp, i32,
                                 vp, i64, vp, C.POINTER(vp), vp, vp]
@@ -270,6 +272,38 @@ class Context:
                                               p(out_scaler), n, int(window_size), int(layout),
                                               F32 if dt == torch.float32 else F64,
                                               _stream_handle(stream)))
+
+    def plf_dev_gen(self, x1, x2, x3, EV, left, right, states, wgt=None, scaler=None,
+                    scaler_sum=None, n=None, fma=False, stream=None):
+        """Any built state count (4 DNA, 20 protein), 4 Gamma categories, on
+        torch device tensors: x[site][cat][state], P [cat][k][l], EV [k][l]."""
+        import torch
+
+        V = 4 * states
+        dt = x1.dtype
+        if dt not in (torch.float32, torch.float64):
+            raise PlfxError(ERR_INVALID, f"unsupported dtype {dt}")
+        if n is None:
+            n = x1.numel() // V
+        n = int(n)
+        for t in (x1, x2, x3, EV, left, right):
+            if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
+                raise PlfxError(ERR_INVALID, "tensors must be contiguous device tensors of one dtype")
+        if min(x1.numel(), x2.numel(), x3.numel()) < V * n:
+            raise PlfxError(ERR_INVALID, "CLV tensors shorter than 4*states*n")
+        if EV.numel() < states * states or min(left.numel(), right.numel()) < 4 * states * states:
+            raise PlfxError(ERR_INVALID, "EV needs S*S, left/right 4*S*S values")
+        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n):
+            raise PlfxError(ERR_INVALID, "wgt must be int32 with >= n elements")
+        if scaler is not None and (scaler.dtype != torch.uint8 or scaler.numel() < n):
+            raise PlfxError(ERR_INVALID, "scaler must be uint8 with >= n elements")
+        if scaler_sum is not None and scaler_sum.dtype != torch.int64:
+            raise PlfxError(ERR_INVALID, "scaler_sum must be int64")
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+        self._check(self._L.plfx_plf_dev_gen(self.h, F32 if dt == torch.float32 else F64, int(states),
+                                             FMA if fma else EXACT, p(x1), p(x2), p(x3), p(EV), n,
+                                             p(left), p(right), p(wgt), p(scaler), p(scaler_sum),
+                                             _stream_handle(stream)))
 
     # -- (6) batched nodes / traversal ---------------------------------------
     def plf_batch_dev(self, nodes, EV, n, wgt=None, stream=None):

@@ -69,7 +69,8 @@ def parse():
     ap.add_argument("--sites", type=int, default=1 << 20)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--buffer-sets", type=int, default=4)
-    ap.add_argument("--workload", choices=["node", "tree64", "nodes64"], default="node",
+    ap.add_argument("--fma", action="store_true", help="protein: fused multiply-add mode")
+    ap.add_argument("--workload", choices=["node", "tree64", "nodes64", "protein"], default="node",
                     help="node: BASELINE configs[1] (headline); tree64: configs[2]; "
                          "nodes64: the per-GPU shard of configs[3]")
     ap.add_argument("--launch", choices=["bound", "checked", "graph"], default="graph",
@@ -275,6 +276,51 @@ class Nodes64Workload:
         return {"lnl_all_nodes_all_ranks": float(tot[0]), "scaler_events_all_ranks": int(tot[1])}
 
 
+class ProteinWorkload:
+    """BASELINE configs[4]: one protein inner node (S=20 states x 4 Gamma
+    categories) of n sites (default 2^18) per GPU per step, rotating buffer sets."""
+
+    def __init__(self, ctx, a, dev, g, tdt, esz):
+        import torch
+
+        n = a.sites if a.sites != (1 << 20) else (1 << 18)
+        R = max(1, a.buffer_sets)
+        V = 80
+        self.n, self.R, self.ctx, self.fma = n, R, ctx, a.fma
+        self.EV = torch.rand(400, dtype=tdt, device=dev, generator=g) - 0.25
+        self.left = torch.rand(1600, dtype=tdt, device=dev, generator=g)
+        self.right = torch.rand(1600, dtype=tdt, device=dev, generator=g)
+        self.sets = []
+        for _ in range(R):
+            x1 = torch.rand(n * V, dtype=tdt, device=dev, generator=g)
+            x1.view(-1, V)[0::4] *= 1e-14
+            self.sets.append(dict(x1=x1, x2=torch.rand(n * V, dtype=tdt, device=dev, generator=g),
+                                  x3=torch.empty_like(x1),
+                                  wgt=torch.ones(n, dtype=torch.int32, device=dev),
+                                  sc=torch.empty(n, dtype=torch.uint8, device=dev),
+                                  s=torch.zeros(1, dtype=torch.int64, device=dev)))
+        self.sites_per_step = n
+        self.bytes_per_site = 3 * V * esz + 1 + 4
+        self.bytes_per_step = self.bytes_per_site * n
+        self.config = {
+            "workload": f"Protein 20-state x 4 Gamma cats, 1 inner node per GPU per step, {n} sites, "
+                        f"{a.dtype}, {'FMA' if a.fma else 'exact'} (BASELINE configs[4])",
+            "sites_per_gpu_per_step": n, "nodes_per_gpu_per_step": 1, "buffer_sets": R}
+
+    def step(self, i, sh):
+        b = self.sets[i % self.R]
+        self.ctx.plf_dev_gen(b["x1"], b["x2"], b["x3"], self.EV, self.left, self.right, 20,
+                             b["wgt"], b["sc"], b["s"], fma=self.fma, stream=sh)
+
+    def check(self):
+        import torch
+
+        return torch.stack([b["s"][0] for b in self.sets]).sum(), self.R * ((self.n + 3) // 4)
+
+    def post(self, world, dev):
+        return {}
+
+
 def _balanced_ops(ntips):
     ops, level, nxt = [], list(range(ntips)), ntips
     while len(level) > 1:
@@ -287,7 +333,8 @@ def _balanced_ops(ntips):
     return ops
 
 
-WORKLOADS = {"node": NodeWorkload, "tree64": Tree64Workload, "nodes64": Nodes64Workload}
+WORKLOADS = {"node": NodeWorkload, "tree64": Tree64Workload, "nodes64": Nodes64Workload,
+             "protein": ProteinWorkload}
 
 
 def main():

@@ -111,6 +111,21 @@ int plfx_plf_dev_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *
                      const double *right, const int32_t *wgt, uint8_t *scaler,
                      int64_t *scaler_sum, void *stream);
 
+/* ---- (2b) any state count (extension: BASELINE configs[4], protein) ------ */
+/* states = 4 (DNA, the kernels above) or 20 (protein); 4 Gamma categories.
+ * Layout generalises plf(): x[site*4S + cat*S + state], left/right
+ * [cat][k][l] (S*S per category), EV[k][l] (S*S).  flags: PLFX_EXACT keeps
+ * plf()'s separate multiply/add and operation order (bit-identical to the
+ * double/float instantiation of the reference loop); PLFX_FMA fuses each
+ * multiply-add (one rounding per term, within 1e-12 relative; protein only,
+ * DNA is always exact). */
+#define PLFX_EXACT 0
+#define PLFX_FMA 1
+int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void *x1,
+                     const void *x2, void *x3, const void *EV, int64_t n, const void *left,
+                     const void *right, const int32_t *wgt, uint8_t *scaler,
+                     int64_t *scaler_sum, void *stream);
+
 /* ---- (3) the accelerator instance-buffer contract ----------------------- */
 /* in_left/in_right/out_clv/out_scaler: device buffers exactly as the
  * reference packs them (host_mem.cpp:221-243): in_left = [EV 16 | P_L 64 |

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "plf_dna.hpp"
+#include "plf_prot.hpp"
 
 using namespace plfx::dev;
 
@@ -168,6 +169,27 @@ int main(int argc, char **argv) {
   ADD_PAIRN(2, 1, 2, false, true) ADD_PAIRN(4, 1, 1, true, true) ADD_PAIRN(4, 1, 2, true, true)
 
 
+  // protein (S=20) ablations on the same buffers: a 640-B protein site record
+  // fits n*128/640 = n/5 times in the 128-B-per-DNA-site allocations
+  const int64_t np = n / 5;
+  if (np * 640 > n * 128) { printf("protein tile does not fit\n"); return 1; }
+#define ADD_PROT(FMA, AB)                                                                          \
+  {                                                                                                \
+    auto k = &plf_prot_kernel<double, FMA, true, AB>;                                              \
+    int res = occ((const void *)k) * CUs;                                                          \
+    int64_t grid = std::min<int64_t>((np + 63) / 64, res);                                         \
+    char nm[160]; snprintf(nm, sizeof nm, "prot fma=%d ablate=%d occ=%d/CU grid=%lld (n=%lld)", FMA, AB, \
+                           occ((const void *)k), (long long)grid, (long long)np);                  \
+    vs.push_back({nm, [=](const Set &s) {                                                          \
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, PEV, PL, PR,  \
+                         s.wgt, s.sc, np, ws, s.sum); }, {}});                                     \
+  }
+  double *PEV, *PL, *PR;
+  CK(hipMalloc(&PEV, 400 * 8)); CK(hipMalloc(&PL, 1600 * 8)); CK(hipMalloc(&PR, 1600 * 8));
+  fill<<<8, 64>>>(PEV, 400, 7, 1.0); fill<<<32, 64>>>(PL, 1600, 8, 1.0); fill<<<32, 64>>>(PR, 1600, 9, 1.0);
+  CK(hipDeviceSynchronize());
+  ADD_PROT(false, 0) ADD_PROT(true, 0) ADD_PROT(false, 1) ADD_PROT(false, 2) ADD_PROT(true, 2)
+
   for (int round = 0; round < rounds; round++) {
     for (auto &v : vs) {
       for (int i = 0; i < 5; i++) v.run(sets[i % R]);
@@ -184,7 +206,11 @@ int main(int argc, char **argv) {
          rounds, R, n * 389.0 / 1048576);
   for (auto &v : vs) {
     std::sort(v.us.begin(), v.us.end());
-    const double bytes = (v.name.rfind("copy", 0) == 0 ? 256.0 : (v.name.rfind("stream3", 0) == 0 && v.name.find("wgt") == std::string::npos) ? 384.0 : 389.0) * n;
+    double per_site = 389.0;  // bytes per DNA site of the run (protein: per 1/5 site)
+    if (v.name.rfind("prot", 0) == 0) per_site = 1925.0 / 5;
+    else if (v.name.rfind("copy", 0) == 0) per_site = 256.0;
+    else if (v.name.rfind("stream3", 0) == 0 && v.name.find("wgt") == std::string::npos) per_site = 384.0;
+    const double bytes = per_site * n;
     printf("%-62s median %8.2f us  min %8.2f us  %7.0f GB/s  %5.1f%% of 8 TB/s  %6.2f Gsites/s\n",
            v.name.c_str(), v.us[v.us.size() / 2], v.us[0], bytes / (v.us[v.us.size() / 2] * 1e-6) / 1e9,
            100.0 * bytes / (v.us[v.us.size() / 2] * 1e-6) / 8e12, n / (v.us[v.us.size() / 2] * 1e-6) / 1e9);
