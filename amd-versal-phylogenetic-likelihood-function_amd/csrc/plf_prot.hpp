@@ -252,5 +252,134 @@ plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restric
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
 
+// ---------------------------------------------------------------------------
+// FMA mode on the matrix cores (f64).  v_mfma_f64_16x16x4_f64 is bit-for-bit a
+// k-ordered fma chain (probed on MI355X: tools/probes/mfma_f64_numerics.hip),
+// so this kernel reproduces plf()'s loop with every multiply-add fused, in the
+// same order -- identical to the VALU FMA kernel above and to the oracle's
+// fma() restatement.  Per category (wave) and 16-site sub-tile:
+//   U^T[k][site]   = P[k][l]  . X^T[l][site]   (M = k: 2 tiles, N = 16 sites,
+//                                               K = l: 5 steps of 4)
+//   p              = U_L^T * U_R^T             (accumulator registers, VALU)
+//   X3^T[l][site]  = EV^T[l][k] . p[k][site]   (the accumulators of the first
+//                                               product ARE the B fragments:
+//                                               k-step s = tile s>>2, reg s&3)
+// A fragments (P rows, EV columns, zero-padded to 32) stay in VGPRs for the
+// whole kernel; B fragments (X^T) come from the LDS tile, conflict-free.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+template <bool kSum, int kMinWaves = 2>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                     double *__restrict__ x3, const double *__restrict__ EV,
+                     const double *__restrict__ left, const double *__restrict__ right,
+                     const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                     unsigned long long *ws, int64_t *scaler_sum) {
+  constexpr int S = 20;
+  using PT = ProtTile<double>;
+  constexpr int kRow = 2 * PT::kStride;  // doubles per site in the LDS tile (82)
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lo16 = lane & 15, g = lane >> 4;
+  // A fragments: [mt][s] -> lane holds M[row = 16mt + lo16][col = 4s + g]
+  double AL[2][5], AR[2][5], AE[2][5];
+#pragma unroll
+  for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+    for (int st = 0; st < 5; st++) {
+      const int row = 16 * mt + lo16, col = 4 * st + g;
+      AL[mt][st] = row < S ? left[c * S * S + row * S + col] : 0.0;   // P_L[k=row][l=col]
+      AR[mt][st] = row < S ? right[c * S * S + row * S + col] : 0.0;
+      AE[mt][st] = row < S ? EV[col * S + row] : 0.0;                // EV^T[l=row][k=col]
+    }
+  const double m = Num<double>::minlik();
+  __shared__ f64x2 tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock];
+  const double *td = reinterpret_cast<const double *>(tile);
+  double *tw = reinterpret_cast<double *>(tile);
+  long long acc = 0;
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+    f64x4 P[4][2];  // per sub-tile: U_L^T, then p = U_L^T * U_R^T
+    tile_load<double>(x1, base, n, tile);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
+#pragma unroll
+      for (int mt = 0; mt < 2; mt++) {
+        f64x4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 5; st++) u = __builtin_amdgcn_mfma_f64_16x16x4f64(AL[mt][st], xr[4 * st], u, 0, 0, 0);
+        P[t][mt] = u;
+      }
+    }
+    __syncthreads();
+    tile_load<double>(x2, base, n, tile);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
+#pragma unroll
+      for (int mt = 0; mt < 2; mt++) {
+        f64x4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 5; st++) u = __builtin_amdgcn_mfma_f64_16x16x4f64(AR[mt][st], xr[4 * st], u, 0, 0, 0);
+        P[t][mt] = P[t][mt] * u;  // prod[k] = umpL[k] * umpR[k]
+      }
+    }
+    __syncthreads();  // every wave is done reading x2: the tile takes X3 now
+    // back-transform: lane holds X3[site 16t+lo16][l = 16mt + g + 4r]; written
+    // unscaled into the tile, the x2^32 rescale happens in the store pass
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      f64x4 X0 = {0.0, 0.0, 0.0, 0.0}, X1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int st = 0; st < 5; st++) {
+        X0 = __builtin_amdgcn_mfma_f64_16x16x4f64(AE[0][st], P[t][st >> 2][st & 3], X0, 0, 0, 0);
+        X1 = __builtin_amdgcn_mfma_f64_16x16x4f64(AE[1][st], P[t][st >> 2][st & 3], X1, 0, 0, 0);
+      }
+      const bool small = (__builtin_fabs(X0[0]) < m) && (__builtin_fabs(X0[1]) < m) &&
+                         (__builtin_fabs(X0[2]) < m) && (__builtin_fabs(X0[3]) < m) &&
+                         (__builtin_fabs(X1[0]) < m);
+      const unsigned long long b = __ballot(small);
+      // site lo16 of sub-tile t is small in category c iff its 4 lanes agree
+      mine |= (b & (b >> 16) & (b >> 32) & (b >> 48) & 0xFFFFull) << (16 * t);
+      double *w = tw + (16 * t + lo16) * kRow + c * S;
+#pragma unroll
+      for (int r = 0; r < 4; r++) w[g + 4 * r] = X0[r];
+      w[16 + g] = X1[0];
+    }
+    if (lane == 0) small_mask[c] = mine;
+    __syncthreads();
+    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+    if (c == 0) {
+      const int64_t site = base + lane;
+      const bool sc = (all >> lane) & 1ull;
+      if (site < n) {
+        if (scaler) scaler[site] = (uint8_t)sc;
+        if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+      }
+    }
+    // coalesced store with the rescale of the scaled sites (exact: x 2^32)
+    {
+      f64x2 *dst = reinterpret_cast<f64x2 *>(x3 + base * 80);
+      const int64_t lim = (n - base) * PT::kChunksPerSite;
+#pragma unroll
+      for (int i = 0; i < PT::kChunks / kBlock; i++) {
+        const int j = threadIdx.x + i * kBlock;
+        const int sl = j / PT::kChunksPerSite, q = j - sl * PT::kChunksPerSite;
+        if (j < lim) {
+          f64x2 v = tile[sl * PT::kStride + q];
+          if ((all >> sl) & 1ull) v = v * Num<double>::two32();
+          __builtin_nontemporal_store(v, dst + j);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
 }  // namespace dev
 }  // namespace plfx

@@ -86,6 +86,10 @@ def lib():
             f.argtypes = [C.c_int, C.c_int, fp, fp, fp, fp, C.c_longlong, fp, fp,
                           C.c_void_p, C.POINTER(C.c_longlong), C.c_void_p]
             f.restype = None
+            f = getattr(L, f"plfo_plf_gen_fma_{sfx}")
+            f.argtypes = [C.c_int, C.c_int, fp, fp, fp, fp, C.c_longlong, fp, fp,
+                          C.c_void_p, C.POINTER(C.c_longlong), C.c_void_p]
+            f.restype = None
             f = getattr(L, f"plfo_gen_hostmem_{sfx}")
             f.argtypes = [C.c_uint32, C.c_longlong, fp, fp, fp, fp, fp, C.c_void_p]
             f.restype = None
@@ -158,9 +162,10 @@ def plf(x1, x2, EV, left, right, wgt=None, n=None, threads=0, out=None):
     return x3, sc, inc.value
 
 
-def plf_generic(S, Ccat, x1, x2, EV, left, right, wgt=None):
+def plf_generic(S, Ccat, x1, x2, EV, left, right, wgt=None, fma=False):
     """Generic S-state / C-category restatement (protein S=20): unpinned
-    extension; identical to plf() for S=C=4."""
+    extension; identical to plf() for S=C=4.  fma=True: every multiply-add
+    fused in the same order (the PLFX_FMA mode)."""
     dt = x1.dtype
     V = S * Ccat
     n = x1.size // V
@@ -169,8 +174,8 @@ def plf_generic(S, Ccat, x1, x2, EV, left, right, wgt=None):
     inc = C.c_longlong(0)
     if wgt is not None:
         wgt = np.ascontiguousarray(wgt, dtype=np.int32)
-    getattr(lib(), f"plfo_plf_gen_{_sfx(dt)}")(S, Ccat, x1, x2, x3, EV, n, left, right,
-                                               _ptr(wgt), C.byref(inc), _ptr(sc))
+    name = f"plfo_plf_gen_fma_{_sfx(dt)}" if fma else f"plfo_plf_gen_{_sfx(dt)}"
+    getattr(lib(), name)(S, Ccat, x1, x2, x3, EV, n, left, right, _ptr(wgt), C.byref(inc), _ptr(sc))
     return x3, sc, inc.value
 
 

@@ -165,6 +165,47 @@ PLFO_DEFINE_DNA(f64, double)
 PLFO_DEFINE_GEN(f32, float)
 PLFO_DEFINE_GEN(f64, double)
 
+/* The same loop with every multiply-add fused (fma(): one rounding per term),
+ * in plf()'s order: the reference for the PLFX_FMA mode (extension). */
+#define PLFO_DEFINE_GEN_FMA(SUFFIX, T, FMA)                                        \
+  void plfo_plf_gen_fma_##SUFFIX(int S, int C, const T *x1s, const T *x2s, T *x3s, \
+                                 const T *EV, long long n, const T *left,          \
+                                 const T *right, const int *wgt,                   \
+                                 long long *scalerIncrement, unsigned char *scaler) { \
+    long long i, addScale = 0;                                                     \
+    T p[64];                                                                       \
+    const int V = S * C;                                                           \
+    for (i = 0; i < n; i++) {                                                      \
+      const T *x1 = x1s + i * V;                                                   \
+      const T *x2 = x2s + i * V;                                                   \
+      T *x3 = x3s + i * V;                                                         \
+      int j, k, l, sc;                                                             \
+      for (j = 0; j < V; j++) x3[j] = (T)0.0;                                      \
+      for (j = 0; j < C; j++) {                                                    \
+        for (k = 0; k < S; k++) {                                                  \
+          T u1 = (T)0.0, u2 = (T)0.0;                                              \
+          for (l = 0; l < S; l++) {                                                \
+            u1 = FMA(x1[j * S + l], left[(j * S + k) * S + l], u1);                \
+            u2 = FMA(x2[j * S + l], right[(j * S + k) * S + l], u2);               \
+          }                                                                        \
+          p[k] = u1 * u2;                                                          \
+        }                                                                          \
+        for (k = 0; k < S; k++)                                                    \
+          for (l = 0; l < S; l++) x3[j * S + l] = FMA(p[k], EV[S * k + l], x3[j * S + l]); \
+      }                                                                            \
+      sc = 1;                                                                      \
+      for (l = 0; sc && l < V; l++) sc = (fabs((double)x3[l]) < PLFO_MINLIK);      \
+      if (sc)                                                                      \
+        for (l = 0; l < V; l++) x3[l] = (T)((double)x3[l] * PLFO_TWO_TO_32);       \
+      if (scaler) scaler[i] = (unsigned char)sc;                                   \
+      if (sc) addScale += wgt ? wgt[i] : 1;                                        \
+    }                                                                              \
+    if (scalerIncrement) *scalerIncrement = addScale;                              \
+  }
+
+PLFO_DEFINE_GEN_FMA(f32, float, fmaf)
+PLFO_DEFINE_GEN_FMA(f64, double, fma)
+
 /* Host-side scaler reduction, app/src/host_mem.cpp:384-388. */
 long long plfo_scaler_sum(const unsigned char *scaler, const int *wgt, long long n) {
   long long s = 0, j;

@@ -62,16 +62,23 @@ def test_protein_exact_matches_oracle(ctx, oracle, dtype, n):
     assert esc.sum() > 0 or n < 4
 
 
-@pytest.mark.parametrize("dtype", [np.float64])
-def test_protein_fma_within_tolerance(ctx, oracle, dtype):
-    n = 4097
-    x1, x2, EV, left, right, w = gen(n, dtype, 5)
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("n", [1, 17, 64, 100, 4097])
+def test_protein_fma_mode(ctx, oracle, dtype, n):
+    """FMA mode (f64: matrix cores, v_mfma_f64_16x16x4 = k-ordered fma chain;
+    f32: fused VALU) is bit-identical to the oracle's fma() restatement and
+    within 1e-12 (f64) of the unfused loop."""
+    x1, x2, EV, left, right, w = gen(n, dtype, 5 + n)
     x3, sc, s = run(ctx, x1, x2, EV, left, right, w, n, fma=True)
-    e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w)
-    assert np.array_equal(sc, esc) and s == einc
-    scale = np.abs(e3).reshape(n, V).max(axis=1, keepdims=True)   # cancellation-aware bound
-    err = np.abs(x3 - e3).reshape(n, V) / scale
-    assert err.max() <= FMA_RTOL
+    f3, fsc, finc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
+    assert np.array_equal(bits(x3), bits(f3))
+    assert np.array_equal(sc, fsc) and s == finc
+    if dtype == np.float64:
+        e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w)
+        assert np.array_equal(sc, esc) and s == einc
+        scale = np.abs(e3).reshape(n, V).max(axis=1, keepdims=True)   # cancellation-aware bound
+        err = np.abs(x3 - e3).reshape(n, V) / scale
+        assert err.max() <= FMA_RTOL
 
 
 def test_protein_full_size_256k(ctx, oracle):
