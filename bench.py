@@ -45,12 +45,24 @@ def bytes_per_site(dtype_bytes):
     return 3 * 16 * dtype_bytes + 1 + 4
 
 
+def coll_device(device):
+    """Device for collective tensors: the GPU under RCCL, the CPU under gloo."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    return device
+
+
 def combine_ranks(wall_ms, dev_ms, got_sum, expect_sum, device, world):
     """Cross-rank reduction of one bench run: MAX of the timed-region wall and
     device times (the driver contract) and ONE all-reduce (RCCL on GPUs, gloo in
     the CPU tests) of the scaler totals.  Returns (wall_ms, dev_ms, check_ok)."""
     import torch
     import torch.distributed as dist
+
+    device = coll_device(device)
 
     t = torch.tensor([wall_ms, dev_ms], dtype=torch.float64, device=device)
     tot = torch.stack([got_sum.to(device=device, dtype=torch.int64).reshape(()),
@@ -270,7 +282,7 @@ class Nodes64Workload:
         for j, nd in enumerate(self.nodes):
             self.ctx.root_lnl(nd["x3"], self.n, lnl[j:j + 1], wgt=self.wgt,
                               scaler_sums=self.sums[j:j + 1])
-        tot = torch.stack([lnl.sum(), self.sums.sum().to(torch.float64)])
+        tot = torch.stack([lnl.sum(), self.sums.sum().to(torch.float64)]).to(coll_device(dev))
         if world > 1:
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)  # the one lnL all-reduce (RCCL over xGMI)
         return {"lnl_all_nodes_all_ranks": float(tot[0]), "scaler_events_all_ranks": int(tot[1])}
@@ -347,10 +359,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world:
         sys.exit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; LOCAL_RANK folds onto the visible devices so the
+    # multi-rank path can be rehearsed on fewer GPUs (PLFX_DIST_BACKEND=gloo)
+    ngpu = torch.cuda.device_count()
+    local_dev = local % max(ngpu, 1)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("PLFX_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
@@ -358,7 +378,7 @@ def main():
 
     import plfx
 
-    ctx = plfx.Context(local)
+    ctx = plfx.Context(local_dev)
     tdt = torch.float64 if a.dtype == "f64" else torch.float32
     esz = 8 if a.dtype == "f64" else 4
     g = torch.Generator(device=dev)
