@@ -110,10 +110,11 @@ int main(int argc, char **argv) {
   for (int r = 0; r < R; r++) {
     Set &s = sets[r];
     CK(hipMalloc(&s.x1, n * 128)); CK(hipMalloc(&s.x2, n * 128)); CK(hipMalloc(&s.x3, n * 128));
-    CK(hipMalloc(&s.wgt, n * 4)); CK(hipMalloc(&s.sc, n)); CK(hipMalloc(&s.sum, 8));
+    // wgt/scaler sized for the f32 variants' 2n sites
+    CK(hipMalloc(&s.wgt, 2 * n * 4)); CK(hipMalloc(&s.sc, 2 * n)); CK(hipMalloc(&s.sum, 8));
     fill<<<2048, 256>>>(s.x1, n * 16, 10 + r, 1e-12);
     fill<<<2048, 256>>>(s.x2, n * 16, 20 + r, 1.0);
-    std::vector<int> ones(n, 1); CK(hipMemcpy(s.wgt, ones.data(), n * 4, hipMemcpyHostToDevice));
+    std::vector<int> ones(2 * n, 1); CK(hipMemcpy(s.wgt, ones.data(), 2 * n * 4, hipMemcpyHostToDevice));
   }
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -169,6 +170,24 @@ int main(int argc, char **argv) {
   ADD_PAIRN(2, 1, 2, false, true) ADD_PAIRN(4, 1, 1, true, true) ADD_PAIRN(4, 1, 2, true, true)
 
 
+  // f32 DNA (lane = category) on the same buffers, 2n sites of 64 B
+#define ADD_F32(U, NT, MW, GM)                                                                     \
+  {                                                                                                \
+    auto k = &plf_dna_kernel<float, U, true, NT, MW>;                                              \
+    int res = occ((const void *)k) * CUs;                                                          \
+    const int64_t nf = 2 * n;                                                                      \
+    int64_t need = (nf + 64 * U - 1) / (64 * U);                                                   \
+    int64_t grid = GM > 0 ? std::min<int64_t>(need, (int64_t)res * GM) : need;                     \
+    char nm[160]; snprintf(nm, sizeof nm, "f32 U=%d nt=%d minw=%d occ=%d/CU grid=%lld", U, NT, MW, \
+                           occ((const void *)k), (long long)grid);                                 \
+    vs.push_back({nm, [=](const Set &s) {                                                          \
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, (const float *)s.x1,            \
+                         (const float *)s.x2, (float *)s.x3, (const float *)EV, (const float *)L,  \
+                         (const float *)Rm, s.wgt, s.sc, nf, ws, s.sum); }, {}});                  \
+  }
+  ADD_F32(4, false, 1, 1) ADD_F32(4, true, 1, 1) ADD_F32(2, true, 1, 1) ADD_F32(2, true, 1, 2)
+  ADD_F32(4, true, 1, 2) ADD_F32(8, true, 1, 1) ADD_F32(1, true, 1, 2) ADD_F32(2, false, 1, 2)
+
   // protein (S=20) ablations on the same buffers: a 640-B protein site record
   // fits n*128/640 = n/5 times in the 128-B-per-DNA-site allocations
   const int64_t np = n / 5;
@@ -208,6 +227,7 @@ int main(int argc, char **argv) {
     std::sort(v.us.begin(), v.us.end());
     double per_site = 389.0;  // bytes per DNA site of the run (protein: per 1/5 site)
     if (v.name.rfind("prot", 0) == 0) per_site = 1925.0 / 5;
+    else if (v.name.rfind("f32", 0) == 0) per_site = 2 * 197.0;  // 2n sites of 197 B
     else if (v.name.rfind("copy", 0) == 0) per_site = 256.0;
     else if (v.name.rfind("stream3", 0) == 0 && v.name.find("wgt") == std::string::npos) per_site = 384.0;
     const double bytes = per_site * n;
