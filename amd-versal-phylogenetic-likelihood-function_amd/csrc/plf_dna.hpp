@@ -120,6 +120,22 @@ __device__ __forceinline__ double dpp_f64(double x) {
 constexpr int kQuadEven = 0 | (0 << 2) | (2 << 4) | (2 << 6);  // quad_perm [0,0,2,2]
 constexpr int kQuadOdd = 1 | (1 << 2) | (3 << 4) | (3 << 6);   // quad_perm [1,1,3,3]
 
+// Tip children: a tip is one DNA state code per site (bit s
+// set = state s allowed, the RAxML/PLL convention); its dense CLV would be
+// x[c][s] = bit s of the code for every category c.  A block precomputes
+// tab[c*64 + code*4 + k] = sum_l bit_l(code) * P_c[k][l] in plf()'s order from
+// +0.0 (0.0/1.0 times P is exact), so a tip's ump values are one LDS read and
+// every result is bit-identical to running plf() on the expanded dense CLV.
+template <typename T>
+__device__ __forceinline__ void build_tip_table(const T *__restrict__ P, T *tab) {
+  const int t = threadIdx.x;  // kBlock == 256 == 4 cats x 16 codes x 4 k
+  const int cc = t >> 6, code = (t >> 2) & 15, k = t & 3;
+  T v = T(0);
+#pragma unroll
+  for (int l = 0; l < 4; l++) v += T((code >> l) & 1) * P[cc * 16 + k * 4 + l];
+  tab[t] = v;
+}
+
 // One site-category (4 values of x1, 4 of x2) -> 4 values of x3, before the
 // scale test.  plf.cpp:31-50: ump from +0.0 ascending l, product per k, x3 from
 // +0.0 ascending k.
@@ -146,20 +162,58 @@ __device__ __forceinline__ void site_cat(const T (&a)[4], const T (&b)[4], const
   }
 }
 
+// site_cat with tip children: a tip's ump[k] comes from its table row.
+template <typename T, bool T1, bool T2>
+__device__ __forceinline__ void site_cat_tips(const T (&a)[4], const T (&b)[4], const T (&PL)[16],
+                                              const T (&PR)[16], const T (&E)[16],
+                                              const T *row1, const T *row2, T (&o)[4]) {
+  T p[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    T u1 = T(0), u2 = T(0);
+    if constexpr (T1) {
+      u1 = row1[k];
+    } else {
+#pragma unroll
+      for (int l = 0; l < 4; l++) u1 += a[l] * PL[k * 4 + l];
+    }
+    if constexpr (T2) {
+      u2 = row2[k];
+    } else {
+#pragma unroll
+      for (int l = 0; l < 4; l++) u2 += b[l] * PR[k * 4 + l];
+    }
+    p[k] = u1 * u2;
+  }
+#pragma unroll
+  for (int l = 0; l < 4; l++) o[l] = T(0);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+#pragma unroll
+    for (int l = 0; l < 4; l++) o[l] += p[k] * E[4 * k + l];
+  }
+}
+
 // Knobs: U = 16-site wave steps per loop trip (bytes in flight per lane =
 // 2*U*4*sizeof(T)); NT = non-temporal CLV loads; kSum = produce the weighted
 // scaler sum; kMinWaves = __launch_bounds__ occupancy hint (waves per SIMD).
-template <typename T, int U, bool kSum, bool NT>
+template <typename T, int U, bool kSum, bool NT, bool T1 = false, bool T2 = false>
 __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *__restrict__ x2,
                                              T *__restrict__ x3, const T *__restrict__ EV,
                                              const T *__restrict__ left, const T *__restrict__ right,
                                              const int32_t *__restrict__ wgt,
                                              uint8_t *__restrict__ scaler, int64_t n,
-                                             unsigned long long *ws, int64_t *scaler_sum) {
+                                             unsigned long long *ws, int64_t *scaler_sum,
+                                             const uint8_t *__restrict__ tip1 = nullptr,
+                                             const uint8_t *__restrict__ tip2 = nullptr) {
   const int lane = threadIdx.x & 63;
   const int c = lane & 3;     // Gamma category owned by this lane
   const int q = lane >> 2;    // site slot within a 16-site wave step
   const int nib = lane & 60;  // bit offset of this site's nibble in the ballot
+  __shared__ T tab1[T1 ? 256 : 1], tab2[T2 ? 256 : 1];
+  if constexpr (T1) build_tip_table<T>(left, tab1);
+  if constexpr (T2) build_tip_table<T>(right, tab2);
+  if constexpr (T1 || T2) __syncthreads();
 
   T PL[16], PR[16], E[16];
 #pragma unroll
@@ -179,19 +233,25 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
   // full steps: no bounds checks, every load of the step issued up front
   for (; base < nfull; base += stride) {
     T a[U][4], b[U][4];
-    int w[U];
+    int w[U], k1[U], k2[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int64_t site = base + u * 16 + q;
-      Num<T>::template load4<NT>(x1 + site * 16 + c * 4, a[u]);
-      Num<T>::template load4<NT>(x2 + site * 16 + c * 4, b[u]);
+      if constexpr (T1) k1[u] = tip1[site] & 15;
+      else Num<T>::template load4<NT>(x1 + site * 16 + c * 4, a[u]);
+      if constexpr (T2) k2[u] = tip2[site] & 15;
+      else Num<T>::template load4<NT>(x2 + site * 16 + c * 4, b[u]);
       if (kSum) w[u] = wgt ? wgt[site] : 1;
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int64_t site = base + u * 16 + q;
       T o[4];
-      site_cat<T>(a[u], b[u], PL, PR, E, o);
+      if constexpr (T1 || T2)
+        site_cat_tips<T, T1, T2>(a[u], b[u], PL, PR, E, tab1 + c * 64 + 4 * (T1 ? k1[u] : 0),
+                                 tab2 + c * 64 + 4 * (T2 ? k2[u] : 0), o);
+      else
+        site_cat<T>(a[u], b[u], PL, PR, E, o);
       const bool small = (Num<T>::abs(o[0]) < m) && (Num<T>::abs(o[1]) < m) &&
                          (Num<T>::abs(o[2]) < m) && (Num<T>::abs(o[3]) < m);
       const unsigned long long mask = __ballot(small);
@@ -215,12 +275,18 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
       const int64_t site = base + u * 16 + q;
       const bool valid = site < n;
       T a[4] = {T(0), T(0), T(0), T(0)}, b[4] = {T(0), T(0), T(0), T(0)};
+      int k1 = 0, k2 = 0;
       if (valid) {
-        Num<T>::template load4<false>(x1 + site * 16 + c * 4, a);
-        Num<T>::template load4<false>(x2 + site * 16 + c * 4, b);
+        if constexpr (T1) k1 = tip1[site] & 15;
+        else Num<T>::template load4<false>(x1 + site * 16 + c * 4, a);
+        if constexpr (T2) k2 = tip2[site] & 15;
+        else Num<T>::template load4<false>(x2 + site * 16 + c * 4, b);
       }
       T o[4];
-      site_cat<T>(a, b, PL, PR, E, o);
+      if constexpr (T1 || T2)
+        site_cat_tips<T, T1, T2>(a, b, PL, PR, E, tab1 + c * 64 + 4 * k1, tab2 + c * 64 + 4 * k2, o);
+      else
+        site_cat<T>(a, b, PL, PR, E, o);
       const bool small = valid && (Num<T>::abs(o[0]) < m) && (Num<T>::abs(o[1]) < m) &&
                          (Num<T>::abs(o[2]) < m) && (Num<T>::abs(o[3]) < m);
       const unsigned long long mask = __ballot(small);
@@ -267,7 +333,9 @@ __device__ __forceinline__ f64x2 ld16(const f64x2 *p) {
   else return *p;
 }
 
-template <int U, bool kSum, bool NTL>
+// T1/T2: child 1/2 is a tip (one state code per site, see build_tip_table);
+// its lane pair reads ump[2h], ump[2h+1] as one 16-B LDS row slice.
+template <int U, bool kSum, bool NTL, bool T1 = false, bool T2 = false>
 __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
                                               const double *__restrict__ x2,
                                               double *__restrict__ x3,
@@ -276,12 +344,19 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
                                               const double *__restrict__ right,
                                               const int32_t *__restrict__ wgt,
                                               uint8_t *__restrict__ scaler, int64_t n,
-                                              unsigned long long *ws, int64_t *scaler_sum) {
+                                              unsigned long long *ws, int64_t *scaler_sum,
+                                              const uint8_t *__restrict__ tip1 = nullptr,
+                                              const uint8_t *__restrict__ tip2 = nullptr) {
   const int lane = threadIdx.x & 63;
   const int h = lane & 1;          // which half of the category's states / k range
   const int c = (lane >> 1) & 3;   // Gamma category
   const int g = lane >> 3;         // site within the 8-site block of one instruction
   const int sh = lane & 56;        // bit offset of this site's byte in the ballot
+  __shared__ double tab1[T1 ? 256 : 1], tab2[T2 ? 256 : 1];
+  if constexpr (T1) build_tip_table<double>(left, tab1);
+  if constexpr (T2) build_tip_table<double>(right, tab2);
+  if constexpr (T1 || T2) __syncthreads();
+  const int trow = c * 64 + 2 * h;  // + 4*code: this lane's slice of a table row
 
   double PL[2][4], PR[2][4], E[4][2];
 #pragma unroll
@@ -303,20 +378,39 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
   const int64_t nfull = n - (16 * U - 1);
 
   // one 8-site block: loads are done by the caller
-  auto body = [&](const f64x2 a, const f64x2 b, int64_t site0, bool valid, int w) {
-    // rebuild the 4 states of x1_c / x2_c in every lane of the pair
-    const double a0 = dpp_f64<kQuadEven>(a.x), a1 = dpp_f64<kQuadEven>(a.y);
-    const double a2 = dpp_f64<kQuadOdd>(a.x), a3 = dpp_f64<kQuadOdd>(a.y);
-    const double b0 = dpp_f64<kQuadEven>(b.x), b1 = dpp_f64<kQuadEven>(b.y);
-    const double b2 = dpp_f64<kQuadOdd>(b.x), b3 = dpp_f64<kQuadOdd>(b.y);
+  auto body = [&](const f64x2 a, const f64x2 b, int k1, int k2, int64_t site0, bool valid,
+                  int w) {
+    double u1[2], u2[2];
+    if constexpr (T1) {
+      const f64x2 r = *reinterpret_cast<const f64x2 *>(tab1 + trow + 4 * k1);
+      u1[0] = r.x; u1[1] = r.y;
+    } else {
+      // rebuild the 4 states of x1_c in every lane of the pair
+      const double a0 = dpp_f64<kQuadEven>(a.x), a1 = dpp_f64<kQuadEven>(a.y);
+      const double a2 = dpp_f64<kQuadOdd>(a.x), a3 = dpp_f64<kQuadOdd>(a.y);
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) {
+        double v = 0.0;
+        v += a0 * PL[kk][0]; v += a1 * PL[kk][1]; v += a2 * PL[kk][2]; v += a3 * PL[kk][3];
+        u1[kk] = v;
+      }
+    }
+    if constexpr (T2) {
+      const f64x2 r = *reinterpret_cast<const f64x2 *>(tab2 + trow + 4 * k2);
+      u2[0] = r.x; u2[1] = r.y;
+    } else {
+      const double b0 = dpp_f64<kQuadEven>(b.x), b1 = dpp_f64<kQuadEven>(b.y);
+      const double b2 = dpp_f64<kQuadOdd>(b.x), b3 = dpp_f64<kQuadOdd>(b.y);
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) {
+        double v = 0.0;
+        v += b0 * PR[kk][0]; v += b1 * PR[kk][1]; v += b2 * PR[kk][2]; v += b3 * PR[kk][3];
+        u2[kk] = v;
+      }
+    }
     double pm[2];
 #pragma unroll
-    for (int kk = 0; kk < 2; kk++) {
-      double u1 = 0.0, u2 = 0.0;
-      u1 += a0 * PL[kk][0]; u1 += a1 * PL[kk][1]; u1 += a2 * PL[kk][2]; u1 += a3 * PL[kk][3];
-      u2 += b0 * PR[kk][0]; u2 += b1 * PR[kk][1]; u2 += b2 * PR[kk][2]; u2 += b3 * PR[kk][3];
-      pm[kk] = u1 * u2;
-    }
+    for (int kk = 0; kk < 2; kk++) pm[kk] = u1[kk] * u2[kk];
     const double p0 = dpp_f64<kQuadEven>(pm[0]), p1 = dpp_f64<kQuadEven>(pm[1]);
     const double p2 = dpp_f64<kQuadOdd>(pm[0]), p3 = dpp_f64<kQuadOdd>(pm[1]);
     double o[2];
@@ -347,20 +441,24 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
   int64_t base = wave * 16 * U;
   for (; base < nfull; base += stride) {
     f64x2 a[U][2], b[U][2];
-    int w[U][2];
+    int w[U][2], k1[U][2], k2[U][2];
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
       for (int j = 0; j < 2; j++) {
         const int64_t site0 = base + u * 16 + j * 8;
-        a[u][j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(x1 + site0 * 16) + lane);
-        b[u][j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
+        if constexpr (T1) k1[u][j] = tip1[site0 + g] & 15;
+        else a[u][j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(x1 + site0 * 16) + lane);
+        if constexpr (T2) k2[u][j] = tip2[site0 + g] & 15;
+        else b[u][j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
         if (kSum) w[u][j] = wgt ? wgt[site0 + g] : 1;
       }
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
-      for (int j = 0; j < 2; j++) body(a[u][j], b[u][j], base + u * 16 + j * 8, true, kSum ? w[u][j] : 0);
+      for (int j = 0; j < 2; j++)
+        body(T1 ? f64x2{} : a[u][j], T2 ? f64x2{} : b[u][j], T1 ? k1[u][j] : 0,
+             T2 ? k2[u][j] : 0, base + u * 16 + j * 8, true, kSum ? w[u][j] : 0);
   }
   if (base < n) {  // tail: at most one partial step per wave
 #pragma unroll
@@ -370,13 +468,15 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
         const int64_t site0 = base + u * 16 + j * 8;
         const bool valid = site0 + g < n;
         f64x2 a = {0.0, 0.0}, b = {0.0, 0.0};
-        int w = 0;
+        int w = 0, k1 = 0, k2 = 0;
         if (valid) {
-          a = reinterpret_cast<const f64x2 *>(x1 + site0 * 16)[lane];
-          b = reinterpret_cast<const f64x2 *>(x2 + site0 * 16)[lane];
+          if constexpr (T1) k1 = tip1[site0 + g] & 15;
+          else a = reinterpret_cast<const f64x2 *>(x1 + site0 * 16)[lane];
+          if constexpr (T2) k2 = tip2[site0 + g] & 15;
+          else b = reinterpret_cast<const f64x2 *>(x2 + site0 * 16)[lane];
           if (kSum) w = wgt ? wgt[site0 + g] : 1;
         }
-        body(a, b, site0, valid, w);
+        body(a, b, k1, k2, site0, valid, w);
       }
   }
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
@@ -409,25 +509,30 @@ struct NodeBatch {
   NodeDesc d[kMaxBatch];
 };
 
-template <int U, bool kSum, int kMinWaves, bool NTL = false>
+// kTips: 0 = both children dense CLVs, 1 = child 1 is a tip (x1 points at its
+// state codes), 2 = both children are tips.  (A dense/tip node is run as
+// tip/dense with the children swapped: u1*u2 == u2*u1 exactly.)
+template <int U, bool kSum, int kMinWaves, bool NTL = false, int kTips = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_f64_pair_batch_kernel(const NodeBatch nodes, const double *__restrict__ EV,
                               const int32_t *__restrict__ wgt, int64_t n,
                               unsigned long long *ws) {
   const NodeDesc &d = nodes.d[blockIdx.y];
-  dna_pair_body<U, kSum, NTL>((const double *)d.x1, (const double *)d.x2, (double *)d.x3, EV,
-                              (const double *)d.left, (const double *)d.right, wgt, d.scaler, n,
-                              ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum);
+  dna_pair_body<U, kSum, NTL, (kTips >= 1), (kTips == 2)>(
+      (const double *)d.x1, (const double *)d.x2, (double *)d.x3, EV, (const double *)d.left,
+      (const double *)d.right, wgt, d.scaler, n, ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum,
+      (const uint8_t *)d.x1, (const uint8_t *)d.x2);
 }
 
-template <typename T, int U, bool kSum, bool NT, int kMinWaves>
+template <typename T, int U, bool kSum, bool NT, int kMinWaves, int kTips = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_batch_kernel(const NodeBatch nodes, const T *__restrict__ EV,
                      const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
   const NodeDesc &d = nodes.d[blockIdx.y];
-  dna_cat_body<T, U, kSum, NT>((const T *)d.x1, (const T *)d.x2, (T *)d.x3, EV, (const T *)d.left,
-                               (const T *)d.right, wgt, d.scaler, n,
-                               ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum);
+  dna_cat_body<T, U, kSum, NT, (kTips >= 1), (kTips == 2)>(
+      (const T *)d.x1, (const T *)d.x2, (T *)d.x3, EV, (const T *)d.left, (const T *)d.right, wgt,
+      d.scaler, n, ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, (const uint8_t *)d.x1,
+      (const uint8_t *)d.x2);
 }
 
 __global__ void __launch_bounds__(kBlock)

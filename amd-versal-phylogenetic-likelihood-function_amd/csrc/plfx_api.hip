@@ -150,6 +150,34 @@ int plf_host(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int n,
   return PLFX_OK;
 }
 
+// Nodes of one kind (tips = number of tip children, tip child first) in
+// launches of kMaxBatch.  A tip child is a uint8 code array (no alignment rule).
+int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, const void *EV,
+               int64_t n, const int32_t *wgt, hipStream_t s, int tips) {
+  if (count < 0 || n < 0 || (count > 0 && (!nodes || !EV)))
+    return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
+  for (int i = 0; i < count; i++) {
+    const plfx_node &d = nodes[i];
+    if (n > 0) {
+      if (!d.x1 || !d.x2 || !d.x3 || !d.left || !d.right)
+        return fail(ctx, PLFX_ERR_INVALID, "node %d: null CLV/tip/matrix pointer", i);
+      if ((tips < 1 && !aligned16(d.x1)) || (tips < 2 && !aligned16(d.x2)) || !aligned16(d.x3))
+        return fail(ctx, PLFX_ERR_INVALID, "node %d: CLV pointers must be 16-byte aligned", i);
+      if (d.x3 == d.x1 || d.x3 == d.x2)
+        return fail(ctx, PLFX_ERR_INVALID, "node %d: x3 may not alias a child", i);
+    }
+    if (n == 0 && d.scaler_sum) PLFX_HIP(ctx, hipMemsetAsync(d.scaler_sum, 0, sizeof(int64_t), s));
+  }
+  if (n == 0) return PLFX_OK;
+  for (int i = 0; i < count; i += plfx::kMaxBatch) {
+    const int c = std::min(plfx::kMaxBatch, count - i);
+    hipError_t e = plfx::launch_plf_dna_batch(dtype, reinterpret_cast<const plfx::NodeDescH *>(nodes + i),
+                                              c, EV, wgt, n, ctx->ws, ctx->max_blocks, s, tips);
+    if (e != hipSuccess) return hip_fail(ctx, e, "plf batch launch");
+  }
+  return PLFX_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -309,31 +337,39 @@ int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *no
   if (!ctx) return PLFX_ERR_INVALID;
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
   if (states != 4) return fail(ctx, PLFX_ERR_UNSUPPORTED, "batched nodes: states=%d not built", states);
-  if (count < 0 || n < 0 || (count > 0 && (!nodes || !EV)))
-    return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
-  hipStream_t s = pick(ctx, stream);
-  for (int i = 0; i < count; i++) {
-    int rc = check_dev_args(ctx, nodes[i].x1, nodes[i].x2, nodes[i].x3, EV, n, nodes[i].left,
-                            nodes[i].right);
-    if (rc != PLFX_OK) return rc;
-    if (n == 0 && nodes[i].scaler_sum)
-      PLFX_HIP(ctx, hipMemsetAsync(nodes[i].scaler_sum, 0, sizeof(int64_t), s));
+  return batch_impl(ctx, dtype, nodes, count, EV, n, wgt, pick(ctx, stream), 0);
+}
+
+int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void *x1,
+                      const uint8_t *tip2, const void *x2, void *x3, const void *EV, int64_t n,
+                      const void *left, const void *right, const int32_t *wgt, uint8_t *scaler,
+                      int64_t *scaler_sum, void *stream) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if ((tip1 != nullptr) == (x1 != nullptr) || (tip2 != nullptr) == (x2 != nullptr))
+    return fail(ctx, PLFX_ERR_INVALID, "each child needs exactly one of tip / CLV");
+  plfx_node nd{tip1 ? (const void *)tip1 : x1, tip2 ? (const void *)tip2 : x2, x3, left, right,
+               scaler, scaler_sum};
+  int tips = (tip1 ? 1 : 0) + (tip2 ? 1 : 0);
+  if (!tip1 && tip2) {  // dense/tip runs as tip/dense: u1*u2 == u2*u1 exactly
+    std::swap(nd.x1, nd.x2);
+    std::swap(nd.left, nd.right);
   }
-  if (n == 0) return PLFX_OK;
-  for (int i = 0; i < count; i += plfx::kMaxBatch) {
-    const int c = std::min(plfx::kMaxBatch, count - i);
-    hipError_t e = plfx::launch_plf_dna_batch(
-        dtype, reinterpret_cast<const plfx::NodeDescH *>(nodes + i), c, EV, wgt, n, ctx->ws,
-        ctx->max_blocks, s);
-    if (e != hipSuccess) return hip_fail(ctx, e, "plf batch launch");
-  }
-  return PLFX_OK;
+  return batch_impl(ctx, dtype, &nd, 1, EV, n, wgt, pick(ctx, stream), tips);
 }
 
 int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
                   void *const *clv, int nslots, const void *pmats, int npmats, const void *EV,
                   int64_t n, const int32_t *wgt, uint8_t *const *scalers, int64_t *scaler_sums,
                   void *stream) {
+  return plfx_traverse_tips(ctx, dtype, states, ops, nops, clv, nullptr, nslots, pmats, npmats, EV,
+                            n, wgt, scalers, scaler_sums, stream);
+}
+
+int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
+                       void *const *clv, const uint8_t *const *tips, int nslots, const void *pmats,
+                       int npmats, const void *EV, int64_t n, const int32_t *wgt,
+                       uint8_t *const *scalers, int64_t *scaler_sums, void *stream) {
   if (!ctx) return PLFX_ERR_INVALID;
   if (states != 4) return fail(ctx, PLFX_ERR_UNSUPPORTED, "traverse: states=%d not built", states);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
@@ -341,6 +377,7 @@ int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops,
     return fail(ctx, PLFX_ERR_INVALID, "bad traverse arguments");
   const size_t es = dtype == PLFX_F32 ? 4 : 8;
   const size_t mat = (size_t)states * states * 4;  // C*S*S values per matrix
+  auto is_tip = [&](int sl) { return tips && tips[sl]; };
   // dependency levels: RAW on children, WAR/WAW on the parent slot
   std::vector<int> level(nops, 0), slot_write(nslots, -1), slot_read(nslots, -1);
   int nlev = 0;
@@ -351,6 +388,7 @@ int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops,
       return fail(ctx, PLFX_ERR_INVALID, "op %d: slot/pmat index out of range", j);
     if (o.parent == o.child1 || o.parent == o.child2)
       return fail(ctx, PLFX_ERR_INVALID, "op %d: parent slot aliases a child", j);
+    if (is_tip(o.parent)) return fail(ctx, PLFX_ERR_INVALID, "op %d: parent slot is a tip", j);
     int lv = 0;
     for (int sl : {o.child1, o.child2})
       if (slot_write[sl] >= 0) lv = std::max(lv, slot_write[sl] + 1);
@@ -362,21 +400,29 @@ int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops,
     nlev = std::max(nlev, lv + 1);
   }
   hipStream_t s = pick(ctx, stream);
-  std::vector<plfx_node> batch;
+  const char *pm = static_cast<const char *>(pmats);
+  std::vector<plfx_node> batch[3];  // by number of tip children
   for (int lv = 0; lv < nlev; lv++) {
-    batch.clear();
+    for (auto &b : batch) b.clear();
     for (int j = 0; j < nops; j++) {
       if (level[j] != lv) continue;
       const plfx_trav_op &o = ops[j];
-      const char *pm = static_cast<const char *>(pmats);
-      batch.push_back(plfx_node{clv[o.child1], clv[o.child2], clv[o.parent],
-                                pm + (size_t)(2 * o.pmat) * mat * es,
-                                pm + (size_t)(2 * o.pmat + 1) * mat * es,
-                                scalers ? scalers[j] : nullptr,
-                                scaler_sums ? scaler_sums + j : nullptr});
+      const bool t1 = is_tip(o.child1), t2 = is_tip(o.child2);
+      plfx_node nd{t1 ? (const void *)tips[o.child1] : clv[o.child1],
+                   t2 ? (const void *)tips[o.child2] : clv[o.child2], clv[o.parent],
+                   pm + (size_t)(2 * o.pmat) * mat * es, pm + (size_t)(2 * o.pmat + 1) * mat * es,
+                   scalers ? scalers[j] : nullptr, scaler_sums ? scaler_sums + j : nullptr};
+      if (!t1 && t2) {  // dense/tip -> tip/dense (exact: the product commutes)
+        std::swap(nd.x1, nd.x2);
+        std::swap(nd.left, nd.right);
+      }
+      batch[(t1 ? 1 : 0) + (t2 ? 1 : 0)].push_back(nd);
     }
-    int rc = plfx_plf_batch_dev(ctx, dtype, states, batch.data(), (int)batch.size(), EV, n, wgt, s);
-    if (rc != PLFX_OK) return rc;
+    for (int k = 0; k < 3; k++) {
+      if (batch[k].empty()) continue;
+      int rc = batch_impl(ctx, dtype, batch[k].data(), (int)batch[k].size(), EV, n, wgt, s, k);
+      if (rc != PLFX_OK) return rc;
+    }
   }
   return PLFX_OK;
 }

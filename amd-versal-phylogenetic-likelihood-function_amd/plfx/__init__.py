@@ -48,6 +48,7 @@ EXPORTS = (
     "plfx_tb_instance_active_elements_left", "plfx_tb_instance_active_elements_right",
     "plfx_tb_num_windows_per_instance", "plfx_pack_instance",
     "plfx_plf_batch_dev", "plfx_traverse", "plfx_root_lnl", "plfx_plf_dev_gen",
+    "plfx_plf_tips_dev", "plfx_traverse_tips",
 )
 EXACT, FMA = 0, 1
 
@@ -122,6 +123,9 @@ def load():
     L.plfx_traverse.argtypes = [vp, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp), i32, vp, i32,
                                 vp, i64, vp, C.POINTER(vp), vp, vp]
     L.plfx_root_lnl.argtypes = [vp, i32, i32, vp, i64, vp, vp, vp, vp, i32, vp, vp, vp]
+    L.plfx_plf_tips_dev.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
+    L.plfx_traverse_tips.argtypes = [vp, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp),
+                                     C.POINTER(vp), i32, vp, i32, vp, i64, vp, C.POINTER(vp), vp, vp]
     _lib = L
     return L
 
@@ -332,32 +336,65 @@ class Context:
                                                C.c_void_p(ptr(wgt)), _stream_handle(stream)))
 
     def traverse(self, ops, clv, pmats, EV, n, wgt=None, scalers=None, scaler_sums=None,
-                 stream=None):
+                 stream=None, tips=None):
         """Run a post-order traversal descriptor.  ops: (nops, 4) int array of
-        [parent, child1, child2, pmat]; clv: list of torch CLV tensors (slots);
-        pmats: tensor of 2*npmat matrices (64 values each for DNA)."""
+        [parent, child1, child2, pmat]; clv: list of torch CLV tensors (slots;
+        None where the slot is a tip); pmats: tensor of 2*npmat matrices (64
+        values each for DNA); tips: optional list (per slot) of uint8 state-code
+        tensors or None (plfx.h section 8)."""
         import torch
 
         ops = np.ascontiguousarray(ops, dtype=np.int32).reshape(-1, 4)
         nops = ops.shape[0]
         dt = EV.dtype
-        for t in clv:
-            if t.dtype != dt or t.numel() < 16 * n or not t.is_contiguous():
+        nslots = len(clv)
+        if tips is not None and len(tips) != nslots:
+            raise PlfxError(ERR_INVALID, "tips must have one entry per slot")
+        for s_, t in enumerate(clv):
+            tip = None if tips is None else tips[s_]
+            if tip is not None:
+                if tip.dtype != torch.uint8 or tip.numel() < n or not tip.is_contiguous():
+                    raise PlfxError(ERR_INVALID, f"tip slot {s_}: contiguous uint8 >= n required")
+                continue
+            if t is None or t.dtype != dt or t.numel() < 16 * n or not t.is_contiguous():
                 raise PlfxError(ERR_INVALID, "every CLV slot must be contiguous, same dtype, >= 16*n")
         if pmats.dtype != dt or pmats.numel() % 128:
             raise PlfxError(ERR_INVALID, "pmats must hold whole (left, right) pairs of 64 values")
         if scaler_sums is not None and (scaler_sums.dtype != torch.int64 or scaler_sums.numel() < nops):
             raise PlfxError(ERR_INVALID, "scaler_sums must be int64 with >= nops entries")
         top = (TravOp * nops)(*[TravOp(*map(int, r)) for r in ops])
-        slots = (C.c_void_p * len(clv))(*[t.data_ptr() for t in clv])
+        slots = (C.c_void_p * nslots)(*[None if t is None else t.data_ptr() for t in clv])
+        tp = None
+        if tips is not None:
+            tp = (C.c_void_p * nslots)(*[None if t is None else t.data_ptr() for t in tips])
         sc = None
         if scalers is not None:
             sc = (C.c_void_p * nops)(*[None if t is None else t.data_ptr() for t in scalers])
-        self._check(self._L.plfx_traverse(
-            self.h, F32 if dt == torch.float32 else F64, 4, top, nops, slots, len(clv),
+        self._check(self._L.plfx_traverse_tips(
+            self.h, F32 if dt == torch.float32 else F64, 4, top, nops, slots, tp, nslots,
             C.c_void_p(pmats.data_ptr()), pmats.numel() // 128, C.c_void_p(EV.data_ptr()), int(n),
             C.c_void_p(None if wgt is None else wgt.data_ptr()), sc,
             C.c_void_p(None if scaler_sums is None else scaler_sums.data_ptr()),
+            _stream_handle(stream)))
+
+    def plf_tips_dev(self, x3, EV, n, left, right, x1=None, x2=None, tip1=None, tip2=None,
+                     wgt=None, scaler=None, scaler_sum=None, stream=None):
+        """One DNA inner node with tip children (plfx.h section 8): for each
+        child pass exactly one of the dense CLV (x1/x2) or the uint8 state
+        codes (tip1/tip2)."""
+        import torch
+
+        dt = EV.dtype
+        for k, t in (("x3", x3), ("x1", x1), ("x2", x2)):
+            if t is not None and (t.dtype != dt or t.numel() < 16 * n or not t.is_contiguous()):
+                raise PlfxError(ERR_INVALID, f"{k} must be contiguous {dt} >= 16*n")
+        for k, t in (("tip1", tip1), ("tip2", tip2)):
+            if t is not None and (t.dtype != torch.uint8 or t.numel() < n or not t.is_contiguous()):
+                raise PlfxError(ERR_INVALID, f"{k} must be contiguous uint8 >= n")
+        p = lambda t: C.c_void_p(None if t is None else t.data_ptr())  # noqa: E731
+        self._check(self._L.plfx_plf_tips_dev(
+            self.h, F32 if dt == torch.float32 else F64, p(tip1), p(x1), p(tip2), p(x2), p(x3),
+            p(EV), int(n), p(left), p(right), p(wgt), p(scaler), p(scaler_sum),
             _stream_handle(stream)))
 
     # -- (7) root log-likelihood --------------------------------------------

@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--buffer-sets", type=int, default=4)
     ap.add_argument("--fma", action="store_true", help="protein: fused multiply-add mode")
+    ap.add_argument("--tips", action="store_true",
+                    help="tree64: tips as uint8 state codes (plfx.h section 8) instead of dense CLVs")
     ap.add_argument("--workload", choices=["node", "tree64", "nodes64", "protein"], default="node",
                     help="node: BASELINE configs[1] (headline); tree64: configs[2]; "
                          "nodes64: the per-GPU shard of configs[3]")
@@ -201,7 +203,14 @@ class Tree64Workload:
         self.n, self.ctx = n, ctx
         self.ops = np.array(_balanced_ops(ntips), np.int32)
         nops = self.ops.shape[0]
-        self.clv = [torch.rand(16 * n, dtype=tdt, device=dev, generator=g) for _ in range(ntips)]
+        self.tips = None
+        if a.tips:
+            acgt = torch.tensor([1, 2, 4, 8], dtype=torch.uint8, device=dev)
+            self.tips = [acgt[torch.randint(0, 4, (n,), device=dev, generator=g)]
+                         for _ in range(ntips)] + [None] * nops
+            self.clv = [None] * ntips
+        else:
+            self.clv = [torch.rand(16 * n, dtype=tdt, device=dev, generator=g) for _ in range(ntips)]
         self.clv += [torch.empty(16 * n, dtype=tdt, device=dev) for _ in range(nops)]
         self.pm = torch.rand(nops * 128, dtype=tdt, device=dev, generator=g) * 0.25
         self.EV = torch.rand(16, dtype=tdt, device=dev, generator=g) * 0.25
@@ -209,17 +218,23 @@ class Tree64Workload:
         self.sums = torch.zeros(nops, dtype=torch.int64, device=dev)
         self.lnl = torch.zeros(1, dtype=torch.float64, device=dev)
         self.sites_per_step = nops * n
-        # per node: read x1, x2, write x3, read wgt (scaler sums, no bytes); + lnL read of the root
+        # per node: read x1, x2, write x3, read wgt (scaler sums, no bytes); + lnL read of the root.
+        # With coded tips the 32 tip/tip nodes read 2 code bytes instead of two CLVs.
         self.bytes_per_site = 3 * 16 * esz + 4
-        self.bytes_per_step = nops * self.bytes_per_site * n + (16 * esz + 4) * n
+        inner = nops - ntips // 2 if a.tips else nops
+        self.bytes_per_step = inner * self.bytes_per_site * n + (16 * esz + 4) * n
+        if a.tips:
+            self.bytes_per_step += (ntips // 2) * (16 * esz + 2 + 4) * n
+        tipdesc = "tips as uint8 state codes" if a.tips else "dense tip CLVs"
         self.config = {
             "workload": f"DNA 4-state, 64-taxon balanced tree post-order sweep (63 inner nodes, "
-                        f"6 level launches) + root lnL, {n} sites, {a.dtype} (BASELINE configs[2])",
+                        f"6 level launches) + root lnL, {n} sites, {a.dtype}, {tipdesc} "
+                        f"(BASELINE configs[2])",
             "sites_per_gpu_per_step": self.sites_per_step, "nodes_per_gpu_per_step": nops}
 
     def step(self, i, sh):
         self.ctx.traverse(self.ops, self.clv, self.pm, self.EV, self.n, self.wgt, None, self.sums,
-                          stream=sh)
+                          stream=sh, tips=self.tips)
         self.ctx.root_lnl(self.clv[-1], self.n, self.lnl, wgt=self.wgt, scaler_sums=self.sums,
                           stream=sh)
 

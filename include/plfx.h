@@ -181,6 +181,30 @@ int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops,
                   int64_t n, const int32_t *wgt, uint8_t *const *scalers, int64_t *scaler_sums,
                   void *stream);
 
+/* ---- (8) tip children (extension) ---------------
+ * A tip (leaf) is stored as one state code per site -- uint8, bit s set =
+ * state s possible (A=1 C=2 G=4 T=8, ambiguity codes are unions, 15 = gap /
+ * unknown; the upper nibble is ignored), the RAxML/PLL encoding -- instead of
+ * a dense CLV of 16 values per site (16x/32x less traffic for that child).
+ * Results are bit-identical to plf() on the expanded dense CLV
+ * x[i][c][s] = (code_i >> s) & 1 for every category c.  DNA (4 states) only. */
+
+/* One node: exactly one of (tip1, x1) and one of (tip2, x2) is non-NULL;
+ * the other arguments are those of plfx_plf_dev_f32/f64 (device pointers). */
+int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void *x1,
+                      const uint8_t *tip2, const void *x2, void *x3, const void *EV, int64_t n,
+                      const void *left, const void *right, const int32_t *wgt, uint8_t *scaler,
+                      int64_t *scaler_sum, void *stream);
+
+/* plfx_traverse with tip slots: tips is a host array of nslots device pointers
+ * (or NULL = no tips); a slot with tips[s] != NULL is a tip (clv[s] is not
+ * read) and may not be an op's parent.  Each level is issued as up to three
+ * batched launches (tip/tip, tip/inner, inner/inner). */
+int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
+                       void *const *clv, const uint8_t *const *tips, int nslots, const void *pmats,
+                       int npmats, const void *EV, int64_t n, const int32_t *wgt,
+                       uint8_t *const *scalers, int64_t *scaler_sums, void *stream);
+
 /* ---- (7) root log-likelihood (extension) -- */
 /* lnL = sum_i wgt_i * log( sum_c catw[c] * sum_s freq[s] * x[i][c][s] )
  *       + (sum_{j<nsums} scaler_sums[j]) * log(2^-32)

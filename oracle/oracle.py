@@ -231,6 +231,25 @@ def balanced_tree_ops(ntips):
     return np.array(ops, np.int32)
 
 
+def expand_tips(codes, dtype=np.float64, Ccat=4):
+    """Dense CLV of a tip stored as DNA state codes (bit s = state s possible,
+    upper nibble ignored; the RAxML/PLL encoding): x[i][c][s] = (code_i >> s) & 1
+    for every category c.  This is the definition the GPU's tip path is
+    checked against (plfx.h section 8): plf() on the expanded CLV."""
+    codes = np.asarray(codes, np.uint8)
+    bits = ((codes[:, None] >> np.arange(4, dtype=np.uint8)) & 1).astype(dtype)
+    return np.ascontiguousarray(np.repeat(bits[:, None, :], Ccat, axis=1).reshape(-1))
+
+
+def random_tip_codes(rng, n, ambiguous=0.1):
+    """Tip codes: mostly unambiguous A/C/G/T (1, 2, 4, 8), a fraction of
+    random bytes (ambiguity codes, gaps 15, code 0, junk in the upper nibble)."""
+    codes = np.array([1, 2, 4, 8], np.uint8)[rng.integers(0, 4, n)]
+    amb = rng.random(n) < ambiguous
+    codes[amb] = rng.integers(0, 256, int(amb.sum())).astype(np.uint8)
+    return codes
+
+
 def ref_plf(x1, x2, EV, left, right, wgt, opt="O0"):
     """Run the reference plf() (float only).  Returns (x3, scalerIncrement)."""
     L = ref_lib(opt)

@@ -216,3 +216,50 @@ def test_testbench_sizing_examples(oracle, N, P, W, layout, aie):
     # 1M sites, W=8192 -> 1954 windows -> 1,000,448 padded sites
     if (N, P, W) == (1000000, 9, 8192):
         assert tb.alignments_per_instance() == 111112
+
+
+def test_tip_expansion_definition(oracle):
+    """Tip codes (plfx.h section 8): bit s -> state s, every category, upper
+    nibble ignored."""
+    codes = np.array([0, 1, 2, 4, 8, 5, 15, 0xF1, 0x30], np.uint8)
+    x = oracle.expand_tips(codes).reshape(-1, 4, 4)
+    exp = np.array([[0, 0, 0, 0], [1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 0], [0, 0, 0, 1],
+                    [1, 0, 1, 0], [1, 1, 1, 1], [1, 0, 0, 0], [0, 0, 0, 0]], np.float64)
+    for c in range(4):
+        assert np.array_equal(x[:, c, :], exp)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_tip_table_identity(oracle, dtype):
+    """The GPU tip path reads ump[k] = T[c][code][k] = sum_l bit_l * P_c[k][l]
+    (ascending l from +0.0) from a per-block table.  Restated here in numpy
+    with the same operation order, the per-site result must equal plf() on the
+    expanded CLV bit for bit -- the algebraic claim the kernel relies on."""
+    rng = np.random.default_rng(11)
+    n = 3000
+    c1 = oracle.random_tip_codes(rng, n, 0.3)
+    c2 = oracle.random_tip_codes(rng, n, 0.3)
+    L = rng.random(64).astype(dtype)
+    R = rng.random(64).astype(dtype)
+    EV = rng.random(16).astype(dtype)
+    x3, sc, inc = oracle.plf(oracle.expand_tips(c1, dtype), oracle.expand_tips(c2, dtype), EV, L, R)
+
+    def table(P):
+        t = np.zeros((4, 16, 4), dtype)
+        for code in range(16):
+            for l in range(4):
+                t[:, code, :] += dtype((code >> l) & 1) * P.reshape(4, 4, 4)[:, :, l]
+        return t
+
+    u1 = table(L)[:, c1 & 15, :].transpose(1, 0, 2)   # (n, c, k)
+    u2 = table(R)[:, c2 & 15, :].transpose(1, 0, 2)
+    p = u1 * u2
+    o = np.zeros((n, 4, 4), dtype)
+    E = EV.reshape(4, 4)
+    for k in range(4):
+        o += p[:, :, k:k + 1] * E[k][None, None, :]
+    small = np.all(np.abs(o.reshape(n, 16)) < dtype(2.0 ** -32), axis=1)
+    o[small] *= dtype(2.0 ** 32)
+    assert np.array_equal(bits(o.reshape(-1)), bits(x3))
+    assert np.array_equal(sc, small.astype(np.uint8))
+    assert int(inc) == int(small.sum())
