@@ -20,6 +20,7 @@
 #include "plf_dna.hpp"
 #include "plf_kernels.hpp"
 #include "plf_lnl.hpp"
+#include "plf_pmat.hpp"
 #include "plf_prot.hpp"
 
 namespace plfx {
@@ -237,6 +238,32 @@ hipError_t launch_scaler_sum(const uint8_t *scaler, const int32_t *wgt, int64_t 
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(dev::scaler_sum_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, scaler,
                      wgt, n, ws, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pmatrix(int dtype, bool eigen_conv, const double *eigen, int S,
+                          const double *rates, int ncat, const double *blen, int64_t nbranch,
+                          void *out, hipStream_t s) {
+  const int64_t total = nbranch * ncat * S * S;
+  int64_t blocks = (total + kBlock - 1) / kBlock;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  const dim3 g((unsigned)blocks), b(kBlock);
+  if (dtype == 1) {
+    if (eigen_conv)
+      hipLaunchKernelGGL((dev::pmatrix_kernel<double, true>), g, b, 0, s, eigen, S, rates, ncat,
+                         blen, nbranch, (double *)out);
+    else
+      hipLaunchKernelGGL((dev::pmatrix_kernel<double, false>), g, b, 0, s, eigen, S, rates, ncat,
+                         blen, nbranch, (double *)out);
+  } else {
+    if (eigen_conv)
+      hipLaunchKernelGGL((dev::pmatrix_kernel<float, true>), g, b, 0, s, eigen, S, rates, ncat,
+                         blen, nbranch, (float *)out);
+    else
+      hipLaunchKernelGGL((dev::pmatrix_kernel<float, false>), g, b, 0, s, eigen, S, rates, ncat,
+                         blen, nbranch, (float *)out);
+  }
   return hipGetLastError();
 }
 

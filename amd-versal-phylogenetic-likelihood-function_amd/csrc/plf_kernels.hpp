@@ -55,4 +55,9 @@ hipError_t launch_scaler_sum(const uint8_t *scaler, const int32_t *wgt, int64_t 
                              int64_t *out, unsigned long long *ws, int max_blocks,
                              hipStream_t s);
 
+// P matrices from an eigensystem (plf_pmat.hpp).  dtype 0 f32 / 1 f64.
+hipError_t launch_pmatrix(int dtype, bool eigen_conv, const double *eigen, int S,
+                          const double *rates, int ncat, const double *blen, int64_t nbranch,
+                          void *out, hipStream_t s);
+
 }  // namespace plfx

@@ -461,4 +461,21 @@ int plfx_scaler_sum(plfx_ctx *ctx, const uint8_t *scaler, const int32_t *wgt, in
   return PLFX_OK;
 }
 
+int plfx_pmatrix(plfx_ctx *ctx, int dtype, int states, int convention, const double *eigen,
+                 const double *rates, int ncat, const double *blen, int64_t nbranch, void *pmats,
+                 void *stream) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if (convention != PLFX_PMAT_STATE && convention != PLFX_PMAT_EIGEN)
+    return fail(ctx, PLFX_ERR_INVALID, "bad convention %d", convention);
+  if (states < 2 || states > 64 || ncat < 1 || nbranch < 0)
+    return fail(ctx, PLFX_ERR_INVALID, "bad pmatrix sizes (states %d, ncat %d)", states, ncat);
+  if (nbranch == 0) return PLFX_OK;
+  if (!eigen || !rates || !blen || !pmats) return fail(ctx, PLFX_ERR_INVALID, "null pmatrix pointer");
+  hipError_t e = plfx::launch_pmatrix(dtype, convention == PLFX_PMAT_EIGEN, eigen, states, rates,
+                                      ncat, blen, nbranch, pmats, pick(ctx, stream));
+  if (e != hipSuccess) return hip_fail(ctx, e, "pmatrix launch");
+  return PLFX_OK;
+}
+
 }  // extern "C"

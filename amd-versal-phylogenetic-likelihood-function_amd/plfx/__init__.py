@@ -49,7 +49,10 @@ EXPORTS = (
     "plfx_tb_num_windows_per_instance", "plfx_pack_instance",
     "plfx_plf_batch_dev", "plfx_traverse", "plfx_root_lnl", "plfx_plf_dev_gen",
     "plfx_plf_tips_dev", "plfx_traverse_tips",
+    "plfx_model_eigen", "plfx_gamma_rates", "plfx_model_ev", "plfx_model_root_weights",
+    "plfx_pmatrix",
 )
+PMAT_STATE, PMAT_EIGEN = 0, 1
 EXACT, FMA = 0, 1
 
 
@@ -123,6 +126,12 @@ def load():
     L.plfx_traverse.argtypes = [vp, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp), i32, vp, i32,
                                 vp, i64, vp, C.POINTER(vp), vp, vp]
     L.plfx_root_lnl.argtypes = [vp, i32, i32, vp, i64, vp, vp, vp, vp, i32, vp, vp, vp]
+    dp = C.POINTER(C.c_double)
+    L.plfx_model_eigen.argtypes = [i32, dp, dp, dp]
+    L.plfx_gamma_rates.argtypes = [C.c_double, i32, i32, dp]
+    L.plfx_model_ev.argtypes = [i32, i32, dp, dp]
+    L.plfx_model_root_weights.argtypes = [i32, i32, dp, dp, dp]
+    L.plfx_pmatrix.argtypes = [vp, i32, i32, i32, vp, vp, i32, vp, i64, vp, vp]
     L.plfx_plf_tips_dev.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
     L.plfx_traverse_tips.argtypes = [vp, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp),
                                      C.POINTER(vp), i32, vp, i32, vp, i64, vp, C.POINTER(vp), vp, vp]
@@ -397,6 +406,26 @@ class Context:
             p(EV), int(n), p(left), p(right), p(wgt), p(scaler), p(scaler_sum),
             _stream_handle(stream)))
 
+    # -- (9) P matrices from branch lengths --------------------------------
+    def pmatrix(self, eigen, rates, blen, out, states=4, convention=PMAT_STATE, stream=None):
+        """out[b][c][k][l] from a device eigensystem (float64, S+2S^2), device
+        category rates (float64) and branch lengths (float64); plfx.h (9)."""
+        import torch
+
+        S = states
+        for k, t in (("eigen", eigen), ("rates", rates), ("blen", blen)):
+            if t.dtype != torch.float64 or not t.is_contiguous():
+                raise PlfxError(ERR_INVALID, f"{k} must be a contiguous float64 device tensor")
+        if eigen.numel() < S + 2 * S * S:
+            raise PlfxError(ERR_INVALID, "eigen too small")
+        ncat, nb = rates.numel(), blen.numel()
+        if out.dtype not in (torch.float32, torch.float64) or out.numel() < nb * ncat * S * S:
+            raise PlfxError(ERR_INVALID, "out must hold nbranch*ncat*S*S float values")
+        self._check(self._L.plfx_pmatrix(
+            self.h, F32 if out.dtype == torch.float32 else F64, S, convention,
+            C.c_void_p(eigen.data_ptr()), C.c_void_p(rates.data_ptr()), ncat,
+            C.c_void_p(blen.data_ptr()), nb, C.c_void_p(out.data_ptr()), _stream_handle(stream)))
+
     # -- (7) root log-likelihood --------------------------------------------
     def root_lnl(self, x, n, out, catw=None, freq=None, wgt=None, scaler_sums=None,
                  site_lnl=None, states=4, stream=None):
@@ -442,6 +471,55 @@ def _stream_handle(stream):
 
 
 _default_ctx = None
+
+
+def _dbl(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _host_check(rc, what):
+    if rc != OK:
+        raise PlfxError(rc, what)
+
+
+def model_eigen(exch, freqs):
+    """Eigensystem of a time-reversible model (plfx.h (9)).  Returns a float64
+    array lambda[S] | V[S*S] | Vinv[S*S] (the device pmatrix input)."""
+    L = load()
+    f, fp = _dbl(freqs)
+    S = f.size
+    e, ep = _dbl(exch)
+    if e.size != S * (S - 1) // 2:
+        raise PlfxError(ERR_INVALID, "exch needs S(S-1)/2 values")
+    out, op = _dbl(np.zeros(S + 2 * S * S))
+    _host_check(L.plfx_model_eigen(S, ep, fp, op), "model_eigen")
+    return out
+
+
+def gamma_rates(alpha, ncat=4, median=False):
+    """Yang (1994) discrete-Gamma category rates (plfx.h (9))."""
+    L = load()
+    out, op = _dbl(np.zeros(ncat))
+    _host_check(L.plfx_gamma_rates(float(alpha), int(ncat), 1 if median else 0, op), "gamma_rates")
+    return out
+
+
+def model_ev(eigen, states, convention=PMAT_STATE):
+    L = load()
+    e, ep = _dbl(eigen)
+    out, op = _dbl(np.zeros(states * states))
+    _host_check(L.plfx_model_ev(states, convention, ep, op), "model_ev")
+    return out
+
+
+def model_root_weights(eigen, freqs, convention=PMAT_STATE):
+    L = load()
+    f, fp = _dbl(freqs)
+    e, ep = _dbl(eigen)
+    out, op = _dbl(np.zeros(f.size))
+    _host_check(L.plfx_model_root_weights(f.size, convention, ep, fp, op), "model_root_weights")
+    return out
 
 
 def default_context():

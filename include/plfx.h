@@ -248,6 +248,44 @@ int plfx_pack_instance(const plfx_testbench *tb, int instance, int dtype,
                        const void *x1_all, const void *x2_all, void *out_left,
                        void *out_right);
 
+/* ---- (9) model setup: P matrices and EV from branch lengths (extension,
+ * SURVEY section 8f row 3; the reference's inputs are random or precomputed,
+ * host_mem.cpp:189-197, aie/data/inputbranch*) ---------------------------- */
+typedef enum { PLFX_PMAT_STATE = 0, PLFX_PMAT_EIGEN = 1 } plfx_pmat_convention;
+
+/* Eigensystem of the time-reversible rate matrix Q_ij = r_ij pi_j (i != j),
+ * normalised to one expected substitution per unit time.  exch: S(S-1)/2
+ * exchangeabilities, upper triangle row-major (DNA: AC AG AT CG CT GT);
+ * freqs: S positive frequencies (normalised here).  eigen (host, S+2S^2
+ * doubles) = lambda[S] (descending, lambda_0 = 0) | V[S*S] | Vinv[S*S],
+ * row-major, Q = V diag(lambda) Vinv.  Host-only; 2 <= S <= 64. */
+int plfx_model_eigen(int states, const double *exch, const double *freqs, double *eigen);
+
+/* Yang (1994) discrete Gamma: ncat equal-probability categories of a
+ * Gamma(alpha, alpha) (mean 1); rate = category mean (median = 0) or the
+ * median rescaled to mean 1 (median != 0).  Host-only. */
+int plfx_gamma_rates(double alpha, int ncat, int median, double *rates);
+
+/* EV (S*S, host) for a convention: STATE -> identity; EIGEN -> EV[k][l] =
+ * Vinv[l][k] (CLVs in eigen coordinates, the RAxML form of plf()). */
+int plfx_model_ev(int states, int convention, const double *eigen, double *EV);
+
+/* Root weights w (S, host) for plfx_root_lnl's `freq`: STATE -> freqs;
+ * EIGEN -> w[k] = sum_s pi_s V[s][k] (the root CLV is in eigen coordinates). */
+int plfx_model_root_weights(int states, int convention, const double *eigen, const double *freqs,
+                            double *w);
+
+/* Device: pmats[b][c][k][l] (nbranch * ncat * S * S values of dtype) from the
+ * eigensystem (device, S+2S^2 doubles, as plfx_model_eigen), category rates
+ * (device, ncat doubles) and branch lengths (device, nbranch doubles):
+ *   STATE: P_c(t_b) = V diag(exp(lambda r_c t_b)) Vinv;
+ *   EIGEN: V[k][l] exp(lambda_l r_c t_b).
+ * Branch 2j / 2j+1 are P-matrix pair j's left / right (the traverse layout).
+ * f64 arithmetic (device exp, within a few ulp of the host libm). */
+int plfx_pmatrix(plfx_ctx *ctx, int dtype, int states, int convention, const double *eigen,
+                 const double *rates, int ncat, const double *blen, int64_t nbranch, void *pmats,
+                 void *stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

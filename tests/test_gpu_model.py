@@ -1,0 +1,142 @@
+"""GPU tests of P-matrix generation (plfx.h section 9)
+and of the whole likelihood pipeline built from it: GTR+Gamma4 eigensystem ->
+device P matrices -> traversal (tips as state codes) -> root lnL, against an
+independent numpy Felsenstein pruning that uses scipy.linalg.expm.  The
+reference has no model code: "parity unpinned" against it; the bar is the
+north-star f64 tolerance, 1e-10 relative."""
+import numpy as np
+import pytest
+
+import plfx
+from scipy.linalg import expm
+
+pytestmark = pytest.mark.gpu
+
+LNL_RTOL = 1e-10
+
+
+def dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def gtr_q(exch, freqs):
+    S = len(freqs)
+    pi = np.asarray(freqs, float) / np.sum(freqs)
+    R = np.zeros((S, S))
+    R[np.triu_indices(S, 1)] = exch
+    R = R + R.T
+    Q = R * pi[None, :]
+    np.fill_diagonal(Q, -Q.sum(axis=1))
+    return Q / -(pi * np.diag(Q)).sum(), pi
+
+
+@pytest.mark.parametrize("S", [4, 20])
+@pytest.mark.parametrize("conv", [plfx.PMAT_STATE, plfx.PMAT_EIGEN])
+def test_pmatrix_vs_expm(ctx, S, conv):
+    import torch
+
+    rng = np.random.default_rng(S + conv)
+    exch = rng.random(S * (S - 1) // 2) * 2 + 0.05
+    freqs = rng.random(S) + 0.1
+    Q, pi = gtr_q(exch, freqs)
+    e = plfx.model_eigen(exch, freqs)
+    lam, V, Vi = e[:S], e[S:S + S * S].reshape(S, S), e[S + S * S:].reshape(S, S)
+    rates = plfx.gamma_rates(0.7, 4)
+    blen = np.concatenate([[0.0, 1e-6], rng.random(37) * 2, [10.0]])
+    out = torch.empty(blen.size * 4 * S * S, dtype=torch.float64, device="cuda")
+    ctx.pmatrix(dev(e), dev(rates), dev(blen), out, states=S, convention=conv)
+    out32 = torch.empty(out.numel(), dtype=torch.float32, device="cuda")
+    ctx.pmatrix(dev(e), dev(rates), dev(blen), out32, states=S, convention=conv)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(blen.size, 4, S, S)
+    for b, t in enumerate(blen):
+        for c in range(4):
+            if conv == plfx.PMAT_STATE:
+                exp_ = expm(Q * rates[c] * t)
+                assert np.abs(got[b, c] - exp_).max() < 1e-12, (b, c)
+            else:
+                exp_ = V * np.exp(lam * rates[c] * t)[None, :]
+                assert np.allclose(got[b, c], exp_, rtol=1e-13, atol=1e-15), (b, c)
+    assert np.array_equal(out32.cpu().numpy(), out.cpu().numpy().astype(np.float32)) or \
+        np.allclose(out32.cpu().numpy(), out.cpu().numpy(), rtol=2e-7, atol=1e-30)
+
+
+def felsenstein_lnl(Q, pi, rates, catw, blen, ops, tipx, ntips, wgt):
+    """Independent numpy pruning: CLVs (n, C, S) in state space, per-site
+    log-scale kept separately, P = expm(Q r t)."""
+    C = len(rates)
+    clv = {t: (tipx[t], np.zeros(tipx[t].shape[0])) for t in range(ntips)}
+    for p, c1, c2, m in ops:
+        out = None
+        logs = clv[c1][1] + clv[c2][1]
+        for side, (child, bl) in enumerate(((c1, blen[2 * m]), (c2, blen[2 * m + 1]))):
+            x = clv[child][0]
+            u = np.stack([x[:, c, :] @ expm(Q * rates[c] * bl).T for c in range(C)], axis=1)
+            out = u if out is None else out * u
+        mx = out.reshape(out.shape[0], -1).max(axis=1)
+        clv[p] = (out / mx[:, None, None], logs + np.log(mx))
+    root, logs = clv[ops[-1][0]]
+    site = np.einsum("c,ncs,s->n", catw, root, pi)
+    return float(np.sum(wgt * (np.log(site) + logs)))
+
+
+@pytest.mark.parametrize("conv", [plfx.PMAT_STATE, plfx.PMAT_EIGEN])
+def test_gtr_gamma_pipeline_lnl(ctx, oracle, conv):
+    """GTR+G4 on a 16-taxon balanced tree, 5000 sites: device P matrices ->
+    traverse -> root lnL equals the numpy pruning within 1e-10 relative.
+    STATE: tips as uint8 state codes, EV = I.  EIGEN: tips as dense eigen-
+    coordinate CLVs Vinv.bits, EV = Vinv^T, root weights pi.V."""
+    import torch
+
+    rng = np.random.default_rng(31 + conv)
+    n, ntips = 5000, 16
+    exch = np.array([1.2, 3.9, 0.8, 1.1, 4.6, 1.0])
+    freqs = np.array([0.31, 0.19, 0.22, 0.28])
+    Q, pi = gtr_q(exch, freqs)
+    e = plfx.model_eigen(exch, freqs)
+    Vi = e[4 + 16:].reshape(4, 4)
+    rates = plfx.gamma_rates(0.42, 4)
+    catw = np.full(4, 0.25)
+    ops = oracle.balanced_tree_ops(ntips)
+    nops = ops.shape[0]
+    blen = rng.random(2 * nops) * 0.3 + 0.01
+    codes = [oracle.random_tip_codes(rng, n, 0.05) for _ in range(ntips)]
+    codes = [np.where((c & 15) == 0, 15, c).astype(np.uint8) for c in codes]  # no empty sets
+    wgt = rng.integers(1, 4, n).astype(np.int32)
+    tipx = [oracle.expand_tips(c).reshape(n, 4, 4) for c in codes]
+    exp_lnl = felsenstein_lnl(Q, pi, rates, catw, blen, ops, tipx, ntips, wgt)
+
+    pm = torch.empty(2 * nops * 64, dtype=torch.float64, device="cuda")
+    ctx.pmatrix(dev(e), dev(rates), dev(blen), pm, states=4, convention=conv)
+    EV = dev(plfx.model_ev(e, 4, conv))
+    nslots = ntips + nops
+    clv = [torch.empty(16 * n, dtype=torch.float64, device="cuda") for _ in range(nops)]
+    if conv == plfx.PMAT_STATE:
+        tips = [dev(c) for c in codes] + [None] * nops
+        clv = [None] * ntips + clv
+    else:
+        tips = None
+        clv = [dev(np.einsum("ls,ncs->ncl", Vi, x).reshape(-1)) for x in tipx] + clv
+    sums = torch.zeros(nops, dtype=torch.int64, device="cuda")
+    ctx.traverse(ops, clv, pm, EV, n, dev(wgt), None, sums, tips=tips)
+    w = dev(plfx.model_root_weights(e, freqs, conv))
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    ctx.root_lnl(clv[nslots - 1], n, out, catw=dev(catw), freq=w, wgt=dev(wgt), scaler_sums=sums)
+    torch.cuda.synchronize()
+    got = float(out.item())
+    assert abs(got - exp_lnl) <= LNL_RTOL * abs(exp_lnl), (got, exp_lnl)
+
+
+def test_pmatrix_rejects_bad_args(ctx):
+    import torch
+
+    e = dev(plfx.model_eigen(np.ones(6), np.full(4, 0.25)))
+    r = dev(np.ones(4))
+    b = dev(np.ones(3))
+    out = torch.empty(3 * 64, dtype=torch.float64, device="cuda")
+    with pytest.raises(plfx.PlfxError):
+        ctx.pmatrix(e, r, b, out, convention=7)
+    with pytest.raises(plfx.PlfxError):
+        ctx.pmatrix(e, r, b, out[:10])

@@ -1,0 +1,106 @@
+"""CPU tests of the host-side model setup (plfx.h
+section 9): GTR eigensystem and Yang (1994) discrete-Gamma rates.  The
+reference has no model code (its P/EV inputs are random or precomputed), so
+these are pinned by independent implementations -- scipy.linalg.expm,
+scipy.stats.gamma / scipy.special.gammainc -- and the published Yang (1994)
+table; "parity unpinned" against the reference itself.  Host-only functions of
+libplfx: no GPU is touched."""
+import numpy as np
+import pytest
+
+import plfx
+from scipy.linalg import expm
+from scipy.special import gammainc
+from scipy.stats import gamma as gamma_dist
+
+
+def gtr_q(exch, freqs):
+    S = len(freqs)
+    pi = np.asarray(freqs, float) / np.sum(freqs)
+    R = np.zeros((S, S))
+    R[np.triu_indices(S, 1)] = exch
+    R = R + R.T
+    Q = R * pi[None, :]
+    np.fill_diagonal(Q, -Q.sum(axis=1))
+    return Q / -(pi * np.diag(Q)).sum(), pi
+
+
+def split(e, S):
+    return e[:S], e[S:S + S * S].reshape(S, S), e[S + S * S:].reshape(S, S)
+
+
+@pytest.mark.parametrize("S,seed", [(4, 0), (4, 1), (20, 2), (2, 3), (7, 4)])
+def test_eigen_reconstructs_q_and_expm(S, seed):
+    rng = np.random.default_rng(seed)
+    exch = rng.random(S * (S - 1) // 2) * 3 + 0.01
+    freqs = rng.random(S) + 0.05
+    Q, pi = gtr_q(exch, freqs)
+    lam, V, Vi = split(plfx.model_eigen(exch, freqs), S)
+    assert np.abs(V @ Vi - np.eye(S)).max() < 1e-12
+    assert np.abs(V @ np.diag(lam) @ Vi - Q).max() < 1e-12
+    assert abs(lam[0]) < 1e-12 and np.all(np.diff(lam) <= 1e-15)
+    for t in (0.0, 0.01, 0.3, 2.0, 25.0):
+        P = V @ np.diag(np.exp(lam * t)) @ Vi
+        assert np.abs(P - expm(Q * t)).max() < 1e-12, t
+
+
+def test_eigen_jc69_closed_form():
+    """Jukes-Cantor: P_ii(t) = 1/4 + 3/4 exp(-4t/3)."""
+    lam, V, Vi = split(plfx.model_eigen(np.ones(6), np.full(4, 0.25)), 4)
+    assert np.allclose(lam, [0, -4 / 3, -4 / 3, -4 / 3], atol=1e-14)
+    t = 0.37
+    P = V @ np.diag(np.exp(lam * t)) @ Vi
+    assert np.allclose(np.diag(P), 0.25 + 0.75 * np.exp(-4 * t / 3), rtol=0, atol=1e-15)
+    assert np.allclose(P[0, 1], 0.25 - 0.25 * np.exp(-4 * t / 3), rtol=0, atol=1e-15)
+
+
+def test_gamma_rates_yang1994_table():
+    """Yang (1994), alpha = 0.5, K = 4, mean rates."""
+    r = plfx.gamma_rates(0.5, 4)
+    assert np.allclose(r, [0.0334, 0.2519, 0.8203, 2.8944], atol=5e-5)
+
+
+@pytest.mark.parametrize("alpha", [0.02, 0.1, 0.5, 1.0, 3.7, 50.0, 400.0])
+@pytest.mark.parametrize("K", [1, 2, 4, 8])
+def test_gamma_rates_vs_scipy(alpha, K):
+    mean = plfx.gamma_rates(alpha, K)
+    med = plfx.gamma_rates(alpha, K, median=True)
+    assert abs(mean.mean() - 1) < 1e-12 and abs(med.mean() - 1) < 1e-12
+    if K == 1:
+        assert mean[0] == 1.0 and med[0] == 1.0
+        return
+    q = gamma_dist.ppf(np.arange(1, K) / K, alpha, scale=1 / alpha)
+    cdf1 = np.concatenate([[0.0], gammainc(alpha + 1, alpha * q), [1.0]])
+    exp_mean = K * np.diff(cdf1)
+    assert np.allclose(mean, exp_mean, rtol=1e-9, atol=1e-13)
+    m = gamma_dist.ppf((2 * np.arange(K) + 1) / (2 * K), alpha, scale=1 / alpha)
+    assert np.allclose(med, m * K / m.sum(), rtol=1e-9, atol=1e-13)
+
+
+def test_ev_and_root_weights():
+    rng = np.random.default_rng(9)
+    exch, freqs = rng.random(6) + 0.1, rng.random(4) + 0.1
+    e = plfx.model_eigen(exch, freqs)
+    lam, V, Vi = split(e, 4)
+    assert np.array_equal(plfx.model_ev(e, 4, plfx.PMAT_STATE), np.eye(4).reshape(-1))
+    assert np.array_equal(plfx.model_ev(e, 4, plfx.PMAT_EIGEN), Vi.T.reshape(-1))
+    pi = freqs / freqs.sum()
+    assert np.allclose(plfx.model_root_weights(e, freqs, plfx.PMAT_STATE), pi, rtol=1e-15)
+    w = plfx.model_root_weights(e, freqs, plfx.PMAT_EIGEN)
+    assert np.allclose(w, pi @ V, rtol=1e-14)
+    # sum_s pi_s L_s == sum_k w_k (Vinv L)_k for any state-space L
+    Lv = rng.random(4)
+    assert abs(pi @ Lv - w @ (Vi @ Lv)) < 1e-14
+
+
+def test_model_rejects_bad_args():
+    with pytest.raises(plfx.PlfxError):
+        plfx.model_eigen(np.ones(6), [0.5, 0.5, 0.0, 0.0])   # zero frequency
+    with pytest.raises(plfx.PlfxError):
+        plfx.model_eigen(-np.ones(6), np.full(4, 0.25))     # negative rate
+    with pytest.raises(plfx.PlfxError):
+        plfx.model_eigen(np.ones(5), np.full(4, 0.25))      # wrong count
+    with pytest.raises(plfx.PlfxError):
+        plfx.gamma_rates(0.0, 4)
+    with pytest.raises(plfx.PlfxError):
+        plfx.gamma_rates(1.0, 0)
