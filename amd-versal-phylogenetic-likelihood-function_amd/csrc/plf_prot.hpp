@@ -110,33 +110,72 @@ struct ProtTile {
   typedef typename std::conditional<sizeof(T) == 8, f64x2, f32x4>::type V;
 };
 
+// fetch: all K 16-B loads of a thread in flight at once (a load->wait->write
+// chain per chunk would serialise K HBM round trips per tile); put: into the
+// padded LDS layout.  Split so a kernel can keep a fetch in flight across work.
 template <typename T>
-__device__ __forceinline__ void tile_load(const T *__restrict__ g, int64_t base, int64_t n,
-                                          typename ProtTile<T>::V *lds) {
+__device__ __forceinline__ void tile_fetch(const T *__restrict__ g, int64_t base, int64_t n,
+                                           typename ProtTile<T>::V (&v)[ProtTile<T>::kChunks / kBlock]) {
   using PT = ProtTile<T>;
+  constexpr int K = PT::kChunks / kBlock;
   const typename PT::V *src = reinterpret_cast<const typename PT::V *>(g + base * 80);
-  const int64_t lim = (n - base) * PT::kChunksPerSite;  // chunks of valid sites
+  if (base + 64 <= n) {
+#pragma unroll
+    for (int i = 0; i < K; i++) v[i] = __builtin_nontemporal_load(src + threadIdx.x + i * kBlock);
+  } else {
+    const int64_t lim = (n - base) * PT::kChunksPerSite;  // chunks of valid sites
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      const int j = threadIdx.x + i * kBlock;
+      v[i] = typename PT::V{};
+      if (j < lim) v[i] = __builtin_nontemporal_load(src + j);
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void tile_put(typename ProtTile<T>::V *lds,
+                                         const typename ProtTile<T>::V (&v)[ProtTile<T>::kChunks / kBlock]) {
+  using PT = ProtTile<T>;
 #pragma unroll
   for (int i = 0; i < PT::kChunks / kBlock; i++) {
     const int j = threadIdx.x + i * kBlock;
     const int s = j / PT::kChunksPerSite, q = j - s * PT::kChunksPerSite;
-    typename PT::V v = {};
-    if (j < lim) v = __builtin_nontemporal_load(src + j);
-    lds[s * PT::kStride + q] = v;
+    lds[s * PT::kStride + q] = v[i];
   }
+}
+
+template <typename T>
+__device__ __forceinline__ void tile_load(const T *__restrict__ g, int64_t base, int64_t n,
+                                          typename ProtTile<T>::V *lds) {
+  typename ProtTile<T>::V v[ProtTile<T>::kChunks / kBlock];
+  tile_fetch<T>(g, base, n, v);
+  tile_put<T>(lds, v);
 }
 
 template <typename T>
 __device__ __forceinline__ void tile_store(T *__restrict__ g, int64_t base, int64_t n,
                                            const typename ProtTile<T>::V *lds) {
   using PT = ProtTile<T>;
+  constexpr int K = PT::kChunks / kBlock;
   typename PT::V *dst = reinterpret_cast<typename PT::V *>(g + base * 80);
-  const int64_t lim = (n - base) * PT::kChunksPerSite;
+  typename PT::V v[K];
 #pragma unroll
-  for (int i = 0; i < PT::kChunks / kBlock; i++) {
+  for (int i = 0; i < K; i++) {
     const int j = threadIdx.x + i * kBlock;
     const int s = j / PT::kChunksPerSite, q = j - s * PT::kChunksPerSite;
-    if (j < lim) __builtin_nontemporal_store(lds[s * PT::kStride + q], dst + j);
+    v[i] = lds[s * PT::kStride + q];
+  }
+  if (base + 64 <= n) {
+#pragma unroll
+    for (int i = 0; i < K; i++) __builtin_nontemporal_store(v[i], dst + threadIdx.x + i * kBlock);
+  } else {
+    const int64_t lim = (n - base) * PT::kChunksPerSite;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      const int j = threadIdx.x + i * kBlock;
+      if (j < lim) __builtin_nontemporal_store(v[i], dst + j);
+    }
   }
 }
 
@@ -174,8 +213,8 @@ __device__ __forceinline__ void row_write(typename ProtTile<T>::V *lds, int site
 
 // kAblate (tuning only, tools/tune_plf.hip): 0 = the kernel; 1 = skip the
 // arithmetic (o = a + b); 2 = skip the child-tile traffic (a, b synthesised).
-template <typename T, bool kFma, bool kSum, int kAblate = 0>
-__global__ void __launch_bounds__(kBlock)
+template <typename T, bool kFma, bool kSum, int kAblate = 0, int kMinWaves = 2>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
                 const T *__restrict__ EV, const T *__restrict__ left, const T *__restrict__ right,
                 const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
@@ -268,7 +307,7 @@ plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restric
 // whole kernel; B fragments (X^T) come from the LDS tile, conflict-free.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-template <bool kSum, int kMinWaves = 2>
+template <bool kSum, int kMinWaves = 2, bool kPrefetch = true>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                      double *__restrict__ x3, const double *__restrict__ EV,
@@ -298,10 +337,22 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   const double *td = reinterpret_cast<const double *>(tile);
   double *tw = reinterpret_cast<double *>(tile);
   long long acc = 0;
-  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+  // kPrefetch: the next child tile's loads are in flight while the current
+  // one is multiplied (x2 during phase 1, the next trip's x1 during phase 2)
+  f64x2 pf[PT::kChunks / kBlock];
+  const int64_t stride = (int64_t)gridDim.x * 64;
+  if constexpr (kPrefetch)
+    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(x1, (int64_t)blockIdx.x * 64, n, pf);
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
     f64x4 P[4][2];  // per sub-tile: U_L^T, then p = U_L^T * U_R^T
-    tile_load<double>(x1, base, n, tile);
-    __syncthreads();
+    if constexpr (kPrefetch) {
+      tile_put<double>(tile, pf);
+      __syncthreads();
+      tile_fetch<double>(x2, base, n, pf);
+    } else {
+      tile_load<double>(x1, base, n, tile);
+      __syncthreads();
+    }
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
@@ -314,8 +365,14 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       }
     }
     __syncthreads();
-    tile_load<double>(x2, base, n, tile);
-    __syncthreads();
+    if constexpr (kPrefetch) {
+      tile_put<double>(tile, pf);
+      __syncthreads();
+      if (base + stride < n) tile_fetch<double>(x1, base + stride, n, pf);
+    } else {
+      tile_load<double>(x2, base, n, tile);
+      __syncthreads();
+    }
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
@@ -363,16 +420,25 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
     }
     // coalesced store with the rescale of the scaled sites (exact: x 2^32)
     {
+      constexpr int K = PT::kChunks / kBlock;
       f64x2 *dst = reinterpret_cast<f64x2 *>(x3 + base * 80);
-      const int64_t lim = (n - base) * PT::kChunksPerSite;
+      f64x2 v[K];
 #pragma unroll
-      for (int i = 0; i < PT::kChunks / kBlock; i++) {
+      for (int i = 0; i < K; i++) {
         const int j = threadIdx.x + i * kBlock;
         const int sl = j / PT::kChunksPerSite, q = j - sl * PT::kChunksPerSite;
-        if (j < lim) {
-          f64x2 v = tile[sl * PT::kStride + q];
-          if ((all >> sl) & 1ull) v = v * Num<double>::two32();
-          __builtin_nontemporal_store(v, dst + j);
+        v[i] = tile[sl * PT::kStride + q];
+        if ((all >> sl) & 1ull) v[i] = v[i] * Num<double>::two32();
+      }
+      if (base + 64 <= n) {
+#pragma unroll
+        for (int i = 0; i < K; i++) __builtin_nontemporal_store(v[i], dst + threadIdx.x + i * kBlock);
+      } else {
+        const int64_t lim = (n - base) * PT::kChunksPerSite;
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+          const int j = threadIdx.x + i * kBlock;
+          if (j < lim) __builtin_nontemporal_store(v[i], dst + j);
         }
       }
     }

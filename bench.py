@@ -81,7 +81,10 @@ def parse():
     ap.add_argument("--sites", type=int, default=1 << 20)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--buffer-sets", type=int, default=4)
-    ap.add_argument("--fma", action="store_true", help="protein: fused multiply-add mode")
+    ap.add_argument("--fma", action="store_true",
+                    help="protein: fused multiply-add mode (the default; f64 runs on the matrix cores)")
+    ap.add_argument("--exact", action="store_true",
+                    help="protein: plf()'s separate multiply/add (bit-identical to the double loop)")
     ap.add_argument("--tips", action="store_true",
                     help="tree64: tips as uint8 state codes (plfx.h section 8) instead of dense CLVs")
     ap.add_argument("--workload", choices=["node", "tree64", "nodes64", "protein"], default="node",
@@ -313,7 +316,7 @@ class ProteinWorkload:
         n = a.sites if a.sites != (1 << 20) else (1 << 18)
         R = max(1, a.buffer_sets)
         V = 80
-        self.n, self.R, self.ctx, self.fma = n, R, ctx, a.fma
+        self.n, self.R, self.ctx, self.fma = n, R, ctx, not a.exact
         self.EV = torch.rand(400, dtype=tdt, device=dev, generator=g) - 0.25
         self.left = torch.rand(1600, dtype=tdt, device=dev, generator=g)
         self.right = torch.rand(1600, dtype=tdt, device=dev, generator=g)
@@ -331,7 +334,7 @@ class ProteinWorkload:
         self.bytes_per_step = self.bytes_per_site * n
         self.config = {
             "workload": f"Protein 20-state x 4 Gamma cats, 1 inner node per GPU per step, {n} sites, "
-                        f"{a.dtype}, {'FMA' if a.fma else 'exact'} (BASELINE configs[4])",
+                        f"{a.dtype}, {('FMA (within 1e-12 of exact)' if esz == 8 else 'FMA') if self.fma else 'exact'} (BASELINE configs[4])",
             "sites_per_gpu_per_step": n, "nodes_per_gpu_per_step": 1, "buffer_sets": R}
 
     def step(self, i, sh):
