@@ -159,6 +159,18 @@ hipError_t launch_prot_mfma_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <bool kSum>
+hipError_t launch_prot_exact64_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
+  static int cache = 0;
+  auto kernel = &dev::plf_prot_exact_f64_kernel<kSum>;
+  const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
+                     (const double *)a.x2, (double *)a.x3, (const double *)a.EV,
+                     (const double *)a.left, (const double *)a.right, a.wgt, a.scaler, a.n, a.ws,
+                     a.scaler_sum);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s) {
@@ -166,7 +178,9 @@ hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks
     if (fma)  // matrix cores: bit-identical to the fused VALU chain (plf_prot.hpp)
       return a.scaler_sum ? launch_prot_mfma_t<true>(a, max_blocks, s)
                           : launch_prot_mfma_t<false>(a, max_blocks, s);
-    return launch_prot_s<double, false>(a, max_blocks, s);
+    // exact: matrices broadcast from LDS (plf_prot.hpp)
+    return a.scaler_sum ? launch_prot_exact64_t<true>(a, max_blocks, s)
+                        : launch_prot_exact64_t<false>(a, max_blocks, s);
   }
   return fma ? launch_prot_s<float, true>(a, max_blocks, s)
              : launch_prot_s<float, false>(a, max_blocks, s);

@@ -292,6 +292,142 @@ plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restric
 }
 
 // ---------------------------------------------------------------------------
+// EXACT mode, f64: the matrices live in LDS (P_L and P_R of the 4 categories
+// and EV, 28.8 KB per block) and every value is a wave-uniform ds_read_b128
+// broadcast -- 2 values per 4 LDS cycles and no VALU issue, where the
+// register-distributed form above pays 2 v_readlane (plus hazard nops) per
+// value on the VALU, which is the binding unit of exact mode (every
+// multiply-add is two f64 instructions).  Phases per 64-site tile and wave
+// (= category), each with plf()'s order:
+//   1: U[k]  = sum_l x1[l] * P_L[k][l]        2: U[k] *= sum_l x2[l] * P_R[k][l]
+//   3: O[l]  = sum_k U[k] * EV[k][l]
+// A matrix streams through registers one row ahead of its use; an empty asm
+// that consumes the previous row's result pins that distance (left alone, the
+// compiler hoists a phase's 200 reads to its start and spills them), and an
+// opaque per-trip offset keeps the reads inside the site loop.
+template <bool kSum, int kMinWaves = 2>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                          double *__restrict__ x3, const double *__restrict__ EV,
+                          const double *__restrict__ left, const double *__restrict__ right,
+                          const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                          unsigned long long *ws, int64_t *scaler_sum) {
+  constexpr int S = 20;
+  using PT = ProtTile<double>;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  __shared__ f64x2 mats[(2 * 4 * S * S + S * S) / 2];  // P_L[4][400] | P_R[4][400] | EV[400]
+  {
+    const f64x2 *gl = reinterpret_cast<const f64x2 *>(left);
+    const f64x2 *gr = reinterpret_cast<const f64x2 *>(right);
+    const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
+    for (int i = threadIdx.x; i < 800; i += kBlock) {
+      mats[i] = gl[i];
+      mats[800 + i] = gr[i];
+    }
+    for (int i = threadIdx.x; i < 200; i += kBlock) mats[1600 + i] = ge[i];
+  }
+  const double m = Num<double>::minlik();
+  __shared__ PT::V tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock];
+  long long acc = 0;
+  __syncthreads();
+  // rows M[k] (10 x f64x2) feed fn(k, row), which returns a value of its result
+  auto phase = [&](const f64x2 *M, auto &&fn) {
+    f64x2 cur[10], nxt[10];
+    int o = 0;
+    double tok = 0.0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) cur[i] = M[i];
+#pragma unroll
+    for (int k = 0; k < S; k++) {
+      asm volatile("" : "+v"(o) : "v"(tok));  // row k+1 is read after row k-1 is used
+      if (k + 1 < S) {
+#pragma unroll
+        for (int i = 0; i < 10; i++) nxt[i] = M[o + (k + 1) * 10 + i];
+      }
+      tok = fn(k, cur);
+#pragma unroll
+      for (int i = 0; i < 10; i++) cur[i] = nxt[i];
+    }
+  };
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    const f64x2 *mL = mats + off + c * 200, *mR = mats + off + 800 + c * 200, *mE = mats + off + 1600;
+    double U[S];
+    {
+      double a[S];
+      tile_load<double>(x1, base, n, tile);
+      __syncthreads();
+      row_read<double>(tile, lane, c, a);
+      __syncthreads();
+      phase(mL, [&](int k, const f64x2 (&p)[10]) {
+        double u = 0.0;
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+          u += a[2 * i] * p[i].x;
+          u += a[2 * i + 1] * p[i].y;
+        }
+        U[k] = u;
+        return u;
+      });
+    }
+    {
+      double b[S];
+      tile_load<double>(x2, base, n, tile);
+      __syncthreads();
+      row_read<double>(tile, lane, c, b);
+      __syncthreads();
+      phase(mR, [&](int k, const f64x2 (&p)[10]) {
+        double u = 0.0;
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+          u += b[2 * i] * p[i].x;
+          u += b[2 * i + 1] * p[i].y;
+        }
+        U[k] = U[k] * u;
+        return U[k];
+      });
+    }
+    double O[S];
+#pragma unroll
+    for (int l = 0; l < S; l++) O[l] = 0.0;
+    phase(mE, [&](int k, const f64x2 (&e)[10]) {
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        O[2 * i] += U[k] * e[i].x;
+        O[2 * i + 1] += U[k] * e[i].y;
+      }
+      return O[S - 1];
+    });
+    bool small = base + lane < n;
+#pragma unroll
+    for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
+    const unsigned long long mk = __ballot(small);
+    if (lane == 0) small_mask[c] = mk;
+    __syncthreads();  // also: every wave is done reading x2 from the tile
+    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+    const bool sc = (all >> lane) & 1ull;
+#pragma unroll
+    for (int l = 0; l < S; l++) {
+      const double sv = O[l] * Num<double>::two32();
+      O[l] = sc ? sv : O[l];
+    }
+    row_write<double>(tile, lane, c, O);
+    const int64_t site = base + lane;
+    if (site < n && c == 0) {
+      if (scaler) scaler[site] = (uint8_t)sc;
+      if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+    }
+    __syncthreads();
+    tile_store<double>(x3, base, n, tile);
+    __syncthreads();  // tile and small_mask are reused by the next trip
+  }
+  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
+// ---------------------------------------------------------------------------
 // FMA mode on the matrix cores (f64).  v_mfma_f64_16x16x4_f64 is bit-for-bit a
 // k-ordered fma chain (probed on MI355X: tools/probes/mfma_f64_numerics.hip),
 // so this kernel reproduces plf()'s loop with every multiply-add fused, in the

@@ -154,5 +154,481 @@ prot_phased_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
   block_ticket_sum(acc, ws, scaler_sum);
 }
 
+// Matrices in LDS, read as wave-uniform ds_read_b128 broadcasts (2 values per
+// 4 LDS cycles, no VALU cost) instead of v_readlane; NS sites per lane.  Rows
+// are double-buffered in registers by hand: row k+1 is read, then an empty
+// asm with a memory clobber pins the order, then row k is used -- otherwise
+// the compiler hoists a whole phase's 200 reads and spills them.
+template <int NS>
+struct RowPipe {
+  f64x2 cur[10], nxt[10];
+  __device__ __forceinline__ void load(f64x2 (&d)[10], const f64x2 *row) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) d[i] = row[i];
+  }
+};
+
+template <int NS, int kMinBlocks = 2>
+__global__ void __launch_bounds__(kBlock, kMinBlocks)
+prot_ldsmat_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                   double *__restrict__ x3, const double *__restrict__ EV,
+                   const double *__restrict__ left, const double *__restrict__ right,
+                   const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                   unsigned long long *ws, int64_t *scaler_sum) {
+  constexpr int S = 20;
+  using PT = ProtTile<double>;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  __shared__ f64x2 mats[(2 * 4 * S * S + S * S) / 2];  // PL[4][400] | PR[4][400] | EV[400]
+  {
+    const f64x2 *gl = reinterpret_cast<const f64x2 *>(left);
+    const f64x2 *gr = reinterpret_cast<const f64x2 *>(right);
+    const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
+    for (int i = threadIdx.x; i < 800; i += kBlock) { mats[i] = gl[i]; mats[800 + i] = gr[i]; }
+    for (int i = threadIdx.x; i < 200; i += kBlock) mats[1600 + i] = ge[i];
+  }
+  const double m = Num<double>::minlik();
+  __shared__ PT::V tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock][NS];
+  long long acc = 0;
+  __syncthreads();
+  // one phase: for k, rows M[k] (10 x f64x2) feed fn(k, row)
+  auto phase = [&](const f64x2 *M, auto &&fn) {
+    f64x2 cur[10], nxt[10];
+    int o = 0;
+    double tok = 0.0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) cur[i] = M[i];
+#pragma unroll
+    for (int k = 0; k < S; k++) {
+      // row k+1's reads wait for row k-1's arithmetic (tok): at most two rows
+      // of the matrix are in registers, whatever the scheduler prefers
+      asm volatile("" : "+v"(o) : "v"(tok));
+      if (k + 1 < S) {
+#pragma unroll
+        for (int i = 0; i < 10; i++) nxt[i] = M[o + (k + 1) * 10 + i];
+      }
+      tok = fn(k, cur);
+#pragma unroll
+      for (int i = 0; i < 10; i++) cur[i] = nxt[i];
+    }
+  };
+  for (int64_t base = (int64_t)blockIdx.x * 64 * NS; base < n; base += (int64_t)gridDim.x * 64 * NS) {
+    int off = 0;  // opaque per trip: the matrix reads are not hoisted out of the loop
+    asm volatile("" : "+v"(off));
+    const f64x2 *mL = mats + off + c * 200, *mR = mats + off + 800 + c * 200, *mE = mats + off + 1600;
+    double U[NS][S];
+    {
+      double a[NS][S];
+#pragma unroll
+      for (int s = 0; s < NS; s++) {
+        tile_load<double>(x1, base + 64 * s, n, tile);
+        __syncthreads();
+        row_read<double>(tile, lane, c, a[s]);
+        __syncthreads();
+      }
+      phase(mL, [&](int k, const f64x2 (&p)[10]) {
+        double u[NS];
+#pragma unroll
+        for (int s = 0; s < NS; s++) u[s] = 0.0;
+#pragma unroll
+        for (int l2 = 0; l2 < S / 2; l2++)
+#pragma unroll
+          for (int s = 0; s < NS; s++) { u[s] += a[s][2 * l2] * p[l2].x; u[s] += a[s][2 * l2 + 1] * p[l2].y; }
+#pragma unroll
+        for (int s = 0; s < NS; s++) U[s][k] = u[s];
+        return u[0];
+      });
+    }
+    {
+      double b[NS][S];
+#pragma unroll
+      for (int s = 0; s < NS; s++) {
+        tile_load<double>(x2, base + 64 * s, n, tile);
+        __syncthreads();
+        row_read<double>(tile, lane, c, b[s]);
+        __syncthreads();
+      }
+      phase(mR, [&](int k, const f64x2 (&p)[10]) {
+        double u[NS];
+#pragma unroll
+        for (int s = 0; s < NS; s++) u[s] = 0.0;
+#pragma unroll
+        for (int l2 = 0; l2 < S / 2; l2++)
+#pragma unroll
+          for (int s = 0; s < NS; s++) { u[s] += b[s][2 * l2] * p[l2].x; u[s] += b[s][2 * l2 + 1] * p[l2].y; }
+#pragma unroll
+        for (int s = 0; s < NS; s++) U[s][k] = U[s][k] * u[s];
+        return U[0][k];
+      });
+    }
+    double O[NS][S];
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+      for (int l = 0; l < S; l++) O[s][l] = 0.0;
+    phase(mE, [&](int k, const f64x2 (&e)[10]) {
+#pragma unroll
+      for (int l2 = 0; l2 < S / 2; l2++)
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+          O[s][2 * l2] += U[s][k] * e[l2].x;
+          O[s][2 * l2 + 1] += U[s][k] * e[l2].y;
+        }
+      return O[0][S - 1];
+    });
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      bool small = base + 64 * s + lane < n;
+#pragma unroll
+      for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[s][l]) < m);
+      const unsigned long long mk = __ballot(small);
+      if (lane == 0) small_mask[c][s] = mk;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      const unsigned long long all =
+          small_mask[0][s] & small_mask[1][s] & small_mask[2][s] & small_mask[3][s];
+      const bool sc = (all >> lane) & 1ull;
+#pragma unroll
+      for (int l = 0; l < S; l++) {
+        const double sv = O[s][l] * Num<double>::two32();
+        O[s][l] = sc ? sv : O[s][l];
+      }
+      row_write<double>(tile, lane, c, O[s]);
+      const int64_t site = base + 64 * s + lane;
+      if (site < n && c == 0) {
+        if (scaler) scaler[site] = (uint8_t)sc;
+        if (sc) acc += wgt ? (long long)wgt[site] : 1ll;
+      }
+      __syncthreads();
+      tile_store<double>(x3, base + 64 * s, n, tile);
+      __syncthreads();
+    }
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
+// As prot_ldsmat_kernel, pipelined by half rows (10 values): row k of a
+// matrix is two halves q = 2k, 2k+1; at most two halves are in registers.
+template <int NS, int kMinBlocks = 2>
+__global__ void __launch_bounds__(kBlock, kMinBlocks)
+prot_ldsmat_h_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                     double *__restrict__ x3, const double *__restrict__ EV,
+                     const double *__restrict__ left, const double *__restrict__ right,
+                     const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                     unsigned long long *ws, int64_t *scaler_sum) {
+  constexpr int S = 20;
+  using PT = ProtTile<double>;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  __shared__ f64x2 mats[(2 * 4 * S * S + S * S) / 2];  // PL[4][400] | PR[4][400] | EV[400]
+  {
+    const f64x2 *gl = reinterpret_cast<const f64x2 *>(left);
+    const f64x2 *gr = reinterpret_cast<const f64x2 *>(right);
+    const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
+    for (int i = threadIdx.x; i < 800; i += kBlock) { mats[i] = gl[i]; mats[800 + i] = gr[i]; }
+    for (int i = threadIdx.x; i < 200; i += kBlock) mats[1600 + i] = ge[i];
+  }
+  const double m = Num<double>::minlik();
+  __shared__ PT::V tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock][NS];
+  long long acc = 0;
+  __syncthreads();
+  // fn(q, half) for q = 0..39 (row q>>1, values 10*(q&1) .. +9); returns a token
+  auto phase = [&](const f64x2 *M, auto &&fn) {
+    f64x2 cur[5], nxt[5];
+    int o = 0;
+    double tok = 0.0;
+#pragma unroll
+    for (int i = 0; i < 5; i++) cur[i] = M[i];
+#pragma unroll
+    for (int q = 0; q < 2 * S; q++) {
+      asm volatile("" : "+v"(o) : "v"(tok));
+      if (q + 1 < 2 * S) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) nxt[i] = M[o + (q + 1) * 5 + i];
+      }
+      tok = fn(q, cur);
+#pragma unroll
+      for (int i = 0; i < 5; i++) cur[i] = nxt[i];
+    }
+    return tok;
+  };
+  for (int64_t base = (int64_t)blockIdx.x * 64 * NS; base < n; base += (int64_t)gridDim.x * 64 * NS) {
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    const f64x2 *mL = mats + off + c * 200, *mR = mats + off + 800 + c * 200, *mE = mats + off + 1600;
+    double U[NS][S];
+    double tok;
+    {
+      double a[NS][S];
+#pragma unroll
+      for (int s = 0; s < NS; s++) {
+        tile_load<double>(x1, base + 64 * s, n, tile);
+        __syncthreads();
+        row_read<double>(tile, lane, c, a[s]);
+        __syncthreads();
+      }
+      double u[NS];
+      tok = phase(mL, [&](int q, const f64x2 (&p)[5]) {
+        const int k = q >> 1, h = q & 1;
+        if (h == 0) {
+#pragma unroll
+          for (int s = 0; s < NS; s++) u[s] = 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+#pragma unroll
+          for (int s = 0; s < NS; s++) {
+            u[s] += a[s][10 * h + 2 * i] * p[i].x;
+            u[s] += a[s][10 * h + 2 * i + 1] * p[i].y;
+          }
+        if (h == 1) {
+#pragma unroll
+          for (int s = 0; s < NS; s++) U[s][k] = u[s];
+        }
+        return u[0];
+      });
+    }
+    {
+      // the x2 tile's loads may not start before phase 1 is done (registers)
+      const double *x2t = x2;
+      asm volatile("" : "+s"(x2t) : "v"(tok));
+      double b[NS][S];
+#pragma unroll
+      for (int s = 0; s < NS; s++) {
+        tile_load<double>(x2t, base + 64 * s, n, tile);
+        __syncthreads();
+        row_read<double>(tile, lane, c, b[s]);
+        __syncthreads();
+      }
+      double u[NS];
+      phase(mR, [&](int q, const f64x2 (&p)[5]) {
+        const int k = q >> 1, h = q & 1;
+        if (h == 0) {
+#pragma unroll
+          for (int s = 0; s < NS; s++) u[s] = 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+#pragma unroll
+          for (int s = 0; s < NS; s++) {
+            u[s] += b[s][10 * h + 2 * i] * p[i].x;
+            u[s] += b[s][10 * h + 2 * i + 1] * p[i].y;
+          }
+        if (h == 1) {
+#pragma unroll
+          for (int s = 0; s < NS; s++) U[s][k] = U[s][k] * u[s];
+        }
+        return u[0];
+      });
+    }
+    double O[NS][S];
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+      for (int l = 0; l < S; l++) O[s][l] = 0.0;
+    phase(mE, [&](int q, const f64x2 (&e)[5]) {
+      const int k = q >> 1, h = q & 1;
+#pragma unroll
+      for (int i = 0; i < 5; i++)
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+          O[s][10 * h + 2 * i] += U[s][k] * e[i].x;
+          O[s][10 * h + 2 * i + 1] += U[s][k] * e[i].y;
+        }
+      return O[0][10 * h + 9];
+    });
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      bool small = base + 64 * s + lane < n;
+#pragma unroll
+      for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[s][l]) < m);
+      const unsigned long long mk = __ballot(small);
+      if (lane == 0) small_mask[c][s] = mk;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      const unsigned long long all =
+          small_mask[0][s] & small_mask[1][s] & small_mask[2][s] & small_mask[3][s];
+      const bool sc = (all >> lane) & 1ull;
+#pragma unroll
+      for (int l = 0; l < S; l++) {
+        const double sv = O[s][l] * Num<double>::two32();
+        O[s][l] = sc ? sv : O[s][l];
+      }
+      row_write<double>(tile, lane, c, O[s]);
+      const int64_t site = base + 64 * s + lane;
+      if (site < n && c == 0) {
+        if (scaler) scaler[site] = (uint8_t)sc;
+        if (sc) acc += wgt ? (long long)wgt[site] : 1ll;
+      }
+      __syncthreads();
+      tile_store<double>(x3, base + 64 * s, n, tile);
+      __syncthreads();
+    }
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
+// NS = 1, rows taken in pairs (k, k+1) by half rows so that phases 1 and 2
+// carry two independent add chains (a single u += a*p chain per row leaves
+// the f64 pipe waiting on its own latency).
+template <int kMinBlocks = 2>
+__global__ void __launch_bounds__(kBlock, kMinBlocks)
+prot_ldsmat_p_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                     double *__restrict__ x3, const double *__restrict__ EV,
+                     const double *__restrict__ left, const double *__restrict__ right,
+                     const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                     unsigned long long *ws, int64_t *scaler_sum) {
+  constexpr int S = 20;
+  using PT = ProtTile<double>;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  __shared__ f64x2 mats[(2 * 4 * S * S + S * S) / 2];  // PL[4][400] | PR[4][400] | EV[400]
+  {
+    const f64x2 *gl = reinterpret_cast<const f64x2 *>(left);
+    const f64x2 *gr = reinterpret_cast<const f64x2 *>(right);
+    const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
+    for (int i = threadIdx.x; i < 800; i += kBlock) { mats[i] = gl[i]; mats[800 + i] = gr[i]; }
+    for (int i = threadIdx.x; i < 200; i += kBlock) mats[1600 + i] = ge[i];
+  }
+  const double m = Num<double>::minlik();
+  __shared__ PT::V tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock];
+  long long acc = 0;
+  __syncthreads();
+  // steps q = 0..19: rows 2(q>>1), 2(q>>1)+1, values 10(q&1) .. +9 of each
+  auto phase2 = [&](const f64x2 *M, auto &&fn) {
+    f64x2 cur[10], nxt[10];
+    int o = 0;
+    double tok = 0.0;
+#pragma unroll
+    for (int i = 0; i < 5; i++) { cur[i] = M[i]; cur[5 + i] = M[10 + i]; }
+#pragma unroll
+    for (int q = 0; q < S; q++) {
+      asm volatile("" : "+v"(o) : "v"(tok));
+      if (q + 1 < S) {
+        const int r = 2 * ((q + 1) >> 1), h = (q + 1) & 1;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          nxt[i] = M[o + r * 10 + 5 * h + i];
+          nxt[5 + i] = M[o + (r + 1) * 10 + 5 * h + i];
+        }
+      }
+      tok = fn(q, cur);
+#pragma unroll
+      for (int i = 0; i < 10; i++) cur[i] = nxt[i];
+    }
+    return tok;
+  };
+  auto phase1 = [&](const f64x2 *M, auto &&fn) {  // one row per step (EV)
+    f64x2 cur[10], nxt[10];
+    int o = 0;
+    double tok = 0.0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) cur[i] = M[i];
+#pragma unroll
+    for (int k = 0; k < S; k++) {
+      asm volatile("" : "+v"(o) : "v"(tok));
+      if (k + 1 < S) {
+#pragma unroll
+        for (int i = 0; i < 10; i++) nxt[i] = M[o + (k + 1) * 10 + i];
+      }
+      tok = fn(k, cur);
+#pragma unroll
+      for (int i = 0; i < 10; i++) cur[i] = nxt[i];
+    }
+    return tok;
+  };
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    const f64x2 *mL = mats + off + c * 200, *mR = mats + off + 800 + c * 200, *mE = mats + off + 1600;
+    double U[S], tok;
+    {
+      double a[S];
+      tile_load<double>(x1, base, n, tile);
+      __syncthreads();
+      row_read<double>(tile, lane, c, a);
+      __syncthreads();
+      double u0 = 0.0, u1 = 0.0;
+      tok = phase2(mL, [&](int q, const f64x2 (&p)[10]) {
+        const int k = 2 * (q >> 1), h = q & 1;
+        if (h == 0) { u0 = 0.0; u1 = 0.0; }
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          u0 += a[10 * h + 2 * i] * p[i].x;
+          u1 += a[10 * h + 2 * i] * p[5 + i].x;
+          u0 += a[10 * h + 2 * i + 1] * p[i].y;
+          u1 += a[10 * h + 2 * i + 1] * p[5 + i].y;
+        }
+        if (h == 1) { U[k] = u0; U[k + 1] = u1; }
+        return u0;
+      });
+    }
+    {
+      const double *x2t = x2;
+      asm volatile("" : "+s"(x2t) : "v"(tok));
+      double b[S];
+      tile_load<double>(x2t, base, n, tile);
+      __syncthreads();
+      row_read<double>(tile, lane, c, b);
+      __syncthreads();
+      double u0 = 0.0, u1 = 0.0;
+      phase2(mR, [&](int q, const f64x2 (&p)[10]) {
+        const int k = 2 * (q >> 1), h = q & 1;
+        if (h == 0) { u0 = 0.0; u1 = 0.0; }
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          u0 += b[10 * h + 2 * i] * p[i].x;
+          u1 += b[10 * h + 2 * i] * p[5 + i].x;
+          u0 += b[10 * h + 2 * i + 1] * p[i].y;
+          u1 += b[10 * h + 2 * i + 1] * p[5 + i].y;
+        }
+        if (h == 1) { U[k] = U[k] * u0; U[k + 1] = U[k + 1] * u1; }
+        return u0;
+      });
+    }
+    double O[S];
+#pragma unroll
+    for (int l = 0; l < S; l++) O[l] = 0.0;
+    phase1(mE, [&](int k, const f64x2 (&e)[10]) {
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        O[2 * i] += U[k] * e[i].x;
+        O[2 * i + 1] += U[k] * e[i].y;
+      }
+      return O[S - 1];
+    });
+    bool small = base + lane < n;
+#pragma unroll
+    for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
+    const unsigned long long mk = __ballot(small);
+    if (lane == 0) small_mask[c] = mk;
+    __syncthreads();
+    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+    const bool sc = (all >> lane) & 1ull;
+#pragma unroll
+    for (int l = 0; l < S; l++) {
+      const double sv = O[l] * Num<double>::two32();
+      O[l] = sc ? sv : O[l];
+    }
+    row_write<double>(tile, lane, c, O);
+    const int64_t site = base + lane;
+    if (site < n && c == 0) {
+      if (scaler) scaler[site] = (uint8_t)sc;
+      if (sc) acc += wgt ? (long long)wgt[site] : 1ll;
+    }
+    __syncthreads();
+    tile_store<double>(x3, base, n, tile);
+    __syncthreads();
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
 }  // namespace dev
 }  // namespace plfx

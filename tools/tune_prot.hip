@@ -90,13 +90,10 @@ int main(int argc, char **argv) {
   }
   ADD_K("product exact", (&plf_prot_kernel<double, false, true>), 64)
   ADD_K("product fma-mfma", (&plf_prot_mfma_kernel<true>), 64)
-  ADD_K("exact minw=1", (&plf_prot_kernel<double, false, true, 0, 1>), 64)
-  ADD_K("exact minw=3", (&plf_prot_kernel<double, false, true, 0, 3>), 64)
-  ADD_K("mfma minw=3", (&plf_prot_mfma_kernel<true, 3>), 64)
-  ADD_K("mfma minw=1", (&plf_prot_mfma_kernel<true, 1>), 64)
-  ADD_K("mfma prefetch minw=1", (&plf_prot_mfma_kernel<true, 1, true>), 64)
-  ADD_K("mfma prefetch minw=2", (&plf_prot_mfma_kernel<true, 2, true>), 64)
-  ADD_K("phased readlane NS=1", (&prot_phased_kernel<false, 1>), 64)
+  ADD_K("ldsmat NS=1", (&prot_ldsmat_kernel<1>), 64)
+  ADD_K("ldsmat-h NS=1", (&prot_ldsmat_h_kernel<1>), 64)
+  ADD_K("ldsmat-pairs", (&prot_ldsmat_p_kernel<2>), 64)
+  ADD_K("ldsmat-pairs minb=3", (&prot_ldsmat_p_kernel<3>), 64)
 
   // FMA-mode reference for the mfma variants
   std::vector<uint64_t> h_fref(n * 80);
