@@ -228,4 +228,24 @@ int plfx_model_root_weights(int states, int convention, const double *eigen, con
   return PLFX_OK;
 }
 
+int plfx_model_tip_vectors(int states, int convention, const double *eigen, double *tv) {
+  const int S = states;
+  if (S != 4 || !tv || (convention != PLFX_PMAT_STATE && convention != PLFX_PMAT_EIGEN))
+    return PLFX_ERR_INVALID;
+  if (convention == PLFX_PMAT_EIGEN && !eigen) return PLFX_ERR_INVALID;
+  const double *Vi = eigen ? eigen + S + (size_t)S * S : nullptr;
+  for (int code = 0; code < 16; code++)
+    for (int k = 0; k < S; k++) {
+      if (convention == PLFX_PMAT_STATE) {
+        tv[code * S + k] = (code >> k) & 1 ? 1.0 : 0.0;
+      } else {
+        double a = 0.0;
+        for (int s = 0; s < S; s++)
+          if ((code >> s) & 1) a += Vi[(size_t)k * S + s];
+        tv[code * S + k] = a;
+      }
+    }
+  return PLFX_OK;
+}
+
 }  // extern "C"

@@ -122,17 +122,21 @@ constexpr int kQuadOdd = 1 | (1 << 2) | (3 << 4) | (3 << 6);   // quad_perm [1,1
 
 // Tip children: a tip is one DNA state code per site (bit s
 // set = state s allowed, the RAxML/PLL convention); its dense CLV would be
-// x[c][s] = bit s of the code for every category c.  A block precomputes
-// tab[c*64 + code*4 + k] = sum_l bit_l(code) * P_c[k][l] in plf()'s order from
-// +0.0 (0.0/1.0 times P is exact), so a tip's ump values are one LDS read and
-// every result is bit-identical to running plf() on the expanded dense CLV.
+// x[c][l] = tv[code][l] for every category c, with tv the tip-vector table
+// (NULL: the 0/1 state indicator, bit l of the code; the eigen convention of
+// plfx.h section 9 passes V^-1 applied to the indicator).  A block
+// precomputes tab[c*64 + code*4 + k] = sum_l tv[code][l] * P_c[k][l] in plf()'s
+// order from +0.0, so a tip's ump values are one LDS read and every result is
+// bit-identical to running plf() on the expanded dense CLV.
 template <typename T>
-__device__ __forceinline__ void build_tip_table(const T *__restrict__ P, T *tab) {
+__device__ __forceinline__ void build_tip_table(const T *__restrict__ P, const T *__restrict__ tv,
+                                                T *tab) {
   const int t = threadIdx.x;  // kBlock == 256 == 4 cats x 16 codes x 4 k
   const int cc = t >> 6, code = (t >> 2) & 15, k = t & 3;
   T v = T(0);
 #pragma unroll
-  for (int l = 0; l < 4; l++) v += T((code >> l) & 1) * P[cc * 16 + k * 4 + l];
+  for (int l = 0; l < 4; l++)
+    v += (tv ? tv[code * 4 + l] : T((code >> l) & 1)) * P[cc * 16 + k * 4 + l];
   tab[t] = v;
 }
 
@@ -205,14 +209,15 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
                                              uint8_t *__restrict__ scaler, int64_t n,
                                              unsigned long long *ws, int64_t *scaler_sum,
                                              const uint8_t *__restrict__ tip1 = nullptr,
-                                             const uint8_t *__restrict__ tip2 = nullptr) {
+                                             const uint8_t *__restrict__ tip2 = nullptr,
+                                             const T *__restrict__ tipvec = nullptr) {
   const int lane = threadIdx.x & 63;
   const int c = lane & 3;     // Gamma category owned by this lane
   const int q = lane >> 2;    // site slot within a 16-site wave step
   const int nib = lane & 60;  // bit offset of this site's nibble in the ballot
   __shared__ T tab1[T1 ? 256 : 1], tab2[T2 ? 256 : 1];
-  if constexpr (T1) build_tip_table<T>(left, tab1);
-  if constexpr (T2) build_tip_table<T>(right, tab2);
+  if constexpr (T1) build_tip_table<T>(left, tipvec, tab1);
+  if constexpr (T2) build_tip_table<T>(right, tipvec, tab2);
   if constexpr (T1 || T2) __syncthreads();
 
   T PL[16], PR[16], E[16];
@@ -346,15 +351,16 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
                                               uint8_t *__restrict__ scaler, int64_t n,
                                               unsigned long long *ws, int64_t *scaler_sum,
                                               const uint8_t *__restrict__ tip1 = nullptr,
-                                              const uint8_t *__restrict__ tip2 = nullptr) {
+                                              const uint8_t *__restrict__ tip2 = nullptr,
+                                              const double *__restrict__ tipvec = nullptr) {
   const int lane = threadIdx.x & 63;
   const int h = lane & 1;          // which half of the category's states / k range
   const int c = (lane >> 1) & 3;   // Gamma category
   const int g = lane >> 3;         // site within the 8-site block of one instruction
   const int sh = lane & 56;        // bit offset of this site's byte in the ballot
   __shared__ double tab1[T1 ? 256 : 1], tab2[T2 ? 256 : 1];
-  if constexpr (T1) build_tip_table<double>(left, tab1);
-  if constexpr (T2) build_tip_table<double>(right, tab2);
+  if constexpr (T1) build_tip_table<double>(left, tipvec, tab1);
+  if constexpr (T2) build_tip_table<double>(right, tipvec, tab2);
   if constexpr (T1 || T2) __syncthreads();
   const int trow = c * 64 + 2 * h;  // + 4*code: this lane's slice of a table row
 
@@ -516,23 +522,24 @@ template <int U, bool kSum, int kMinWaves, bool NTL = false, int kTips = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_f64_pair_batch_kernel(const NodeBatch nodes, const double *__restrict__ EV,
                               const int32_t *__restrict__ wgt, int64_t n,
-                              unsigned long long *ws) {
+                              unsigned long long *ws, const double *__restrict__ tipvec) {
   const NodeDesc &d = nodes.d[blockIdx.y];
   dna_pair_body<U, kSum, NTL, (kTips >= 1), (kTips == 2)>(
       (const double *)d.x1, (const double *)d.x2, (double *)d.x3, EV, (const double *)d.left,
       (const double *)d.right, wgt, d.scaler, n, ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum,
-      (const uint8_t *)d.x1, (const uint8_t *)d.x2);
+      (const uint8_t *)d.x1, (const uint8_t *)d.x2, tipvec);
 }
 
 template <typename T, int U, bool kSum, bool NT, int kMinWaves, int kTips = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_batch_kernel(const NodeBatch nodes, const T *__restrict__ EV,
-                     const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
+                     const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
+                     const T *__restrict__ tipvec) {
   const NodeDesc &d = nodes.d[blockIdx.y];
   dna_cat_body<T, U, kSum, NT, (kTips >= 1), (kTips == 2)>(
       (const T *)d.x1, (const T *)d.x2, (T *)d.x3, EV, (const T *)d.left, (const T *)d.right, wgt,
       d.scaler, n, ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, (const uint8_t *)d.x1,
-      (const uint8_t *)d.x2);
+      (const uint8_t *)d.x2, tipvec);
 }
 
 __global__ void __launch_bounds__(kBlock)

@@ -31,7 +31,7 @@ hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks
 
 // Batched nodes (<= kMaxBatch per launch) sharing EV, n, wgt.  dtype: 0 f32, 1 f64.
 // tips: 0 dense children; 1 x1 of every node is a tip (uint8 state codes);
-// 2 x1 and x2 are tips.
+// 2 x1 and x2 are tips.  tipvec: 16 x 4 tip vectors of dtype (NULL = 0/1 bits).
 struct NodeDescH {
   const void *x1, *x2;
   void *x3;
@@ -42,7 +42,8 @@ struct NodeDescH {
 constexpr int kMaxBatch = 32;
 hipError_t launch_plf_dna_batch(int dtype, const NodeDescH *nodes, int count, const void *EV,
                                 const int32_t *wgt, int64_t n, unsigned long long *ws,
-                                int max_blocks, hipStream_t s, int tips = 0);
+                                int max_blocks, hipStream_t s, int tips = 0,
+                                const void *tipvec = nullptr);
 
 // Root log-likelihood; partials: >= kLnlMaxGrid doubles; ticket: 1 u64 (zero at rest).
 constexpr int kLnlMaxGrid = 4096;

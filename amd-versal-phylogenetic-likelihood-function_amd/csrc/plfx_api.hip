@@ -153,7 +153,8 @@ int plf_host(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int n,
 // Nodes of one kind (tips = number of tip children, tip child first) in
 // launches of kMaxBatch.  A tip child is a uint8 code array (no alignment rule).
 int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, const void *EV,
-               int64_t n, const int32_t *wgt, hipStream_t s, int tips) {
+               int64_t n, const int32_t *wgt, hipStream_t s, int tips,
+               const void *tipvec = nullptr) {
   if (count < 0 || n < 0 || (count > 0 && (!nodes || !EV)))
     return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
   for (int i = 0; i < count; i++) {
@@ -172,7 +173,8 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
   for (int i = 0; i < count; i += plfx::kMaxBatch) {
     const int c = std::min(plfx::kMaxBatch, count - i);
     hipError_t e = plfx::launch_plf_dna_batch(dtype, reinterpret_cast<const plfx::NodeDescH *>(nodes + i),
-                                              c, EV, wgt, n, ctx->ws, ctx->max_blocks, s, tips);
+                                              c, EV, wgt, n, ctx->ws, ctx->max_blocks, s, tips,
+                                              tipvec);
     if (e != hipSuccess) return hip_fail(ctx, e, "plf batch launch");
   }
   return PLFX_OK;
@@ -343,7 +345,7 @@ int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *no
 int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void *x1,
                       const uint8_t *tip2, const void *x2, void *x3, const void *EV, int64_t n,
                       const void *left, const void *right, const int32_t *wgt, uint8_t *scaler,
-                      int64_t *scaler_sum, void *stream) {
+                      int64_t *scaler_sum, const void *tipvec, void *stream) {
   if (!ctx) return PLFX_ERR_INVALID;
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
   if ((tip1 != nullptr) == (x1 != nullptr) || (tip2 != nullptr) == (x2 != nullptr))
@@ -355,7 +357,7 @@ int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void 
     std::swap(nd.x1, nd.x2);
     std::swap(nd.left, nd.right);
   }
-  return batch_impl(ctx, dtype, &nd, 1, EV, n, wgt, pick(ctx, stream), tips);
+  return batch_impl(ctx, dtype, &nd, 1, EV, n, wgt, pick(ctx, stream), tips, tipvec);
 }
 
 int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
@@ -363,13 +365,14 @@ int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops,
                   int64_t n, const int32_t *wgt, uint8_t *const *scalers, int64_t *scaler_sums,
                   void *stream) {
   return plfx_traverse_tips(ctx, dtype, states, ops, nops, clv, nullptr, nslots, pmats, npmats, EV,
-                            n, wgt, scalers, scaler_sums, stream);
+                            n, wgt, scalers, scaler_sums, nullptr, stream);
 }
 
 int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
                        void *const *clv, const uint8_t *const *tips, int nslots, const void *pmats,
                        int npmats, const void *EV, int64_t n, const int32_t *wgt,
-                       uint8_t *const *scalers, int64_t *scaler_sums, void *stream) {
+                       uint8_t *const *scalers, int64_t *scaler_sums, const void *tipvec,
+                       void *stream) {
   if (!ctx) return PLFX_ERR_INVALID;
   if (states != 4) return fail(ctx, PLFX_ERR_UNSUPPORTED, "traverse: states=%d not built", states);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
@@ -420,7 +423,8 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op 
     }
     for (int k = 0; k < 3; k++) {
       if (batch[k].empty()) continue;
-      int rc = batch_impl(ctx, dtype, batch[k].data(), (int)batch[k].size(), EV, n, wgt, s, k);
+      int rc = batch_impl(ctx, dtype, batch[k].data(), (int)batch[k].size(), EV, n, wgt, s, k,
+                          tipvec);
       if (rc != PLFX_OK) return rc;
     }
   }

@@ -50,7 +50,7 @@ EXPORTS = (
     "plfx_plf_batch_dev", "plfx_traverse", "plfx_root_lnl", "plfx_plf_dev_gen",
     "plfx_plf_tips_dev", "plfx_traverse_tips",
     "plfx_model_eigen", "plfx_gamma_rates", "plfx_model_ev", "plfx_model_root_weights",
-    "plfx_pmatrix",
+    "plfx_pmatrix", "plfx_model_tip_vectors",
 )
 PMAT_STATE, PMAT_EIGEN = 0, 1
 EXACT, FMA = 0, 1
@@ -132,9 +132,12 @@ def load():
     L.plfx_model_ev.argtypes = [i32, i32, dp, dp]
     L.plfx_model_root_weights.argtypes = [i32, i32, dp, dp, dp]
     L.plfx_pmatrix.argtypes = [vp, i32, i32, i32, vp, vp, i32, vp, i64, vp, vp]
-    L.plfx_plf_tips_dev.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
+    L.plfx_model_tip_vectors.argtypes = [i32, i32, dp, dp]
+    L.plfx_plf_tips_dev.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp,
+                                    vp]
     L.plfx_traverse_tips.argtypes = [vp, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp),
-                                     C.POINTER(vp), i32, vp, i32, vp, i64, vp, C.POINTER(vp), vp, vp]
+                                     C.POINTER(vp), i32, vp, i32, vp, i64, vp, C.POINTER(vp), vp, vp,
+                                     vp]
     _lib = L
     return L
 
@@ -345,12 +348,13 @@ class Context:
                                                C.c_void_p(ptr(wgt)), _stream_handle(stream)))
 
     def traverse(self, ops, clv, pmats, EV, n, wgt=None, scalers=None, scaler_sums=None,
-                 stream=None, tips=None):
+                 stream=None, tips=None, tipvec=None):
         """Run a post-order traversal descriptor.  ops: (nops, 4) int array of
         [parent, child1, child2, pmat]; clv: list of torch CLV tensors (slots;
         None where the slot is a tip); pmats: tensor of 2*npmat matrices (64
         values each for DNA); tips: optional list (per slot) of uint8 state-code
-        tensors or None (plfx.h section 8)."""
+        tensors or None (plfx.h section 8); tipvec: optional device table of
+        16 x 4 tip vectors (dtype of the CLVs)."""
         import torch
 
         ops = np.ascontiguousarray(ops, dtype=np.int32).reshape(-1, 4)
@@ -384,10 +388,18 @@ class Context:
             C.c_void_p(pmats.data_ptr()), pmats.numel() // 128, C.c_void_p(EV.data_ptr()), int(n),
             C.c_void_p(None if wgt is None else wgt.data_ptr()), sc,
             C.c_void_p(None if scaler_sums is None else scaler_sums.data_ptr()),
-            _stream_handle(stream)))
+            self._tipvec(tipvec, dt), _stream_handle(stream)))
+
+    @staticmethod
+    def _tipvec(tipvec, dt):
+        if tipvec is None:
+            return C.c_void_p(None)
+        if tipvec.dtype != dt or tipvec.numel() < 64 or not tipvec.is_contiguous():
+            raise PlfxError(ERR_INVALID, "tipvec must be a contiguous device table of 16 x 4 values")
+        return C.c_void_p(tipvec.data_ptr())
 
     def plf_tips_dev(self, x3, EV, n, left, right, x1=None, x2=None, tip1=None, tip2=None,
-                     wgt=None, scaler=None, scaler_sum=None, stream=None):
+                     wgt=None, scaler=None, scaler_sum=None, tipvec=None, stream=None):
         """One DNA inner node with tip children (plfx.h section 8): for each
         child pass exactly one of the dense CLV (x1/x2) or the uint8 state
         codes (tip1/tip2)."""
@@ -404,7 +416,7 @@ class Context:
         self._check(self._L.plfx_plf_tips_dev(
             self.h, F32 if dt == torch.float32 else F64, p(tip1), p(x1), p(tip2), p(x2), p(x3),
             p(EV), int(n), p(left), p(right), p(wgt), p(scaler), p(scaler_sum),
-            _stream_handle(stream)))
+            self._tipvec(tipvec, dt), _stream_handle(stream)))
 
     # -- (9) P matrices from branch lengths --------------------------------
     def pmatrix(self, eigen, rates, blen, out, states=4, convention=PMAT_STATE, stream=None):
@@ -519,6 +531,18 @@ def model_root_weights(eigen, freqs, convention=PMAT_STATE):
     e, ep = _dbl(eigen)
     out, op = _dbl(np.zeros(f.size))
     _host_check(L.plfx_model_root_weights(f.size, convention, ep, fp, op), "model_root_weights")
+    return out
+
+
+def model_tip_vectors(eigen=None, convention=PMAT_STATE, states=4):
+    """16 x S tip vectors for the tip paths (plfx.h (9))."""
+    L = load()
+    out, op = _dbl(np.zeros(16 * states))
+    if eigen is None:
+        ep = C.cast(None, C.POINTER(C.c_double))
+    else:
+        e, ep = _dbl(eigen)
+    _host_check(L.plfx_model_tip_vectors(states, convention, ep, op), "model_tip_vectors")
     return out
 
 

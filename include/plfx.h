@@ -189,12 +189,17 @@ int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops,
  * Results are bit-identical to plf() on the expanded dense CLV
  * x[i][c][s] = (code_i >> s) & 1 for every category c.  DNA (4 states) only. */
 
-/* One node: exactly one of (tip1, x1) and one of (tip2, x2) is non-NULL;
+/* tipvec: NULL, or a device table of 16 x 4 values of dtype -- the dense
+ * per-category CLV entry of each code, tipvec[code*4 + s] (the default is the
+ * 0/1 state indicator; plfx_model_tip_vectors gives the eigen-convention
+ * table).  Results are bit-identical to plf() on x[i][c][s] = tipvec[code_i][s].
+ *
+ * One node: exactly one of (tip1, x1) and one of (tip2, x2) is non-NULL;
  * the other arguments are those of plfx_plf_dev_f32/f64 (device pointers). */
 int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void *x1,
                       const uint8_t *tip2, const void *x2, void *x3, const void *EV, int64_t n,
                       const void *left, const void *right, const int32_t *wgt, uint8_t *scaler,
-                      int64_t *scaler_sum, void *stream);
+                      int64_t *scaler_sum, const void *tipvec, void *stream);
 
 /* plfx_traverse with tip slots: tips is a host array of nslots device pointers
  * (or NULL = no tips); a slot with tips[s] != NULL is a tip (clv[s] is not
@@ -203,7 +208,8 @@ int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void 
 int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
                        void *const *clv, const uint8_t *const *tips, int nslots, const void *pmats,
                        int npmats, const void *EV, int64_t n, const int32_t *wgt,
-                       uint8_t *const *scalers, int64_t *scaler_sums, void *stream);
+                       uint8_t *const *scalers, int64_t *scaler_sums, const void *tipvec,
+                       void *stream);
 
 /* ---- (7) root log-likelihood (extension) -- */
 /* lnL = sum_i wgt_i * log( sum_c catw[c] * sum_s freq[s] * x[i][c][s] )
@@ -274,6 +280,11 @@ int plfx_model_ev(int states, int convention, const double *eigen, double *EV);
  * EIGEN -> w[k] = sum_s pi_s V[s][k] (the root CLV is in eigen coordinates). */
 int plfx_model_root_weights(int states, int convention, const double *eigen, const double *freqs,
                             double *w);
+
+/* Tip vectors (host, 16 x S doubles; DNA: S = 4) for plfx_plf_tips_dev /
+ * plfx_traverse_tips: STATE -> tv[code][s] = bit s of code; EIGEN -> tv[code]
+ * = Vinv . bits(code) (tips in eigen coordinates). */
+int plfx_model_tip_vectors(int states, int convention, const double *eigen, double *tv);
 
 /* Device: pmats[b][c][k][l] (nbranch * ncat * S * S values of dtype) from the
  * eigensystem (device, S+2S^2 doubles, as plfx_model_eigen), category rates

@@ -231,14 +231,18 @@ def balanced_tree_ops(ntips):
     return np.array(ops, np.int32)
 
 
-def expand_tips(codes, dtype=np.float64, Ccat=4):
+def expand_tips(codes, dtype=np.float64, Ccat=4, tipvec=None):
     """Dense CLV of a tip stored as DNA state codes (bit s = state s possible,
     upper nibble ignored; the RAxML/PLL encoding): x[i][c][s] = (code_i >> s) & 1
-    for every category c.  This is the definition the GPU's tip path is
-    checked against (plfx.h section 8): plf() on the expanded CLV."""
+    for every category c, or tipvec[code_i & 15][s] when a 16 x 4 tip-vector
+    table is given.  This is the definition the GPU's tip path is checked
+    against (plfx.h section 8): plf() on the expanded CLV."""
     codes = np.asarray(codes, np.uint8)
-    bits = ((codes[:, None] >> np.arange(4, dtype=np.uint8)) & 1).astype(dtype)
-    return np.ascontiguousarray(np.repeat(bits[:, None, :], Ccat, axis=1).reshape(-1))
+    if tipvec is None:
+        rows = ((codes[:, None] >> np.arange(4, dtype=np.uint8)) & 1).astype(dtype)
+    else:
+        rows = np.asarray(tipvec, dtype).reshape(16, 4)[codes & 15]
+    return np.ascontiguousarray(np.repeat(rows[:, None, :], Ccat, axis=1).reshape(-1))
 
 
 def random_tip_codes(rng, n, ambiguous=0.1):

@@ -82,12 +82,14 @@ def felsenstein_lnl(Q, pi, rates, catw, blen, ops, tipx, ntips, wgt):
     return float(np.sum(wgt * (np.log(site) + logs)))
 
 
-@pytest.mark.parametrize("conv", [plfx.PMAT_STATE, plfx.PMAT_EIGEN])
-def test_gtr_gamma_pipeline_lnl(ctx, oracle, conv):
+@pytest.mark.parametrize("conv,coded", [(plfx.PMAT_STATE, True), (plfx.PMAT_EIGEN, False),
+                                        (plfx.PMAT_EIGEN, True)])
+def test_gtr_gamma_pipeline_lnl(ctx, oracle, conv, coded):
     """GTR+G4 on a 16-taxon balanced tree, 5000 sites: device P matrices ->
     traverse -> root lnL equals the numpy pruning within 1e-10 relative.
     STATE: tips as uint8 state codes, EV = I.  EIGEN: tips as dense eigen-
-    coordinate CLVs Vinv.bits, EV = Vinv^T, root weights pi.V."""
+    coordinate CLVs Vinv.bits, EV = Vinv^T, root weights pi.V.  EIGEN_CODED:
+    the eigen convention with coded tips and the eigen tip-vector table."""
     import torch
 
     rng = np.random.default_rng(31 + conv)
@@ -113,14 +115,17 @@ def test_gtr_gamma_pipeline_lnl(ctx, oracle, conv):
     EV = dev(plfx.model_ev(e, 4, conv))
     nslots = ntips + nops
     clv = [torch.empty(16 * n, dtype=torch.float64, device="cuda") for _ in range(nops)]
-    if conv == plfx.PMAT_STATE:
+    tipvec = None
+    if coded:
         tips = [dev(c) for c in codes] + [None] * nops
         clv = [None] * ntips + clv
+        if conv == plfx.PMAT_EIGEN:
+            tipvec = dev(plfx.model_tip_vectors(e, conv))
     else:
         tips = None
         clv = [dev(np.einsum("ls,ncs->ncl", Vi, x).reshape(-1)) for x in tipx] + clv
     sums = torch.zeros(nops, dtype=torch.int64, device="cuda")
-    ctx.traverse(ops, clv, pm, EV, n, dev(wgt), None, sums, tips=tips)
+    ctx.traverse(ops, clv, pm, EV, n, dev(wgt), None, sums, tips=tips, tipvec=tipvec)
     w = dev(plfx.model_root_weights(e, freqs, conv))
     out = torch.zeros(1, dtype=torch.float64, device="cuda")
     ctx.root_lnl(clv[nslots - 1], n, out, catw=dev(catw), freq=w, wgt=dev(wgt), scaler_sums=sums)

@@ -133,6 +133,44 @@ def test_plf_dev_full_size_1M(ctx, oracle, dtype):
         rel_ok(got, e3)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_plf_dev_beyond_2g_elements(ctx, oracle, dtype):
+    """Maximum sizes: n = 2^27 + 5 sites puts CLV element indices past 2^31
+    (the reference's `int` element index would overflow at n >= 2^27); the
+    kernels index in 64 bits.  Windows at the start, across 2^27 and at the
+    ragged end are checked bit-exactly against the oracle; the weighted scaler
+    sum equals the sum over the per-site scaler bytes (size-independent)."""
+    import torch
+
+    n = (1 << 27) + 5
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    g = torch.Generator(device="cuda")
+    g.manual_seed(31)
+    x1 = torch.rand(16 * n, dtype=tdt, device="cuda", generator=g)
+    x1.view(n, 16)[0::4] *= 1e-12
+    x2 = torch.rand(16 * n, dtype=tdt, device="cuda", generator=g)
+    x3 = torch.empty_like(x1)
+    EV = torch.rand(16, dtype=tdt, device="cuda", generator=g)
+    L = torch.rand(64, dtype=tdt, device="cuda", generator=g)
+    R = torch.rand(64, dtype=tdt, device="cuda", generator=g)
+    wgt = torch.randint(0, 3, (n,), dtype=torch.int32, device="cuda", generator=g)
+    sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.plf_dev(x1, x2, x3, EV, L, R, wgt, sc, s)
+    torch.cuda.synchronize()
+    assert int(s.item()) == int((sc.to(torch.int64) * wgt.to(torch.int64)).sum().item())
+    assert int(sc.sum().item()) >= n // 4
+    h = lambda t: t.cpu().numpy()  # noqa: E731
+    for lo in (0, (1 << 27) - 1000, n - 2000):
+        m = min(2000, n - lo)
+        sl = slice(16 * lo, 16 * (lo + m))
+        e3, esc, _ = oracle.plf(h(x1[sl]), h(x2[sl]), h(EV), h(L), h(R), h(wgt[lo:lo + m]))
+        assert np.array_equal(bits(h(x3[sl])), bits(e3)), lo
+        assert np.array_equal(h(sc[lo:lo + m]), esc), lo
+    del x1, x2, x3
+    torch.cuda.empty_cache()
+
+
 def test_plf_dev_repeated_calls_and_optional_outputs(ctx, oracle):
     """The in-kernel ticket reduction resets itself: back-to-back launches with
     different weights each report their own sum; outputs are optional."""

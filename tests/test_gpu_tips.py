@@ -62,6 +62,36 @@ def test_single_node_tips(ctx, oracle, dtype, kind, n):
         assert esc.sum() > 0
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("kind", ["tip_tip", "tip_inner"])
+def test_tip_vector_table(ctx, oracle, dtype, kind):
+    """A caller-supplied 16 x 4 tip-vector table (e.g. eigen-coordinate tips,
+    plfx_model_tip_vectors): bit-exact vs plf() on x[i][c][s] = tv[code_i][s]."""
+    import torch
+
+    n = 5003
+    rng = np.random.default_rng(77)
+    tv = (rng.random(64) * 2 - 0.5).astype(dtype)
+    c1 = oracle.random_tip_codes(rng, n, 0.5)
+    c2 = oracle.random_tip_codes(rng, n, 0.5)
+    x1 = oracle.expand_tips(c1, dtype, tipvec=tv)
+    x2 = oracle.expand_tips(c2, dtype, tipvec=tv) if kind == "tip_tip" else rng.random(16 * n).astype(dtype)
+    L, R, EV = (rng.random(64).astype(dtype), rng.random(64).astype(dtype),
+                rng.random(16).astype(dtype))
+    e3, esc, einc = oracle.plf(x1, x2, EV, L, R)
+    x3 = torch.empty(16 * n, dtype=torch.float64 if dtype == np.float64 else torch.float32, device="cuda")
+    ss = torch.zeros(1, dtype=torch.int64, device="cuda")
+    args = dict(tip1=dev(c1), scaler_sum=ss, tipvec=dev(tv))
+    if kind == "tip_tip":
+        args["tip2"] = dev(c2)
+    else:
+        args["x2"] = dev(x2)
+    ctx.plf_tips_dev(x3, dev(EV), n, dev(L), dev(R), **args)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(x3.cpu().numpy()), bits(e3))
+    assert int(ss.item()) == einc
+
+
 def test_tip_tip_all_codes_scale(ctx, oracle):
     """Code 0 (no state possible) gives an all-zero site: scaled (0 < 2^-32),
     stays 0; a weight per site reaches the sum."""

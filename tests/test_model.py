@@ -104,3 +104,17 @@ def test_model_rejects_bad_args():
         plfx.gamma_rates(0.0, 4)
     with pytest.raises(plfx.PlfxError):
         plfx.gamma_rates(1.0, 0)
+
+
+def test_tip_vectors():
+    tv = plfx.model_tip_vectors().reshape(16, 4)
+    for code in range(16):
+        assert np.array_equal(tv[code], [(code >> s) & 1 for s in range(4)])
+    rng = np.random.default_rng(4)
+    e = plfx.model_eigen(rng.random(6) + 0.1, rng.random(4) + 0.1)
+    Vi = e[20:].reshape(4, 4)
+    tve = plfx.model_tip_vectors(e, plfx.PMAT_EIGEN).reshape(16, 4)
+    for code in range(16):
+        assert np.allclose(tve[code], Vi @ tv[code], rtol=0, atol=1e-15)
+    with pytest.raises(plfx.PlfxError):
+        plfx.model_tip_vectors(None, plfx.PMAT_EIGEN)
