@@ -81,21 +81,13 @@ __device__ __forceinline__ long long decode_count(long long word) {
   return (word + (kTick >> 1)) >> 41;  // floor((word + kTick/2) / kTick)
 }
 
-__device__ inline void block_ticket_sum(long long v, unsigned long long *wsu, int64_t *out) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  __shared__ long long part[kWavesPerBlock];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x != 0) return;
+// The two round trips for one block total `tot` (one thread).
+__device__ inline void ticket_publish(long long tot, unsigned long long *wsu, int64_t *out) {
   long long *ws = reinterpret_cast<long long *>(wsu);
   const long long G = gridDim.x;
   const long long slot = blockIdx.x % kSlots;
   const long long nslots = G < kSlots ? G : kSlots;
   const long long arrivals = (G - slot + kSlots - 1) / kSlots;
-  long long tot = 0;
-#pragma unroll
-  for (int i = 0; i < kWavesPerBlock; i++) tot += part[i];
   const long long old = __hip_atomic_fetch_add(ws + slot * 16, kTick + tot, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
   if (decode_count(old) != arrivals - 1) return;
@@ -106,6 +98,45 @@ __device__ inline void block_ticket_sum(long long v, unsigned long long *wsu, in
   if (decode_count(told) != nslots - 1) return;
   if (out) *out = (int64_t)(told + kTick + slot_sum - nslots * kTick);
   __hip_atomic_store(ws + kSlots * 16, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline void block_ticket_sum(long long v, unsigned long long *wsu, int64_t *out) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __shared__ long long part[kWavesPerBlock];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  long long tot = 0;
+#pragma unroll
+  for (int i = 0; i < kWavesPerBlock; i++) tot += part[i];
+  ticket_publish(tot, wsu, out);
+}
+
+// Three independent sums (consecutive kWsWords regions of ws), published by
+// threads 0..2 in parallel.
+__device__ inline void block_ticket_sum3(long long v0, long long v1, long long v2,
+                                         unsigned long long *wsu, int64_t *o0, int64_t *o1,
+                                         int64_t *o2) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    v0 += __shfl_xor(v0, off);
+    v1 += __shfl_xor(v1, off);
+    v2 += __shfl_xor(v2, off);
+  }
+  __shared__ long long part3[3][kWavesPerBlock];
+  if ((threadIdx.x & 63) == 0) {
+    part3[0][threadIdx.x >> 6] = v0;
+    part3[1][threadIdx.x >> 6] = v1;
+    part3[2][threadIdx.x >> 6] = v2;
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= 3) return;
+  long long tot = 0;
+#pragma unroll
+  for (int i = 0; i < kWavesPerBlock; i++) tot += part3[t][i];
+  ticket_publish(tot, wsu + (size_t)t * kWsWords, t == 0 ? o0 : (t == 1 ? o1 : o2));
 }
 
 // Swap 64-bit values between adjacent lanes with DPP quad_perm patterns:
@@ -550,6 +581,206 @@ scaler_sum_kernel(const uint8_t *__restrict__ scaler, const int32_t *__restrict_
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n; j += stride)
     acc += (long long)scaler[j] * (wgt ? (long long)wgt[j] : 1ll);
   block_ticket_sum(acc, ws, out);
+}
+
+// ---------------------------------------------------------------------------
+// Fused level pair ("triple"): parent P of two inner nodes A, B that are
+// computed in the same pass -- A from (a1, a2), B from (b1, b2), then P from
+// (A, B) -- so the two intermediate CLVs are written once and never read back
+// (per site and f64: 4 child reads + 3 writes = 896 B instead of 3 x 384).
+// The lane-pair layout of a node's output (states 2h, 2h+1 of category c of
+// site g) is exactly the layout the next node's body reads, so A and B feed P
+// from registers.  Every node keeps plf()'s arithmetic, scale test, scaler
+// byte and weighted scaler sum: results are bit-identical to three separate
+// updates.  kTips: 0 = a1, a2, b1, b2 dense; 1 = a1 and b1 are tips (a2, b2
+// dense); 2 = all four are tips.
+struct TripleDesc {
+  const void *a1, *a2, *b1, *b2;
+  void *xa, *xb, *xp;
+  const double *la, *ra, *lb, *rb, *lp, *rp;
+  uint8_t *sa, *sb, *sp;
+  int64_t *ssa, *ssb, *ssp;
+};
+constexpr int kMaxTriples = 10;
+struct TripleBatch {
+  TripleDesc d[kMaxTriples];
+};
+
+struct PairMats {
+  double PL[2][4], PR[2][4];
+};
+
+__device__ __forceinline__ void pair_mats(const double *__restrict__ left,
+                                          const double *__restrict__ right, int c, int h,
+                                          PairMats &M) {
+#pragma unroll
+  for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      M.PL[kk][l] = left[c * 16 + (2 * h + kk) * 4 + l];
+      M.PR[kk][l] = right[c * 16 + (2 * h + kk) * 4 + l];
+    }
+}
+
+// One node on one 8-site block in the lane-pair layout (dna_pair_body's body):
+// returns the (possibly rescaled) output pair and the site's scale flag.
+template <bool TL, bool TR>
+__device__ __forceinline__ f64x2 pair_node(const f64x2 a, const f64x2 b, const double *rowL,
+                                           const double *rowR, const PairMats &M,
+                                           const double (&E)[4][2], bool valid, int sh,
+                                           double m, bool &sc) {
+  double u1[2], u2[2];
+  if constexpr (TL) {
+    const f64x2 r = *reinterpret_cast<const f64x2 *>(rowL);
+    u1[0] = r.x; u1[1] = r.y;
+  } else {
+    const double a0 = dpp_f64<kQuadEven>(a.x), a1 = dpp_f64<kQuadEven>(a.y);
+    const double a2 = dpp_f64<kQuadOdd>(a.x), a3 = dpp_f64<kQuadOdd>(a.y);
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+      double v = 0.0;
+      v += a0 * M.PL[kk][0]; v += a1 * M.PL[kk][1]; v += a2 * M.PL[kk][2]; v += a3 * M.PL[kk][3];
+      u1[kk] = v;
+    }
+  }
+  if constexpr (TR) {
+    const f64x2 r = *reinterpret_cast<const f64x2 *>(rowR);
+    u2[0] = r.x; u2[1] = r.y;
+  } else {
+    const double b0 = dpp_f64<kQuadEven>(b.x), b1 = dpp_f64<kQuadEven>(b.y);
+    const double b2 = dpp_f64<kQuadOdd>(b.x), b3 = dpp_f64<kQuadOdd>(b.y);
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+      double v = 0.0;
+      v += b0 * M.PR[kk][0]; v += b1 * M.PR[kk][1]; v += b2 * M.PR[kk][2]; v += b3 * M.PR[kk][3];
+      u2[kk] = v;
+    }
+  }
+  double pm[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; kk++) pm[kk] = u1[kk] * u2[kk];
+  const double p0 = dpp_f64<kQuadEven>(pm[0]), p1 = dpp_f64<kQuadEven>(pm[1]);
+  const double p2 = dpp_f64<kQuadOdd>(pm[0]), p3 = dpp_f64<kQuadOdd>(pm[1]);
+  double o[2];
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    double x = 0.0;
+    x += p0 * E[0][t]; x += p1 * E[1][t]; x += p2 * E[2][t]; x += p3 * E[3][t];
+    o[t] = x;
+  }
+  const bool small = valid && (__builtin_fabs(o[0]) < m) && (__builtin_fabs(o[1]) < m);
+  const unsigned long long mask = __ballot(small);
+  sc = ((mask >> sh) & 0xFFull) == 0xFFull;
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    const double s = o[t] * Num<double>::two32();
+    o[t] = sc ? s : o[t];
+  }
+  return f64x2{o[0], o[1]};
+}
+
+template <bool kSum, int kMinWaves, bool NTL, int kTips, int U = 1>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_f64_triple_kernel(const TripleBatch tb, const double *__restrict__ EV,
+                          const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
+                          const double *__restrict__ tipvec) {
+  constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
+  const TripleDesc &d = tb.d[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 1, c = (lane >> 1) & 3, g = lane >> 3, sh = lane & 56;
+  // tip tables: [0] A's left, [1] B's left, [2] A's right, [3] B's right
+  __shared__ double tab[T2 ? 4 : (T1 ? 2 : 1)][T1 ? 256 : 1];
+  if constexpr (T1) {
+    build_tip_table<double>(d.la, tipvec, tab[0]);
+    build_tip_table<double>(d.lb, tipvec, tab[1]);
+  }
+  if constexpr (T2) {
+    build_tip_table<double>(d.ra, tipvec, tab[2]);
+    build_tip_table<double>(d.rb, tipvec, tab[3]);
+  }
+  if constexpr (T1) __syncthreads();
+  const int trow = c * 64 + 2 * h;
+  PairMats MA, MB, MP;
+  pair_mats(d.la, d.ra, c, h, MA);
+  pair_mats(d.lb, d.rb, c, h, MB);
+  pair_mats(d.lp, d.rp, c, h, MP);
+  double E[4][2];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int t = 0; t < 2; t++) E[k][t] = EV[4 * k + 2 * h + t];
+  const double m = Num<double>::minlik();
+  const uint8_t *ta1 = (const uint8_t *)d.a1, *ta2 = (const uint8_t *)d.a2;
+  const uint8_t *tb1 = (const uint8_t *)d.b1, *tb2 = (const uint8_t *)d.b2;
+  const double *xa1 = (const double *)d.a1, *xa2 = (const double *)d.a2;
+  const double *xb1 = (const double *)d.b1, *xb2 = (const double *)d.b2;
+  double *xa = (double *)d.xa, *xb = (double *)d.xb, *xp = (double *)d.xp;
+
+  long long accA = 0, accB = 0, accP = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  for (int64_t base = wave * 16 * U; base < n; base += stride) {
+    f64x2 va1[2 * U], va2[2 * U], vb1[2 * U], vb2[2 * U];
+    int ka1[2 * U], ka2[2 * U], kb1[2 * U], kb2[2 * U], w[2 * U];
+    bool valid[2 * U];
+#pragma unroll
+    for (int j = 0; j < 2 * U; j++) {  // all loads of the 16*U sites first
+      const int64_t site0 = base + j * 8;
+      valid[j] = site0 + g < n;
+      va1[j] = va2[j] = vb1[j] = vb2[j] = f64x2{0.0, 0.0};
+      ka1[j] = ka2[j] = kb1[j] = kb2[j] = 0;
+      w[j] = 0;
+      if (valid[j]) {
+        const int64_t rec = site0 * 8 + lane;  // f64x2 index of this lane's pair (8 per site)
+        if constexpr (T1) {
+          ka1[j] = ta1[site0 + g] & 15;
+          kb1[j] = tb1[site0 + g] & 15;
+        } else {
+          va1[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xa1) + rec);
+          vb1[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xb1) + rec);
+        }
+        if constexpr (T2) {
+          ka2[j] = ta2[site0 + g] & 15;
+          kb2[j] = tb2[site0 + g] & 15;
+        } else {
+          va2[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xa2) + rec);
+          vb2[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xb2) + rec);
+        }
+        if (kSum) w[j] = wgt ? wgt[site0 + g] : 1;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2 * U; j++) {
+      const int64_t site0 = base + j * 8;
+      const int64_t rec = site0 * 8 + lane;
+      bool sA, sB, sP;
+      const f64x2 oA = pair_node<T1, T2>(va1[j], va2[j], tab[0] + trow + 4 * ka1[j],
+                                         tab[T2 ? 2 : 0] + trow + 4 * ka2[j], MA, E, valid[j], sh,
+                                         m, sA);
+      const f64x2 oB = pair_node<T1, T2>(vb1[j], vb2[j], tab[T1 ? 1 : 0] + trow + 4 * kb1[j],
+                                         tab[T2 ? 3 : 0] + trow + 4 * kb2[j], MB, E, valid[j], sh,
+                                         m, sB);
+      const f64x2 oP = pair_node<false, false>(oA, oB, nullptr, nullptr, MP, E, valid[j], sh, m, sP);
+      if (valid[j]) {
+        __builtin_nontemporal_store(oA, reinterpret_cast<f64x2 *>(xa) + rec);
+        __builtin_nontemporal_store(oB, reinterpret_cast<f64x2 *>(xb) + rec);
+        __builtin_nontemporal_store(oP, reinterpret_cast<f64x2 *>(xp) + rec);
+        if ((lane & 7) == 0) {
+          if (d.sa) d.sa[site0 + g] = (uint8_t)sA;
+          if (d.sb) d.sb[site0 + g] = (uint8_t)sB;
+          if (d.sp) d.sp[site0 + g] = (uint8_t)sP;
+          if (kSum) {
+            if (sA) accA += w[j];
+            if (sB) accB += w[j];
+            if (sP) accP += w[j];
+          }
+        }
+      }
+    }
+  }
+  if constexpr (kSum)
+    block_ticket_sum3(accA, accB, accP, ws + (size_t)blockIdx.y * 3 * kWsWords, d.ssa, d.ssb,
+                      d.ssp);
 }
 
 }  // namespace dev

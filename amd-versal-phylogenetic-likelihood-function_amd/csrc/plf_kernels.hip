@@ -15,6 +15,7 @@
 // blocks over the batch's nodes (blockIdx.y = node).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "plf_dna.hpp"
@@ -31,6 +32,8 @@ using dev::kWavesPerBlock;
 static_assert(kWsWords == dev::kWsWords, "workspace size mismatch");
 static_assert(kMaxBatch == dev::kMaxBatch, "batch size mismatch");
 static_assert(sizeof(NodeDescH) == sizeof(dev::NodeDesc), "node descriptor mismatch");
+static_assert(sizeof(TripleDescH) == sizeof(dev::TripleDesc), "triple descriptor mismatch");
+static_assert(kMaxTriples == dev::kMaxTriples && 3 * kMaxTriples <= kMaxBatch, "triple batch size");
 
 // Tuned on MI355X (tools/tune_plf.hip, profiles/r01_tune.log):
 // f64 lane-pair kernel, 2 x 16-site steps per trip, non-temporal CLV loads
@@ -40,6 +43,7 @@ constexpr int kGridMul64 = 1, kGridMul32 = 1;
 constexpr bool kNt = true;   // f32: NT CLV loads (74.8% vs 70.2% of HBM peak, r01_tune_f32.log)
 constexpr bool kNtl64 = true;
 constexpr int kMinWaves = 1;
+constexpr int kTripleU = 1;  // fused level pairs: 16 sites per trip (tools/tune_triple.hip)
 
 // Co-resident 256-thread blocks of `kernel` on the current device (cached per
 // kernel instantiation by the caller).
@@ -62,7 +66,10 @@ int64_t grid_x(const void *kernel, int &cache, int grid_mul, int64_t n, int site
                int count, int max_blocks) {
   int64_t blocks = (n + sites_per_block - 1) / sites_per_block;
   const int64_t resident = (int64_t)grid_mul * resident_blocks(kernel, cache);
-  const int64_t cap = max_blocks > 0 ? max_blocks : (resident + count - 1) / count;
+  // floor: count x cap blocks must fit in one wave of resident blocks (a ceil
+  // would leave a few blocks for a second, nearly empty wave: +30% on a
+  // 10-node batch)
+  const int64_t cap = max_blocks > 0 ? max_blocks : std::max<int64_t>(1, resident / count);
   if (blocks > cap) blocks = cap;
   return blocks < 1 ? 1 : blocks;
 }
@@ -172,7 +179,42 @@ hipError_t launch_prot_exact64_t(const DnaArgs &a, int max_blocks, hipStream_t s
   return hipGetLastError();
 }
 
+template <bool kSum, int kTips>
+hipError_t launch_triples_t(const dev::TripleBatch &b, int count, const double *EV,
+                            const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                            hipStream_t s, const double *tipvec) {
+  static int cache = 0;
+  constexpr int U = kTripleU;
+  auto kernel = &dev::plf_dna_f64_triple_kernel<kSum, 1, kNtl64, kTips, U>;
+  const int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 16 * U, count,
+                            max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt,
+                     n, ws, tipvec);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_plf_dna_triples(const TripleDescH *t, int count, const double *EV,
+                                  const int32_t *wgt, int64_t n, unsigned long long *ws,
+                                  int max_blocks, hipStream_t s, int tips, const double *tipvec) {
+  if (count < 1 || count > kMaxTriples || tips < 0 || tips > 2) return hipErrorInvalidValue;
+  dev::TripleBatch b{};
+  bool any_sum = false;
+  for (int i = 0; i < count; i++) {
+    static_assert(sizeof(b.d[0]) == sizeof(t[0]), "layout");
+    __builtin_memcpy(&b.d[i], &t[i], sizeof(t[i]));
+    any_sum |= t[i].ssa || t[i].ssb || t[i].ssp;
+  }
+  switch ((any_sum ? 3 : 0) + tips) {
+    case 0: return launch_triples_t<false, 0>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 1: return launch_triples_t<false, 1>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 2: return launch_triples_t<false, 2>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 3: return launch_triples_t<true, 0>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 4: return launch_triples_t<true, 1>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    default: return launch_triples_t<true, 2>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+  }
+}
 
 hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s) {
   if (dtype == 1) {

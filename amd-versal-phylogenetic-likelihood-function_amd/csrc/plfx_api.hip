@@ -23,6 +23,7 @@ struct plfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
+  bool fuse = true;                 // traverse: fused level pairs (PLFX_FUSE=0 disables)
   unsigned long long *ws = nullptr; // ticket reduction words (kMaxBatch x kWsWords u64), zero at rest
   double *lnl_partials = nullptr;   // kLnlMaxGrid doubles
   unsigned long long *lnl_ticket = nullptr;
@@ -150,6 +151,18 @@ int plf_host(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int n,
   return PLFX_OK;
 }
 
+// One node of a kind (tips = number of tip children, tip child first).
+int check_node(plfx_ctx *ctx, const plfx_node &d, int tips, int64_t n, int i) {
+  if (n <= 0) return PLFX_OK;
+  if (!d.x1 || !d.x2 || !d.x3 || !d.left || !d.right)
+    return fail(ctx, PLFX_ERR_INVALID, "node %d: null CLV/tip/matrix pointer", i);
+  if ((tips < 1 && !aligned16(d.x1)) || (tips < 2 && !aligned16(d.x2)) || !aligned16(d.x3))
+    return fail(ctx, PLFX_ERR_INVALID, "node %d: CLV pointers must be 16-byte aligned", i);
+  if (d.x3 == d.x1 || d.x3 == d.x2)
+    return fail(ctx, PLFX_ERR_INVALID, "node %d: x3 may not alias a child", i);
+  return PLFX_OK;
+}
+
 // Nodes of one kind (tips = number of tip children, tip child first) in
 // launches of kMaxBatch.  A tip child is a uint8 code array (no alignment rule).
 int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, const void *EV,
@@ -159,14 +172,8 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
     return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
   for (int i = 0; i < count; i++) {
     const plfx_node &d = nodes[i];
-    if (n > 0) {
-      if (!d.x1 || !d.x2 || !d.x3 || !d.left || !d.right)
-        return fail(ctx, PLFX_ERR_INVALID, "node %d: null CLV/tip/matrix pointer", i);
-      if ((tips < 1 && !aligned16(d.x1)) || (tips < 2 && !aligned16(d.x2)) || !aligned16(d.x3))
-        return fail(ctx, PLFX_ERR_INVALID, "node %d: CLV pointers must be 16-byte aligned", i);
-      if (d.x3 == d.x1 || d.x3 == d.x2)
-        return fail(ctx, PLFX_ERR_INVALID, "node %d: x3 may not alias a child", i);
-    }
+    int rc = check_node(ctx, d, tips, n, i);
+    if (rc != PLFX_OK) return rc;
     if (n == 0 && d.scaler_sum) PLFX_HIP(ctx, hipMemsetAsync(d.scaler_sum, 0, sizeof(int64_t), s));
   }
   if (n == 0) return PLFX_OK;
@@ -209,6 +216,7 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
     int v = std::atoi(env);
     if (v > 0) ctx->max_blocks = v;
   }
+  if (const char *env = std::getenv("PLFX_FUSE")) ctx->fuse = std::atoi(env) != 0;
   const size_t ws_bytes = (size_t)plfx::kMaxBatch * plfx::kWsWords * sizeof(unsigned long long);
   if (hipMalloc(reinterpret_cast<void **>(&ctx->ws), ws_bytes) != hipSuccess ||
       hipMemsetAsync(ctx->ws, 0, ws_bytes, ctx->stream) != hipSuccess ||
@@ -381,8 +389,9 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op 
   const size_t es = dtype == PLFX_F32 ? 4 : 8;
   const size_t mat = (size_t)states * states * 4;  // C*S*S values per matrix
   auto is_tip = [&](int sl) { return tips && tips[sl]; };
-  // dependency levels: RAW on children, WAR/WAW on the parent slot
-  std::vector<int> level(nops, 0), slot_write(nslots, -1), slot_read(nslots, -1);
+  // dependency levels: RAW on children (cdep), WAR/WAW on the parent slot (pdep)
+  std::vector<int> level(nops, 0), pdep(nops, 0), w1(nops, -1), w2(nops, -1);
+  std::vector<int> slot_write(nslots, -1), slot_read(nslots, -1), last_writer(nslots, -1);
   int nlev = 0;
   for (int j = 0; j < nops; j++) {
     const plfx_trav_op &o = ops[j];
@@ -392,36 +401,105 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op 
     if (o.parent == o.child1 || o.parent == o.child2)
       return fail(ctx, PLFX_ERR_INVALID, "op %d: parent slot aliases a child", j);
     if (is_tip(o.parent)) return fail(ctx, PLFX_ERR_INVALID, "op %d: parent slot is a tip", j);
-    int lv = 0;
+    int cdep = 0, pd = 0;
     for (int sl : {o.child1, o.child2})
-      if (slot_write[sl] >= 0) lv = std::max(lv, slot_write[sl] + 1);
-    if (slot_write[o.parent] >= 0) lv = std::max(lv, slot_write[o.parent] + 1);
-    if (slot_read[o.parent] >= 0) lv = std::max(lv, slot_read[o.parent] + 1);
+      if (slot_write[sl] >= 0) cdep = std::max(cdep, slot_write[sl] + 1);
+    if (slot_write[o.parent] >= 0) pd = std::max(pd, slot_write[o.parent] + 1);
+    if (slot_read[o.parent] >= 0) pd = std::max(pd, slot_read[o.parent] + 1);
+    const int lv = std::max(cdep, pd);
     level[j] = lv;
+    pdep[j] = pd;
+    w1[j] = last_writer[o.child1];
+    w2[j] = last_writer[o.child2];
     slot_write[o.parent] = lv;
+    last_writer[o.parent] = j;
     for (int sl : {o.child1, o.child2}) slot_read[sl] = std::max(slot_read[sl], lv);
     nlev = std::max(nlev, lv + 1);
   }
   hipStream_t s = pick(ctx, stream);
   const char *pm = static_cast<const char *>(pmats);
+  // the node descriptor of op j, tip child first (dense/tip runs as tip/dense:
+  // the product u1*u2 commutes exactly); *kind = number of tip children
+  auto node_of = [&](int j, int *kind) {
+    const plfx_trav_op &o = ops[j];
+    const bool t1 = is_tip(o.child1), t2 = is_tip(o.child2);
+    plfx_node nd{t1 ? (const void *)tips[o.child1] : clv[o.child1],
+                 t2 ? (const void *)tips[o.child2] : clv[o.child2], clv[o.parent],
+                 pm + (size_t)(2 * o.pmat) * mat * es, pm + (size_t)(2 * o.pmat + 1) * mat * es,
+                 scalers ? scalers[j] : nullptr, scaler_sums ? scaler_sums + j : nullptr};
+    if (!t1 && t2) {
+      std::swap(nd.x1, nd.x2);
+      std::swap(nd.left, nd.right);
+    }
+    *kind = (t1 ? 1 : 0) + (t2 ? 1 : 0);
+    return nd;
+  };
+  // Fused level pairs (f64 DNA): op P whose two children were last written by
+  // ops A, B of the level just below it, with the same tip kind, and whose own
+  // slot is free by then (pdep <= level of A), runs with A and B in one pass
+  // (plf_dna.hpp TripleDesc): A's and B's CLVs are written but not read back.
+  struct Triple {
+    int a, b, p, kind;
+  };
+  std::vector<Triple> triples;
+  std::vector<char> used(nops, 0);
+  if (ctx->fuse && dtype == PLFX_F64) {
+    for (int p = 0; p < nops; p++) {
+      const int a = w1[p], b = w2[p];
+      if (a < 0 || b < 0 || a == b || used[a] || used[b] || used[p]) continue;
+      const int L = level[a];
+      if (level[b] != L || level[p] != L + 1 || pdep[p] > L) continue;
+      int ka, kb;
+      node_of(a, &ka);
+      node_of(b, &kb);
+      if (ka != kb) continue;
+      used[a] = used[b] = used[p] = 1;
+      triples.push_back({a, b, p, ka});
+    }
+  }
   std::vector<plfx_node> batch[3];  // by number of tip children
+  std::vector<plfx::TripleDescH> tb[3];
   for (int lv = 0; lv < nlev; lv++) {
-    for (auto &b : batch) b.clear();
+    for (int k = 0; k < 3; k++) {
+      batch[k].clear();
+      tb[k].clear();
+    }
+    for (const Triple &t : triples) {
+      if (level[t.a] != lv) continue;
+      int ka, kb, kp;
+      const plfx_node A = node_of(t.a, &ka), B = node_of(t.b, &kb), P = node_of(t.p, &kp);
+      for (int rc : {check_node(ctx, A, ka, n, t.a), check_node(ctx, B, kb, n, t.b),
+                     check_node(ctx, P, kp, n, t.p)})
+        if (rc != PLFX_OK) return rc;
+      // P's children as op P names them: child1 = A's slot or B's slot
+      const bool a_first = ops[t.p].child1 == ops[t.a].parent;
+      const plfx_node &F = a_first ? A : B, &G = a_first ? B : A;
+      tb[t.kind].push_back(plfx::TripleDescH{
+          F.x1, F.x2, G.x1, G.x2, F.x3, G.x3, P.x3, (const double *)F.left,
+          (const double *)F.right, (const double *)G.left, (const double *)G.right,
+          (const double *)P.left, (const double *)P.right, F.scaler, G.scaler, P.scaler,
+          F.scaler_sum, G.scaler_sum, P.scaler_sum});
+    }
     for (int j = 0; j < nops; j++) {
-      if (level[j] != lv) continue;
-      const plfx_trav_op &o = ops[j];
-      const bool t1 = is_tip(o.child1), t2 = is_tip(o.child2);
-      plfx_node nd{t1 ? (const void *)tips[o.child1] : clv[o.child1],
-                   t2 ? (const void *)tips[o.child2] : clv[o.child2], clv[o.parent],
-                   pm + (size_t)(2 * o.pmat) * mat * es, pm + (size_t)(2 * o.pmat + 1) * mat * es,
-                   scalers ? scalers[j] : nullptr, scaler_sums ? scaler_sums + j : nullptr};
-      if (!t1 && t2) {  // dense/tip -> tip/dense (exact: the product commutes)
-        std::swap(nd.x1, nd.x2);
-        std::swap(nd.left, nd.right);
-      }
-      batch[(t1 ? 1 : 0) + (t2 ? 1 : 0)].push_back(nd);
+      if (level[j] != lv || used[j]) continue;
+      int kind;
+      const plfx_node nd = node_of(j, &kind);
+      batch[kind].push_back(nd);
     }
     for (int k = 0; k < 3; k++) {
+      for (size_t i = 0; i < tb[k].size(); i += plfx::kMaxTriples) {
+        const int c = (int)std::min<size_t>(plfx::kMaxTriples, tb[k].size() - i);
+        if (n == 0) {
+          for (int q = 0; q < c; q++)
+            for (int64_t *ss : {tb[k][i + q].ssa, tb[k][i + q].ssb, tb[k][i + q].ssp})
+              if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
+          continue;
+        }
+        hipError_t e = plfx::launch_plf_dna_triples(tb[k].data() + i, c, (const double *)EV, wgt, n,
+                                                    ctx->ws, ctx->max_blocks, s, k,
+                                                    (const double *)tipvec);
+        if (e != hipSuccess) return hip_fail(ctx, e, "fused level-pair launch");
+      }
       if (batch[k].empty()) continue;
       int rc = batch_impl(ctx, dtype, batch[k].data(), (int)batch[k].size(), EV, n, wgt, s, k,
                           tipvec);

@@ -85,6 +85,8 @@ def parse():
                     help="protein: fused multiply-add mode (the default; f64 runs on the matrix cores)")
     ap.add_argument("--exact", action="store_true",
                     help="protein: plf()'s separate multiply/add (bit-identical to the double loop)")
+    ap.add_argument("--no-fuse", action="store_true",
+                    help="tree64: one launch per level instead of fused level pairs (PLFX_FUSE=0)")
     ap.add_argument("--tips", action="store_true",
                     help="tree64: tips as uint8 state codes (plfx.h section 8) instead of dense CLVs")
     ap.add_argument("--workload", choices=["node", "tree64", "nodes64", "protein"], default="node",
@@ -222,16 +224,23 @@ class Tree64Workload:
         self.lnl = torch.zeros(1, dtype=torch.float64, device=dev)
         self.sites_per_step = nops * n
         # per node: read x1, x2, write x3, read wgt (scaler sums, no bytes); + lnL read of the root.
-        # With coded tips the 32 tip/tip nodes read 2 code bytes instead of two CLVs.
-        self.bytes_per_site = 3 * 16 * esz + 4
-        inner = nops - ntips // 2 if a.tips else nops
-        self.bytes_per_step = inner * self.bytes_per_site * n + (16 * esz + 4) * n
-        if a.tips:
-            self.bytes_per_step += (ntips // 2) * (16 * esz + 2 + 4) * n
+        # With coded tips a tip child reads 1 code byte instead of a CLV.  Fused level pairs
+        # (f64): A, B and their parent P in one pass -- 4 child reads + 3 writes + wgt.
+        clv_b, tip_b = 16 * esz, 1
+        self.fused = esz == 8 and not a.no_fuse
+        self.bytes_per_site = 3 * clv_b + 4
+        if self.fused:  # levels (32,16), (8,4), (2,1) as 16 + 4 + 1 triples
+            first = 4 * (tip_b if a.tips else clv_b) + 3 * clv_b + 4
+            self.bytes_per_step = (16 * first + 5 * (7 * clv_b + 4) + (clv_b + 4)) * n
+        else:
+            first = 2 * (tip_b if a.tips else clv_b) + clv_b + 4
+            self.bytes_per_step = (32 * first + 31 * (3 * clv_b + 4) + (clv_b + 4)) * n
         tipdesc = "tips as uint8 state codes" if a.tips else "dense tip CLVs"
+        sched = ("fused level pairs: 21 three-node passes in 3 launch groups" if self.fused
+                 else "6 level launches")
         self.config = {
             "workload": f"DNA 4-state, 64-taxon balanced tree post-order sweep (63 inner nodes, "
-                        f"6 level launches) + root lnL, {n} sites, {a.dtype}, {tipdesc} "
+                        f"{sched}) + root lnL, {n} sites, {a.dtype}, {tipdesc} "
                         f"(BASELINE configs[2])",
             "sites_per_gpu_per_step": self.sites_per_step, "nodes_per_gpu_per_step": nops}
 
@@ -369,6 +378,8 @@ WORKLOADS = {"node": NodeWorkload, "tree64": Tree64Workload, "nodes64": Nodes64W
 
 def main():
     a = parse()
+    if a.no_fuse:
+        os.environ["PLFX_FUSE"] = "0"  # read by plfx_ctx_create
     import torch
     import torch.distributed as dist
 

@@ -176,3 +176,56 @@ def test_tree64_full_size_window(ctx, oracle):
     root = clv[-1].cpu().numpy()
     exp = oracle.root_lnl(4, 4, root, n, scaler_sums=gsums)
     assert abs(float(out.item()) - exp) <= LNL_RTOL * abs(exp)
+
+
+@pytest.mark.parametrize("coded", [False, True])
+def test_fused_level_pairs_match_unfused(ctx, oracle, coded, monkeypatch):
+    """f64 traversals run fused level pairs (parent + both children in one
+    pass).  A 32-taxon tree with a caterpillar tail and mixed tip kinds: the
+    fused schedule (default context) and the level-by-level one (PLFX_FUSE=0)
+    produce identical CLVs, scaler bytes and sums, equal to the oracle."""
+    import plfx
+    import torch
+
+    n = 3001
+    rng = np.random.default_rng(12)
+    ops = [list(r) for r in oracle.balanced_tree_ops(32)]      # slots 32..62, root 62
+    nb = len(ops)
+    ops += [[63, 62, 0, nb], [64, 63, 5, nb + 1], [65, 64, 63, nb + 2]]  # tail reuses tips/inner
+    ops = np.array(ops, np.int32)
+    nslots, nops = 66, ops.shape[0]
+    codes = [oracle.random_tip_codes(rng, n, 0.2) for _ in range(32)]
+    is_coded = [coded and t % 4 != 3 for t in range(32)]
+    dense = [rng.random(16 * n) for _ in range(32)]
+    pm = rng.random(nops * 128) * 0.3
+    EV = rng.random(16) * 0.3
+    wgt = rng.integers(1, 5, n).astype(np.int32)
+    host = [oracle.expand_tips(codes[t]) if is_coded[t] else dense[t].copy() for t in range(32)]
+    host += [np.zeros(16 * n) for _ in range(nslots - 32)]
+    esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
+    assert esums.sum() > 0
+
+    def run(c):
+        clv = [None if is_coded[t] else dev(dense[t]) for t in range(32)]
+        clv += [torch.zeros(16 * n, dtype=torch.float64, device="cuda") for _ in range(nslots - 32)]
+        tips = [dev(codes[t]) if is_coded[t] else None for t in range(32)] + [None] * (nslots - 32)
+        sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
+        scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+        c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips)
+        torch.cuda.synchronize()
+        return clv, sums.cpu().numpy(), [x.cpu().numpy() for x in scal]
+
+    fused = run(ctx)
+    monkeypatch.setenv("PLFX_FUSE", "0")
+    plain_ctx = plfx.Context(0)
+    try:
+        plain = run(plain_ctx)
+    finally:
+        plain_ctx.close()
+    for s in range(32, nslots):
+        f = fused[0][s].cpu().numpy()
+        assert np.array_equal(bits(f), bits(host[s])), s
+        assert np.array_equal(bits(f), bits(plain[0][s].cpu().numpy())), s
+    assert np.array_equal(fused[1], esums) and np.array_equal(plain[1], esums)
+    for j in range(nops):
+        assert np.array_equal(fused[2][j], escal[j]) and np.array_equal(plain[2][j], escal[j]), j
