@@ -45,7 +45,7 @@ hipError_t launch_plf_dna_batch(int dtype, const NodeDescH *nodes, int count, co
                                 int max_blocks, hipStream_t s, int tips = 0,
                                 const void *tipvec = nullptr);
 
-// Root log-likelihood; partials: >= kLnlMaxGrid doubles; ticket: 1 u64 (zero at rest).
+// Root log-likelihood; partials: >= kLnlMaxGrid doubles; ticket: kWsWords u64 (zero at rest).
 constexpr int kLnlMaxGrid = 4096;
 hipError_t launch_root_lnl(int dtype, int states, const void *x, int64_t n, const double *catw,
                            const double *freq, const int32_t *wgt, const int64_t *scaler_sums,

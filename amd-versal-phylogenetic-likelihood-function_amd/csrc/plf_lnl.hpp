@@ -11,8 +11,9 @@
 // scalerIncrement_node (plf.cpp:58-64).
 //
 // Deterministic: per-block partial sums land in fixed slots (sc1 stores,
-// drained), a ticket elects the last block, which sums the slots in index
-// order (sc1 loads) -- the result does not depend on block arrival order.
+// drained), a two-level ticket (kWsWords words, zero at rest) elects the last
+// block, which sums the slots in index order (sc1 loads) -- the result does
+// not depend on block arrival order.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -24,7 +25,11 @@ namespace dev {
 
 constexpr double kLogMinLik = -22.18070977791824990137;  // log(2^-32) = -32 ln 2
 
-// C lanes per site (lane = category); S states per lane.
+// C lanes per site (lane = category); S states per lane.  A loop trip covers C
+// wave steps (C x 64/C sites): all loads first, then each site's L is built in
+// its C lanes (ascending s, then c, as the oracle) and lane c takes the log of
+// step c's site -- every lane evaluates one log per trip instead of one lane
+// in C (the log, not HBM, bounded the one-step form: 51 us for 2^20 DNA sites).
 template <typename T, int S, int C>
 __global__ void __launch_bounds__(kBlock)
 root_lnl_kernel(const T *__restrict__ x, int64_t n, const double *__restrict__ catw,
@@ -46,21 +51,47 @@ root_lnl_kernel(const T *__restrict__ x, int64_t n, const double *__restrict__ c
 
   double acc = 0.0;
   const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * SPW;
-  for (int64_t base = wave * SPW; base < n; base += stride) {
-    const int64_t site = base + q;
-    const bool valid = site < n;
-    double t = 0.0;
-    if (valid) {
-      const T *xs = x + site * V + c * S;
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * SPW * C;
+  for (int64_t base = wave * SPW * C; base < n; base += stride) {
+    T v[C][S];
 #pragma unroll
-      for (int s = 0; s < S; s++) t += fr[s] * (double)xs[s];
+    for (int u = 0; u < C; u++) {
+      const int64_t site = base + u * SPW + q;
+      if (site < n) {
+        const T *xs = x + site * V + c * S;  // 16-B aligned: S*sizeof(T) is a multiple of 16
+        if constexpr (sizeof(T) == 8) {
+#pragma unroll
+          for (int s = 0; s < S; s += 2) {
+            const f64x2 w = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(xs + s));
+            v[u][s] = w.x;
+            v[u][s + 1] = w.y;
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < S; s += 4) {
+            const f32x4 w = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(xs + s));
+            v[u][s] = w.x; v[u][s + 1] = w.y; v[u][s + 2] = w.z; v[u][s + 3] = w.w;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; s++) v[u][s] = T(0);
+      }
     }
-    double L = 0.0;
+    double mine = 1.0;  // L of step c's site (this lane's log)
 #pragma unroll
-    for (int k = 0; k < C; k++) L += cw[k] * __shfl(t, (lane / C) * C + k);
-    if (valid && c == 0) {
-      const double l = log(L);
+    for (int u = 0; u < C; u++) {
+      double t = 0.0;
+#pragma unroll
+      for (int s = 0; s < S; s++) t += fr[s] * (double)v[u][s];
+      double L = 0.0;
+#pragma unroll
+      for (int k = 0; k < C; k++) L += cw[k] * __shfl(t, (lane / C) * C + k);
+      if (u == c) mine = L;
+    }
+    const int64_t site = base + c * SPW + q;
+    if (site < n) {
+      const double l = log(mine);
       if (site_lnl) site_lnl[site] = l;
       acc += (wgt ? (double)wgt[site] : 1.0) * l;
     }
@@ -80,9 +111,20 @@ root_lnl_kernel(const T *__restrict__ x, int64_t n, const double *__restrict__ c
                        __builtin_bit_cast(unsigned long long, b), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long t =
-        __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == gridDim.x - 1);
+    // two-level election (a single counter serialises ~12 ns per arrival:
+    // 20 us for 1800 blocks): slot counters 128 B apart, then a top counter;
+    // both return to zero
+    const unsigned long long G = gridDim.x, slot = blockIdx.x % kSlots;
+    const unsigned long long nslots = G < kSlots ? G : kSlots;
+    const unsigned long long arrivals = (G - slot + kSlots - 1) / kSlots;
+    int is_last = 0;
+    if (__hip_atomic_fetch_add(ticket + slot * 16, 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT) == arrivals - 1) {
+      __hip_atomic_store(ticket + slot * 16, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      is_last = __hip_atomic_fetch_add(ticket + kSlots * 16, 1ull, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) == nslots - 1;
+    }
+    last = is_last;
   }
   __syncthreads();
   if (!last) return;
@@ -103,7 +145,7 @@ root_lnl_kernel(const T *__restrict__ x, int64_t n, const double *__restrict__ c
     long long nsc = 0;
     for (int i = 0; i < nsums; i++) nsc += scaler_sums[i];
     *out = tot + (double)nsc * kLogMinLik;
-    __hip_atomic_store(ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ticket + kSlots * 16, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

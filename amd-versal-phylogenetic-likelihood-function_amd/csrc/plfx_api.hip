@@ -221,8 +221,8 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
   if (hipMalloc(reinterpret_cast<void **>(&ctx->ws), ws_bytes) != hipSuccess ||
       hipMemsetAsync(ctx->ws, 0, ws_bytes, ctx->stream) != hipSuccess ||
       hipMalloc(reinterpret_cast<void **>(&ctx->lnl_partials), plfx::kLnlMaxGrid * sizeof(double)) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void **>(&ctx->lnl_ticket), sizeof(unsigned long long)) != hipSuccess ||
-      hipMemsetAsync(ctx->lnl_ticket, 0, sizeof(unsigned long long), ctx->stream) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void **>(&ctx->lnl_ticket), plfx::kWsWords * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemsetAsync(ctx->lnl_ticket, 0, plfx::kWsWords * sizeof(unsigned long long), ctx->stream) != hipSuccess ||
       hipStreamSynchronize(ctx->stream) != hipSuccess) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->lnl_partials) (void)hipFree(ctx->lnl_partials);

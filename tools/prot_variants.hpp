@@ -630,5 +630,124 @@ prot_ldsmat_p_kernel(const double *__restrict__ x1, const double *__restrict__ x
   block_ticket_sum(acc, ws, scaler_sum);
 }
 
+// Phases 1 and 2 merged (two independent add chains per row: u1 over x1 and
+// P_L, u2 over x2 and P_R), half rows streamed one ahead; phase 3 as before.
+template <int kMinBlocks = 2>
+__global__ void __launch_bounds__(kBlock, kMinBlocks)
+prot_ldsmat_c_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                     double *__restrict__ x3, const double *__restrict__ EV,
+                     const double *__restrict__ left, const double *__restrict__ right,
+                     const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                     unsigned long long *ws, int64_t *scaler_sum) {
+  constexpr int S = 20;
+  using PT = ProtTile<double>;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  __shared__ f64x2 mats[(2 * 4 * S * S + S * S) / 2];
+  {
+    const f64x2 *gl = reinterpret_cast<const f64x2 *>(left);
+    const f64x2 *gr = reinterpret_cast<const f64x2 *>(right);
+    const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
+    for (int i = threadIdx.x; i < 800; i += kBlock) { mats[i] = gl[i]; mats[800 + i] = gr[i]; }
+    for (int i = threadIdx.x; i < 200; i += kBlock) mats[1600 + i] = ge[i];
+  }
+  const double m = Num<double>::minlik();
+  __shared__ PT::V tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock];
+  long long acc = 0;
+  __syncthreads();
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    const f64x2 *mL = mats + off + c * 200, *mR = mats + off + 800 + c * 200, *mE = mats + off + 1600;
+    double a[S], b[S], U[S];
+    tile_load<double>(x1, base, n, tile);
+    __syncthreads();
+    row_read<double>(tile, lane, c, a);
+    __syncthreads();
+    tile_load<double>(x2, base, n, tile);
+    __syncthreads();
+    row_read<double>(tile, lane, c, b);
+    {
+      // half row q of both matrices: row q>>1, values 10*(q&1) .. +9
+      f64x2 cl[5], cr[5], nl[5], nr[5];
+      int o = 0;
+      double tok = 0.0, u1 = 0.0, u2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < 5; i++) { cl[i] = mL[i]; cr[i] = mR[i]; }
+#pragma unroll
+      for (int q = 0; q < 2 * S; q++) {
+        asm volatile("" : "+v"(o) : "v"(tok));
+        if (q + 1 < 2 * S) {
+#pragma unroll
+          for (int i = 0; i < 5; i++) { nl[i] = mL[o + (q + 1) * 5 + i]; nr[i] = mR[o + (q + 1) * 5 + i]; }
+        }
+        const int k = q >> 1, h = q & 1;
+        if (h == 0) { u1 = 0.0; u2 = 0.0; }
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          u1 += a[10 * h + 2 * i] * cl[i].x;
+          u2 += b[10 * h + 2 * i] * cr[i].x;
+          u1 += a[10 * h + 2 * i + 1] * cl[i].y;
+          u2 += b[10 * h + 2 * i + 1] * cr[i].y;
+        }
+        if (h == 1) U[k] = u1 * u2;
+        tok = u1;
+#pragma unroll
+        for (int i = 0; i < 5; i++) { cl[i] = nl[i]; cr[i] = nr[i]; }
+      }
+    }
+    double O[S];
+#pragma unroll
+    for (int l = 0; l < S; l++) O[l] = 0.0;
+    {
+      f64x2 cur[10], nxt[10];
+      int o = 0;
+      double tok = 0.0;
+#pragma unroll
+      for (int i = 0; i < 10; i++) cur[i] = mE[i];
+#pragma unroll
+      for (int k = 0; k < S; k++) {
+        asm volatile("" : "+v"(o) : "v"(tok));
+        if (k + 1 < S) {
+#pragma unroll
+          for (int i = 0; i < 10; i++) nxt[i] = mE[o + (k + 1) * 10 + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+          O[2 * i] += U[k] * cur[i].x;
+          O[2 * i + 1] += U[k] * cur[i].y;
+        }
+        tok = O[S - 1];
+#pragma unroll
+        for (int i = 0; i < 10; i++) cur[i] = nxt[i];
+      }
+    }
+    bool small = base + lane < n;
+#pragma unroll
+    for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
+    const unsigned long long mk = __ballot(small);
+    if (lane == 0) small_mask[c] = mk;
+    __syncthreads();
+    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+    const bool sc = (all >> lane) & 1ull;
+#pragma unroll
+    for (int l = 0; l < S; l++) {
+      const double sv = O[l] * Num<double>::two32();
+      O[l] = sc ? sv : O[l];
+    }
+    row_write<double>(tile, lane, c, O);
+    const int64_t site = base + lane;
+    if (site < n && c == 0) {
+      if (scaler) scaler[site] = (uint8_t)sc;
+      if (sc) acc += wgt ? (long long)wgt[site] : 1ll;
+    }
+    __syncthreads();
+    tile_store<double>(x3, base, n, tile);
+    __syncthreads();
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
 }  // namespace dev
 }  // namespace plfx

@@ -90,10 +90,9 @@ int main(int argc, char **argv) {
   }
   ADD_K("product exact", (&plf_prot_kernel<double, false, true>), 64)
   ADD_K("product fma-mfma", (&plf_prot_mfma_kernel<true>), 64)
-  ADD_K("ldsmat NS=1", (&prot_ldsmat_kernel<1>), 64)
-  ADD_K("ldsmat-h NS=1", (&prot_ldsmat_h_kernel<1>), 64)
-  ADD_K("ldsmat-pairs", (&prot_ldsmat_p_kernel<2>), 64)
-  ADD_K("ldsmat-pairs minb=3", (&prot_ldsmat_p_kernel<3>), 64)
+  ADD_K("product exact-lds (NS=1)", (&plf_prot_exact_f64_kernel<true>), 64)
+  ADD_K("ldsmat-c (phases 1+2 merged)", (&prot_ldsmat_c_kernel<2>), 64)
+  ADD_K("ldsmat-c minb=1", (&prot_ldsmat_c_kernel<1>), 64)
 
   // FMA-mode reference for the mfma variants
   std::vector<uint64_t> h_fref(n * 80);
