@@ -783,5 +783,128 @@ plf_dna_f64_triple_kernel(const TripleBatch tb, const double *__restrict__ EV,
                       d.ssp);
 }
 
+// Fused level pair in the lane = category mapping (f32): a node's output
+// (category c of site q, 4 states) is again exactly the next node's input.
+template <typename T, bool TL, bool TR>
+__device__ __forceinline__ void cat_node(const T (&a)[4], const T (&b)[4], const T *rowL,
+                                         const T *rowR, const T (&PL)[16], const T (&PR)[16],
+                                         const T (&E)[16], bool valid, int nib, T m, T (&o)[4],
+                                         bool &sc) {
+  if constexpr (TL || TR) site_cat_tips<T, TL, TR>(a, b, PL, PR, E, rowL, rowR, o);
+  else site_cat<T>(a, b, PL, PR, E, o);
+  const bool small = valid && (Num<T>::abs(o[0]) < m) && (Num<T>::abs(o[1]) < m) &&
+                     (Num<T>::abs(o[2]) < m) && (Num<T>::abs(o[3]) < m);
+  const unsigned long long mask = __ballot(small);
+  sc = ((mask >> nib) & 0xFull) == 0xFull;
+#pragma unroll
+  for (int l = 0; l < 4; l++) {
+    const T s = o[l] * Num<T>::two32();
+    o[l] = sc ? s : o[l];
+  }
+}
+
+template <typename T, bool kSum, int kMinWaves, bool NT, int kTips, int U = 1>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_cat_triple_kernel(const TripleBatch tb, const T *__restrict__ EV,
+                          const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
+                          const T *__restrict__ tipvec) {
+  constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
+  const TripleDesc &d = tb.d[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 3, q = lane >> 2, nib = lane & 60;
+  __shared__ T tab[T2 ? 4 : (T1 ? 2 : 1)][T1 ? 256 : 1];
+  const T *la = (const T *)d.la, *ra = (const T *)d.ra, *lb = (const T *)d.lb;
+  const T *rb = (const T *)d.rb, *lp = (const T *)d.lp, *rp = (const T *)d.rp;
+  if constexpr (T1) {
+    build_tip_table<T>(la, tipvec, tab[0]);
+    build_tip_table<T>(lb, tipvec, tab[1]);
+  }
+  if constexpr (T2) {
+    build_tip_table<T>(ra, tipvec, tab[2]);
+    build_tip_table<T>(rb, tipvec, tab[3]);
+  }
+  if constexpr (T1) __syncthreads();
+  T LA[16], RA[16], LB[16], RB[16], LP[16], RP[16], E[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    LA[i] = la[c * 16 + i]; RA[i] = ra[c * 16 + i];
+    LB[i] = lb[c * 16 + i]; RB[i] = rb[c * 16 + i];
+    LP[i] = lp[c * 16 + i]; RP[i] = rp[c * 16 + i];
+    E[i] = EV[i];
+  }
+  const T m = Num<T>::minlik();
+  const uint8_t *ta1 = (const uint8_t *)d.a1, *ta2 = (const uint8_t *)d.a2;
+  const uint8_t *tb1 = (const uint8_t *)d.b1, *tb2 = (const uint8_t *)d.b2;
+  const T *xa1 = (const T *)d.a1, *xa2 = (const T *)d.a2;
+  const T *xb1 = (const T *)d.b1, *xb2 = (const T *)d.b2;
+  T *xa = (T *)d.xa, *xb = (T *)d.xb, *xp = (T *)d.xp;
+  const int trow = c * 64;
+
+  long long accA = 0, accB = 0, accP = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  for (int64_t base = wave * 16 * U; base < n; base += stride) {
+    T va1[U][4], va2[U][4], vb1[U][4], vb2[U][4];
+    int ka1[U], ka2[U], kb1[U], kb2[U], w[U];
+    bool valid[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      valid[u] = site < n;
+      ka1[u] = ka2[u] = kb1[u] = kb2[u] = w[u] = 0;
+#pragma unroll
+      for (int l = 0; l < 4; l++) va1[u][l] = va2[u][l] = vb1[u][l] = vb2[u][l] = T(0);
+      if (valid[u]) {
+        const int64_t off = site * 16 + c * 4;
+        if constexpr (T1) {
+          ka1[u] = ta1[site] & 15;
+          kb1[u] = tb1[site] & 15;
+        } else {
+          Num<T>::template load4<NT>(xa1 + off, va1[u]);
+          Num<T>::template load4<NT>(xb1 + off, vb1[u]);
+        }
+        if constexpr (T2) {
+          ka2[u] = ta2[site] & 15;
+          kb2[u] = tb2[site] & 15;
+        } else {
+          Num<T>::template load4<NT>(xa2 + off, va2[u]);
+          Num<T>::template load4<NT>(xb2 + off, vb2[u]);
+        }
+        if (kSum) w[u] = wgt ? wgt[site] : 1;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      const int64_t off = site * 16 + c * 4;
+      T oA[4], oB[4], oP[4];
+      bool sA, sB, sP;
+      cat_node<T, T1, T2>(va1[u], va2[u], tab[0] + trow + 4 * ka1[u],
+                          tab[T2 ? 2 : 0] + trow + 4 * ka2[u], LA, RA, E, valid[u], nib, m, oA, sA);
+      cat_node<T, T1, T2>(vb1[u], vb2[u], tab[T1 ? 1 : 0] + trow + 4 * kb1[u],
+                          tab[T2 ? 3 : 0] + trow + 4 * kb2[u], LB, RB, E, valid[u], nib, m, oB, sB);
+      cat_node<T, false, false>(oA, oB, nullptr, nullptr, LP, RP, E, valid[u], nib, m, oP, sP);
+      if (valid[u]) {
+        Num<T>::store4_nt(xa + off, oA);
+        Num<T>::store4_nt(xb + off, oB);
+        Num<T>::store4_nt(xp + off, oP);
+        if (c == 0) {
+          if (d.sa) d.sa[site] = (uint8_t)sA;
+          if (d.sb) d.sb[site] = (uint8_t)sB;
+          if (d.sp) d.sp[site] = (uint8_t)sP;
+          if (kSum) {
+            if (sA) accA += w[u];
+            if (sB) accB += w[u];
+            if (sP) accP += w[u];
+          }
+        }
+      }
+    }
+  }
+  if constexpr (kSum)
+    block_ticket_sum3(accA, accB, accP, ws + (size_t)blockIdx.y * 3 * kWsWords, d.ssa, d.ssb,
+                      d.ssp);
+}
+
 }  // namespace dev
 }  // namespace plfx

@@ -44,6 +44,7 @@ constexpr bool kNt = true;   // f32: NT CLV loads (74.8% vs 70.2% of HBM peak, r
 constexpr bool kNtl64 = true;
 constexpr int kMinWaves = 1;
 constexpr int kTripleU = 1;  // fused level pairs: 16 sites per trip (tools/tune_triple.hip)
+constexpr int kTripleU32 = 2;
 
 // Co-resident 256-thread blocks of `kernel` on the current device (cached per
 // kernel instantiation by the caller).
@@ -193,11 +194,25 @@ hipError_t launch_triples_t(const dev::TripleBatch &b, int count, const double *
   return hipGetLastError();
 }
 
+template <bool kSum, int kTips>
+hipError_t launch_triples32_t(const dev::TripleBatch &b, int count, const float *EV,
+                              const int32_t *wgt, int64_t n, unsigned long long *ws,
+                              int max_blocks, hipStream_t s, const float *tipvec) {
+  static int cache = 0;
+  constexpr int U = kTripleU32;
+  auto kernel = &dev::plf_dna_cat_triple_kernel<float, kSum, 1, kNt, kTips, U>;
+  const int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 16 * U, count,
+                            max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt,
+                     n, ws, tipvec);
+  return hipGetLastError();
+}
+
 }  // namespace
 
-hipError_t launch_plf_dna_triples(const TripleDescH *t, int count, const double *EV,
+hipError_t launch_plf_dna_triples(int dtype, const TripleDescH *t, int count, const void *EV,
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,
-                                  int max_blocks, hipStream_t s, int tips, const double *tipvec) {
+                                  int max_blocks, hipStream_t s, int tips, const void *tipvec) {
   if (count < 1 || count > kMaxTriples || tips < 0 || tips > 2) return hipErrorInvalidValue;
   dev::TripleBatch b{};
   bool any_sum = false;
@@ -206,13 +221,21 @@ hipError_t launch_plf_dna_triples(const TripleDescH *t, int count, const double 
     __builtin_memcpy(&b.d[i], &t[i], sizeof(t[i]));
     any_sum |= t[i].ssa || t[i].ssb || t[i].ssp;
   }
-  switch ((any_sum ? 3 : 0) + tips) {
-    case 0: return launch_triples_t<false, 0>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    case 1: return launch_triples_t<false, 1>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    case 2: return launch_triples_t<false, 2>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    case 3: return launch_triples_t<true, 0>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    case 4: return launch_triples_t<true, 1>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    default: return launch_triples_t<true, 2>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+  const double *E64 = (const double *)EV, *V64 = (const double *)tipvec;
+  const float *E32 = (const float *)EV, *V32 = (const float *)tipvec;
+  switch ((dtype == 1 ? 6 : 0) + (any_sum ? 3 : 0) + tips) {
+    case 0: return launch_triples32_t<false, 0>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 1: return launch_triples32_t<false, 1>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 2: return launch_triples32_t<false, 2>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 3: return launch_triples32_t<true, 0>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 4: return launch_triples32_t<true, 1>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 5: return launch_triples32_t<true, 2>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 6: return launch_triples_t<false, 0>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    case 7: return launch_triples_t<false, 1>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    case 8: return launch_triples_t<false, 2>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    case 9: return launch_triples_t<true, 0>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    case 10: return launch_triples_t<true, 1>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    default: return launch_triples_t<true, 2>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
   }
 }
 

@@ -61,7 +61,7 @@ hipError_t launch_pmatrix(int dtype, bool eigen_conv, const double *eigen, int S
                           const double *rates, int ncat, const double *blen, int64_t nbranch,
                           void *out, hipStream_t s);
 
-// Fused level pairs (plf_dna.hpp TripleDesc), f64 only; <= kMaxTriples per
+// Fused level pairs (plf_dna.hpp TripleDesc), dtype 0 f32 / 1 f64; <= kMaxTriples per
 // launch, ws >= 3 * count regions.  tips as plf_dna_f64_triple_kernel's kTips.
 struct TripleDescH {
   const void *a1, *a2, *b1, *b2;
@@ -71,8 +71,8 @@ struct TripleDescH {
   int64_t *ssa, *ssb, *ssp;
 };
 constexpr int kMaxTriples = 10;
-hipError_t launch_plf_dna_triples(const TripleDescH *t, int count, const double *EV,
+hipError_t launch_plf_dna_triples(int dtype, const TripleDescH *t, int count, const void *EV,
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,
-                                  int max_blocks, hipStream_t s, int tips, const double *tipvec);
+                                  int max_blocks, hipStream_t s, int tips, const void *tipvec);
 
 }  // namespace plfx

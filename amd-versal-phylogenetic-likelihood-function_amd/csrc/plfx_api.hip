@@ -434,7 +434,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op 
     *kind = (t1 ? 1 : 0) + (t2 ? 1 : 0);
     return nd;
   };
-  // Fused level pairs (f64 DNA): op P whose two children were last written by
+  // Fused level pairs (DNA): op P whose two children were last written by
   // ops A, B of the level just below it, with the same tip kind, and whose own
   // slot is free by then (pdep <= level of A), runs with A and B in one pass
   // (plf_dna.hpp TripleDesc): A's and B's CLVs are written but not read back.
@@ -443,7 +443,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op 
   };
   std::vector<Triple> triples;
   std::vector<char> used(nops, 0);
-  if (ctx->fuse && dtype == PLFX_F64) {
+  if (ctx->fuse) {
     for (int p = 0; p < nops; p++) {
       const int a = w1[p], b = w2[p];
       if (a < 0 || b < 0 || a == b || used[a] || used[b] || used[p]) continue;
@@ -495,9 +495,8 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op 
               if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
           continue;
         }
-        hipError_t e = plfx::launch_plf_dna_triples(tb[k].data() + i, c, (const double *)EV, wgt, n,
-                                                    ctx->ws, ctx->max_blocks, s, k,
-                                                    (const double *)tipvec);
+        hipError_t e = plfx::launch_plf_dna_triples(dtype, tb[k].data() + i, c, EV, wgt, n, ctx->ws,
+                                                    ctx->max_blocks, s, k, tipvec);
         if (e != hipSuccess) return hip_fail(ctx, e, "fused level-pair launch");
       }
       if (batch[k].empty()) continue;

@@ -224,10 +224,10 @@ class Tree64Workload:
         self.lnl = torch.zeros(1, dtype=torch.float64, device=dev)
         self.sites_per_step = nops * n
         # per node: read x1, x2, write x3, read wgt (scaler sums, no bytes); + lnL read of the root.
-        # With coded tips a tip child reads 1 code byte instead of a CLV.  Fused level pairs
-        # (f64): A, B and their parent P in one pass -- 4 child reads + 3 writes + wgt.
+        # With coded tips a tip child reads 1 code byte instead of a CLV.  Fused level pairs:
+        # A, B and their parent P in one pass -- 4 child reads + 3 writes + wgt.
         clv_b, tip_b = 16 * esz, 1
-        self.fused = esz == 8 and not a.no_fuse
+        self.fused = not a.no_fuse
         self.bytes_per_site = 3 * clv_b + 4
         if self.fused:  # levels (32,16), (8,4), (2,1) as 16 + 4 + 1 triples
             first = 4 * (tip_b if a.tips else clv_b) + 3 * clv_b + 4

@@ -178,9 +178,10 @@ def test_tree64_full_size_window(ctx, oracle):
     assert abs(float(out.item()) - exp) <= LNL_RTOL * abs(exp)
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("coded", [False, True])
-def test_fused_level_pairs_match_unfused(ctx, oracle, coded, monkeypatch):
-    """f64 traversals run fused level pairs (parent + both children in one
+def test_fused_level_pairs_match_unfused(ctx, oracle, coded, dtype, monkeypatch):
+    """Traversals run fused level pairs (parent + both children in one
     pass).  A 32-taxon tree with a caterpillar tail and mixed tip kinds: the
     fused schedule (default context) and the level-by-level one (PLFX_FUSE=0)
     produce identical CLVs, scaler bytes and sums, equal to the oracle."""
@@ -196,18 +197,19 @@ def test_fused_level_pairs_match_unfused(ctx, oracle, coded, monkeypatch):
     nslots, nops = 66, ops.shape[0]
     codes = [oracle.random_tip_codes(rng, n, 0.2) for _ in range(32)]
     is_coded = [coded and t % 4 != 3 for t in range(32)]
-    dense = [rng.random(16 * n) for _ in range(32)]
-    pm = rng.random(nops * 128) * 0.3
-    EV = rng.random(16) * 0.3
+    dense = [rng.random(16 * n).astype(dtype) for _ in range(32)]
+    pm = (rng.random(nops * 128) * 0.3).astype(dtype)
+    EV = (rng.random(16) * 0.3).astype(dtype)
     wgt = rng.integers(1, 5, n).astype(np.int32)
-    host = [oracle.expand_tips(codes[t]) if is_coded[t] else dense[t].copy() for t in range(32)]
-    host += [np.zeros(16 * n) for _ in range(nslots - 32)]
+    host = [oracle.expand_tips(codes[t], dtype) if is_coded[t] else dense[t].copy() for t in range(32)]
+    host += [np.zeros(16 * n, dtype) for _ in range(nslots - 32)]
     esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
     assert esums.sum() > 0
 
     def run(c):
         clv = [None if is_coded[t] else dev(dense[t]) for t in range(32)]
-        clv += [torch.zeros(16 * n, dtype=torch.float64, device="cuda") for _ in range(nslots - 32)]
+        tt = torch.float64 if dtype == np.float64 else torch.float32
+        clv += [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nslots - 32)]
         tips = [dev(codes[t]) if is_coded[t] else None for t in range(32)] + [None] * (nslots - 32)
         sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
         scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
