@@ -143,6 +143,29 @@ def cpu_baseline(n_sites, seconds):
     return res
 
 
+def host_buffers_rate(ctx, n_sites, dtype, seconds=2.0):
+    """The plf()-shaped entry on host arrays (plfx_plf_f64/f32: H2D -> kernel ->
+    D2H, synchronous, pageable numpy buffers as plf()'s callers pass them):
+    the PCIe-inclusive rate, reported beside `value`, never as it."""
+    import numpy as np
+
+    rng = np.random.default_rng(SEED)
+    x1 = rng.random(16 * n_sites).astype(dtype)
+    x2 = rng.random(16 * n_sites).astype(dtype)
+    x3 = np.empty_like(x1)
+    EV, L, R = (rng.random(16).astype(dtype), rng.random(64).astype(dtype),
+                rng.random(64).astype(dtype))
+    wgt = np.ones(n_sites, np.int32)
+    ctx.plf(x1, x2, x3, EV, n_sites, L, R, wgt)  # warm-up (staging buffers)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        ctx.plf(x1, x2, x3, EV, n_sites, L, R, wgt)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return reps * n_sites / el, reps
+
+
 class NodeWorkload:
     """BASELINE configs[1]: one inner node of n sites per GPU per step, rotating
     over R buffer sets (R x 389 MiB > the 256 MiB Infinity Cache)."""
@@ -497,7 +520,21 @@ def main():
             "check": "ok" if check_ok else "CHECK_FAILED",
         }
         if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(a.sites, a.cpu_seconds)
+            out["cpu_baseline"] = cb = cpu_baseline(a.sites, a.cpu_seconds)
+            if a.workload == "node":
+                # the reference host's report rows (timing.h:107-151): its CPU
+                # plf() as "Reference" and the speed-ups excluding / including
+                # the host<->device transfers
+                import numpy as np
+
+                hb, reps = host_buffers_rate(ctx, a.sites, np.float64 if esz == 8 else np.float32)
+                out["host_buffers"] = {
+                    "value": hb, "unit": "sites/s",
+                    "sample": f"{reps} x plfx_plf_{a.dtype}({a.sites} sites) on pageable host arrays"}
+                ref = cb.get("reference_plf_O0_f32_1thread")
+                if ref:
+                    out["speedup_vs_reference_plf"] = {"excluding_pcie": value / ref,
+                                                       "including_pcie": hb / ref}
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
