@@ -167,7 +167,7 @@ int check_node(plfx_ctx *ctx, const plfx_node &d, int tips, int64_t n, int i) {
 // launches of kMaxBatch.  A tip child is a uint8 code array (no alignment rule).
 int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, const void *EV,
                int64_t n, const int32_t *wgt, hipStream_t s, int tips,
-               const void *tipvec = nullptr) {
+               const void *tipvec = nullptr, int states = 4, int flags = PLFX_EXACT) {
   if (count < 0 || n < 0 || (count > 0 && (!nodes || !EV)))
     return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
   for (int i = 0; i < count; i++) {
@@ -177,6 +177,15 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
     if (n == 0 && d.scaler_sum) PLFX_HIP(ctx, hipMemsetAsync(d.scaler_sum, 0, sizeof(int64_t), s));
   }
   if (n == 0) return PLFX_OK;
+  if (states == 20) {  // protein: one full-GPU launch per node (plf_prot.hpp)
+    for (int i = 0; i < count; i++) {
+      const plfx_node &d = nodes[i];
+      plfx::DnaArgs a{d.x1, d.x2, d.x3, EV, d.left, d.right, wgt, d.scaler, d.scaler_sum, ctx->ws, n};
+      hipError_t e = plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s);
+      if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot launch");
+    }
+    return PLFX_OK;
+  }
   for (int i = 0; i < count; i += plfx::kMaxBatch) {
     const int c = std::min(plfx::kMaxBatch, count - i);
     hipError_t e = plfx::launch_plf_dna_batch(dtype, reinterpret_cast<const plfx::NodeDescH *>(nodes + i),
@@ -346,8 +355,9 @@ int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *no
                        const void *EV, int64_t n, const int32_t *wgt, void *stream) {
   if (!ctx) return PLFX_ERR_INVALID;
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
-  if (states != 4) return fail(ctx, PLFX_ERR_UNSUPPORTED, "batched nodes: states=%d not built", states);
-  return batch_impl(ctx, dtype, nodes, count, EV, n, wgt, pick(ctx, stream), 0);
+  if (states != 4 && states != 20)
+    return fail(ctx, PLFX_ERR_UNSUPPORTED, "batched nodes: states=%d not built (4, 20)", states);
+  return batch_impl(ctx, dtype, nodes, count, EV, n, wgt, pick(ctx, stream), 0, nullptr, states);
 }
 
 int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void *x1,
@@ -372,20 +382,26 @@ int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops,
                   void *const *clv, int nslots, const void *pmats, int npmats, const void *EV,
                   int64_t n, const int32_t *wgt, uint8_t *const *scalers, int64_t *scaler_sums,
                   void *stream) {
-  return plfx_traverse_tips(ctx, dtype, states, ops, nops, clv, nullptr, nslots, pmats, npmats, EV,
-                            n, wgt, scalers, scaler_sums, nullptr, stream);
+  return plfx_traverse_tips(ctx, dtype, states, PLFX_EXACT, ops, nops, clv, nullptr, nslots, pmats,
+                            npmats, EV, n, wgt, scalers, scaler_sums, nullptr, stream);
 }
 
-int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
+int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const plfx_trav_op *ops,
+                       int nops,
                        void *const *clv, const uint8_t *const *tips, int nslots, const void *pmats,
                        int npmats, const void *EV, int64_t n, const int32_t *wgt,
                        uint8_t *const *scalers, int64_t *scaler_sums, const void *tipvec,
                        void *stream) {
   if (!ctx) return PLFX_ERR_INVALID;
-  if (states != 4) return fail(ctx, PLFX_ERR_UNSUPPORTED, "traverse: states=%d not built", states);
+  if (states != 4 && states != 20)
+    return fail(ctx, PLFX_ERR_UNSUPPORTED, "traverse: states=%d not built (4, 20)", states);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if (flags & ~PLFX_FMA) return fail(ctx, PLFX_ERR_INVALID, "bad flags %d", flags);
   if (nops < 0 || (nops > 0 && (!ops || !clv || !pmats || !EV)))
     return fail(ctx, PLFX_ERR_INVALID, "bad traverse arguments");
+  if (states != 4 && tips)
+    for (int sl = 0; sl < nslots; sl++)
+      if (tips[sl]) return fail(ctx, PLFX_ERR_UNSUPPORTED, "tip codes are DNA only (states=%d)", states);
   const size_t es = dtype == PLFX_F32 ? 4 : 8;
   const size_t mat = (size_t)states * states * 4;  // C*S*S values per matrix
   auto is_tip = [&](int sl) { return tips && tips[sl]; };
@@ -443,7 +459,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op 
   };
   std::vector<Triple> triples;
   std::vector<char> used(nops, 0);
-  if (ctx->fuse) {
+  if (ctx->fuse && states == 4) {
     for (int p = 0; p < nops; p++) {
       const int a = w1[p], b = w2[p];
       if (a < 0 || b < 0 || a == b || used[a] || used[b] || used[p]) continue;
@@ -501,7 +517,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op 
       }
       if (batch[k].empty()) continue;
       int rc = batch_impl(ctx, dtype, batch[k].data(), (int)batch[k].size(), EV, n, wgt, s, k,
-                          tipvec);
+                          tipvec, states, flags);
       if (rc != PLFX_OK) return rc;
     }
   }

@@ -135,7 +135,7 @@ def load():
     L.plfx_model_tip_vectors.argtypes = [i32, i32, dp, dp]
     L.plfx_plf_tips_dev.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp,
                                     vp]
-    L.plfx_traverse_tips.argtypes = [vp, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp),
+    L.plfx_traverse_tips.argtypes = [vp, i32, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp),
                                      C.POINTER(vp), i32, vp, i32, vp, i64, vp, C.POINTER(vp), vp, vp,
                                      vp]
     _lib = L
@@ -322,39 +322,41 @@ class Context:
                                              _stream_handle(stream)))
 
     # -- (6) batched nodes / traversal ---------------------------------------
-    def plf_batch_dev(self, nodes, EV, n, wgt=None, stream=None):
+    def plf_batch_dev(self, nodes, EV, n, wgt=None, stream=None, states=4):
         """nodes: sequence of dicts with torch tensors x1, x2, x3, left, right and
         optional scaler (uint8[n]), scaler_sum (int64[1]); all one float dtype,
         all sharing EV, n (sites) and wgt."""
         import torch
 
         dt = EV.dtype
+        V, M = 4 * states, 4 * states * states
         arr = (Node * len(nodes))()
         ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         for i, nd in enumerate(nodes):
             for k in ("x1", "x2", "x3"):
                 t = nd[k]
-                if t.dtype != dt or t.numel() < 16 * n or not t.is_contiguous():
-                    raise PlfxError(ERR_INVALID, f"node {i}: {k} must be contiguous {dt} >= 16*n")
+                if t.dtype != dt or t.numel() < V * n or not t.is_contiguous():
+                    raise PlfxError(ERR_INVALID, f"node {i}: {k} must be contiguous {dt} >= {V}*n")
             for k in ("left", "right"):
-                if nd[k].dtype != dt or nd[k].numel() < 64:
-                    raise PlfxError(ERR_INVALID, f"node {i}: {k} needs 64 values")
+                if nd[k].dtype != dt or nd[k].numel() < M:
+                    raise PlfxError(ERR_INVALID, f"node {i}: {k} needs {M} values")
             arr[i] = Node(ptr(nd["x1"]), ptr(nd["x2"]), ptr(nd["x3"]), ptr(nd["left"]),
                           ptr(nd["right"]), ptr(nd.get("scaler")), ptr(nd.get("scaler_sum")))
         if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n):
             raise PlfxError(ERR_INVALID, "wgt must be int32 with >= n elements")
-        self._check(self._L.plfx_plf_batch_dev(self.h, F32 if dt == torch.float32 else F64, 4, arr,
+        self._check(self._L.plfx_plf_batch_dev(self.h, F32 if dt == torch.float32 else F64, states, arr,
                                                len(nodes), C.c_void_p(EV.data_ptr()), int(n),
                                                C.c_void_p(ptr(wgt)), _stream_handle(stream)))
 
     def traverse(self, ops, clv, pmats, EV, n, wgt=None, scalers=None, scaler_sums=None,
-                 stream=None, tips=None, tipvec=None):
+                 stream=None, tips=None, tipvec=None, states=4, fma=False):
         """Run a post-order traversal descriptor.  ops: (nops, 4) int array of
         [parent, child1, child2, pmat]; clv: list of torch CLV tensors (slots;
         None where the slot is a tip); pmats: tensor of 2*npmat matrices (64
         values each for DNA); tips: optional list (per slot) of uint8 state-code
         tensors or None (plfx.h section 8); tipvec: optional device table of
-        16 x 4 tip vectors (dtype of the CLVs)."""
+        16 x 4 tip vectors (dtype of the CLVs); states 4 or 20 (protein: no
+        tips), fma: PLFX_FMA for protein nodes."""
         import torch
 
         ops = np.ascontiguousarray(ops, dtype=np.int32).reshape(-1, 4)
@@ -363,16 +365,17 @@ class Context:
         nslots = len(clv)
         if tips is not None and len(tips) != nslots:
             raise PlfxError(ERR_INVALID, "tips must have one entry per slot")
+        V, M = 4 * states, 4 * states * states
         for s_, t in enumerate(clv):
             tip = None if tips is None else tips[s_]
             if tip is not None:
                 if tip.dtype != torch.uint8 or tip.numel() < n or not tip.is_contiguous():
                     raise PlfxError(ERR_INVALID, f"tip slot {s_}: contiguous uint8 >= n required")
                 continue
-            if t is None or t.dtype != dt or t.numel() < 16 * n or not t.is_contiguous():
-                raise PlfxError(ERR_INVALID, "every CLV slot must be contiguous, same dtype, >= 16*n")
-        if pmats.dtype != dt or pmats.numel() % 128:
-            raise PlfxError(ERR_INVALID, "pmats must hold whole (left, right) pairs of 64 values")
+            if t is None or t.dtype != dt or t.numel() < V * n or not t.is_contiguous():
+                raise PlfxError(ERR_INVALID, f"every CLV slot must be contiguous, same dtype, >= {V}*n")
+        if pmats.dtype != dt or pmats.numel() % (2 * M):
+            raise PlfxError(ERR_INVALID, f"pmats must hold whole (left, right) pairs of {M} values")
         if scaler_sums is not None and (scaler_sums.dtype != torch.int64 or scaler_sums.numel() < nops):
             raise PlfxError(ERR_INVALID, "scaler_sums must be int64 with >= nops entries")
         top = (TravOp * nops)(*[TravOp(*map(int, r)) for r in ops])
@@ -384,8 +387,9 @@ class Context:
         if scalers is not None:
             sc = (C.c_void_p * nops)(*[None if t is None else t.data_ptr() for t in scalers])
         self._check(self._L.plfx_traverse_tips(
-            self.h, F32 if dt == torch.float32 else F64, 4, top, nops, slots, tp, nslots,
-            C.c_void_p(pmats.data_ptr()), pmats.numel() // 128, C.c_void_p(EV.data_ptr()), int(n),
+            self.h, F32 if dt == torch.float32 else F64, states, FMA if fma else EXACT, top, nops,
+            slots, tp, nslots, C.c_void_p(pmats.data_ptr()), pmats.numel() // (2 * M),
+            C.c_void_p(EV.data_ptr()), int(n),
             C.c_void_p(None if wgt is None else wgt.data_ptr()), sc,
             C.c_void_p(None if scaler_sums is None else scaler_sums.data_ptr()),
             self._tipvec(tipvec, dt), _stream_handle(stream)))

@@ -159,7 +159,8 @@ typedef struct {
 
 /* `count` independent nodes sharing EV, n and wgt; all device pointers, the
  * `nodes` array itself is host memory (it travels in the kernel arguments, 32
- * nodes per launch: graph-capture safe).  states must be 4 (DNA). */
+ * nodes per launch: graph-capture safe).  states 4 (DNA) or 20 (protein, one
+ * launch per node, exact mode). */
 int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *nodes, int count,
                        const void *EV, int64_t n, const int32_t *wgt, void *stream);
 
@@ -201,12 +202,16 @@ int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void 
                       const void *left, const void *right, const int32_t *wgt, uint8_t *scaler,
                       int64_t *scaler_sum, const void *tipvec, void *stream);
 
-/* plfx_traverse with tip slots: tips is a host array of nslots device pointers
- * (or NULL = no tips); a slot with tips[s] != NULL is a tip (clv[s] is not
- * read) and may not be an op's parent.  Each level is issued as up to three
- * batched launches (tip/tip, tip/inner, inner/inner). */
-int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
-                       void *const *clv, const uint8_t *const *tips, int nslots, const void *pmats,
+/* plfx_traverse with tip slots and flags: tips is a host array of nslots device
+ * pointers (or NULL = no tips); a slot with tips[s] != NULL is a tip (clv[s] is
+ * not read) and may not be an op's parent (tips: DNA only).  Each level is
+ * issued as up to three batched launches (tip/tip, tip/inner, inner/inner),
+ * level pairs fused where possible.  states 4 or 20; flags as
+ * plfx_plf_dev_gen (PLFX_FMA: protein nodes on the f64 matrix cores; DNA is
+ * always exact).  plfx_traverse == flags PLFX_EXACT, no tips, no tipvec. */
+int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const plfx_trav_op *ops,
+                       int nops, void *const *clv, const uint8_t *const *tips, int nslots,
+                       const void *pmats,
                        int npmats, const void *EV, int64_t n, const int32_t *wgt,
                        uint8_t *const *scalers, int64_t *scaler_sums, const void *tipvec,
                        void *stream);

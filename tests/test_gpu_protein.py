@@ -98,3 +98,98 @@ def test_protein_full_size_256k(ctx, oracle):
     torch.cuda.synchronize()
     exp = oracle.root_lnl(S, CAT, np.abs(x3), n, freq=freq, wgt=w)
     assert abs(float(out.item()) - exp) <= 1e-12 * abs(exp)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_protein_traverse_exact(ctx, oracle, dtype):
+    """Protein traversal (states=20, one launch per node): CLVs, scaler bytes
+    and sums bit-exact vs the oracle's sequential traversal; the FMA-mode
+    traversal's root lnL within 1e-10 of the exact one (lnL is invariant to
+    where the rescales happen)."""
+    import torch
+
+    n, ntips = 513, 8
+    rng = np.random.default_rng(3)
+    ops = oracle.balanced_tree_ops(ntips)
+    nops, nslots = ops.shape[0], ntips + ops.shape[0]
+    tips = [rng.random(V * n).astype(dtype) for _ in range(ntips)]
+    pm = (rng.random(nops * 2 * CAT * S * S) * 0.01).astype(dtype)  # deep levels underflow
+    EV = (rng.random(S * S) * 0.01).astype(dtype)
+    wgt = rng.integers(1, 4, n).astype(np.int32)
+    host = [t.copy() for t in tips] + [np.zeros(V * n, dtype) for _ in range(nops)]
+    esums, escal = oracle.traverse(S, CAT, ops, host, pm, EV, n, wgt, want_scalers=True)
+    assert esums.sum() > 0
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    lnl = {}
+    for fma in (False, True) if dtype == np.float64 else (False,):
+        clv = [dev(t) for t in tips] + [torch.zeros(V * n, dtype=tt, device="cuda") for _ in range(nops)]
+        sums = torch.zeros(nops, dtype=torch.int64, device="cuda")
+        scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+        ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, states=S, fma=fma)
+        out = torch.zeros(1, dtype=torch.float64, device="cuda")
+        ctx.root_lnl(clv[-1], n, out, wgt=dev(wgt), scaler_sums=sums, states=S)
+        torch.cuda.synchronize()
+        lnl[fma] = float(out.item())
+        if not fma:
+            for s in range(ntips, nslots):
+                assert np.array_equal(bits(clv[s].cpu().numpy()), bits(host[s])), s
+            assert np.array_equal(sums.cpu().numpy(), esums)
+            for j in range(nops):
+                assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+    if True in lnl:
+        assert abs(lnl[True] - lnl[False]) <= 1e-10 * abs(lnl[False])
+
+
+def test_protein_model_pipeline_lnl(ctx, oracle):
+    """A 20-state reversible model end to end: eigensystem -> device P
+    matrices (states=20) -> protein traversal -> root lnL, against an
+    independent numpy pruning with scipy.linalg.expm (1e-10 relative)."""
+    import plfx
+    import torch
+    from scipy.linalg import expm
+
+    n, ntips = 400, 8
+    rng = np.random.default_rng(20)
+    exch = rng.random(S * (S - 1) // 2) * 2 + 0.1
+    freqs = rng.random(S) + 0.2
+    pi = freqs / freqs.sum()
+    R = np.zeros((S, S))
+    R[np.triu_indices(S, 1)] = exch
+    R = R + R.T
+    Q = R * pi[None, :]
+    np.fill_diagonal(Q, -Q.sum(axis=1))
+    Q /= -(pi * np.diag(Q)).sum()
+    e = plfx.model_eigen(exch, freqs)
+    rates = plfx.gamma_rates(0.8, CAT)
+    ops = oracle.balanced_tree_ops(ntips)
+    nops = ops.shape[0]
+    blen = rng.random(2 * nops) * 0.4 + 0.02
+    obs = [rng.integers(0, S, n) for _ in range(ntips)]
+    tipx = []
+    for o in obs:  # one observed amino acid per site: indicator in every category
+        x = np.zeros((n, CAT, S))
+        x[np.arange(n), :, o] = 1.0
+        tipx.append(x)
+    clvs = {t: (tipx[t], np.zeros(n)) for t in range(ntips)}
+    for p, c1, c2, m in ops:
+        out = None
+        for child, bl in ((c1, blen[2 * m]), (c2, blen[2 * m + 1])):
+            u = np.stack([clvs[child][0][:, c, :] @ expm(Q * rates[c] * bl).T for c in range(CAT)], axis=1)
+            out = u if out is None else out * u
+        mx = out.reshape(n, -1).max(axis=1)
+        clvs[p] = (out / mx[:, None, None], clvs[c1][1] + clvs[c2][1] + np.log(mx))
+    root, logs = clvs[ops[-1][0]]
+    exp_lnl = float(np.sum(np.log(np.einsum("c,ncs,s->n", np.full(CAT, 1 / CAT), root, pi)) + logs))
+
+    pm = torch.empty(2 * nops * CAT * S * S, dtype=torch.float64, device="cuda")
+    ctx.pmatrix(dev(e), dev(rates), dev(blen), pm, states=S, convention=plfx.PMAT_STATE)
+    EVd = dev(plfx.model_ev(e, S, plfx.PMAT_STATE))
+    clv = [dev(x.reshape(-1)) for x in tipx] + [torch.zeros(V * n, dtype=torch.float64, device="cuda")
+                                                for _ in range(nops)]
+    sums = torch.zeros(nops, dtype=torch.int64, device="cuda")
+    ctx.traverse(ops, clv, pm, EVd, n, None, None, sums, states=S, fma=True)
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    ctx.root_lnl(clv[-1], n, out, freq=dev(pi), scaler_sums=sums, states=S)
+    torch.cuda.synchronize()
+    got = float(out.item())
+    assert abs(got - exp_lnl) <= 1e-10 * abs(exp_lnl), (got, exp_lnl)
