@@ -231,3 +231,75 @@ def test_fused_level_pairs_match_unfused(ctx, oracle, coded, dtype, monkeypatch)
     assert np.array_equal(fused[1], esums) and np.array_equal(plain[1], esums)
     for j in range(nops):
         assert np.array_equal(fused[2][j], escal[j]) and np.array_equal(plain[2][j], escal[j]), j
+
+
+def _tree_driver_expected(oracle, taxa, n, seed, alpha=0.5):
+    """Re-derive plfx_tree's inputs (std::mt19937 + uniform_real_distribution,
+    restated by the oracle) and its GTR+G4 lnL by an independent numpy pruning
+    with scipy.linalg.expm."""
+    import plfx
+    from scipy.linalg import expm
+
+    nops = taxa - 1
+    _, u = oracle.mt_draws(seed, 2 * nops + 2 * taxa * n + 16)
+    blen = 0.01 + 0.3 * u[:2 * nops]
+    k = 2 * nops
+    codes = np.empty((taxa, n), np.uint8)
+    for t in range(taxa):
+        for i in range(n):
+            if u[k] < 0.05:
+                codes[t, i] = 1 + int(u[k + 1] * 15)
+            else:
+                codes[t, i] = (1, 2, 4, 8)[int(u[k + 1] * 4) & 3]
+            k += 2
+    exch = np.array([1.2, 3.9, 0.8, 1.1, 4.6, 1.0])
+    freqs = np.array([0.31, 0.19, 0.22, 0.28])
+    pi = freqs / freqs.sum()
+    R = np.zeros((4, 4))
+    R[np.triu_indices(4, 1)] = exch
+    R = R + R.T
+    Q = R * pi[None, :]
+    np.fill_diagonal(Q, -Q.sum(axis=1))
+    Q /= -(pi * np.diag(Q)).sum()
+    rates = plfx.gamma_rates(alpha, 4)
+    ops = oracle.balanced_tree_ops(taxa)
+    clvs = {t: (oracle.expand_tips(codes[t]).reshape(n, 4, 4), np.zeros(n)) for t in range(taxa)}
+    for p, c1, c2, m in ops:
+        out = None
+        for child, bl in ((c1, blen[2 * m]), (c2, blen[2 * m + 1])):
+            x = clvs[child][0]
+            uu = np.stack([x[:, c, :] @ expm(Q * rates[c] * bl).T for c in range(4)], axis=1)
+            out = uu if out is None else out * uu
+        mx = out.reshape(n, -1).max(axis=1)
+        clvs[p] = (out / mx[:, None, None], clvs[c1][1] + clvs[c2][1] + np.log(mx))
+    root, logs = clvs[ops[-1][0]]
+    return float(np.sum(np.log(np.einsum("c,ncs,s->n", np.full(4, 0.25), root, pi)) + logs))
+
+
+def test_tree_driver_end_to_end(oracle):
+    """The C++ tree driver (host/plfx_tree.cpp: model -> device P -> fused
+    traversal -> root lnL): its lnL equals an independent numpy pruning of the
+    same inputs within 1e-10; dense tips, coded tips and PLFX_FUSE=0 give the
+    bit-identical lnL; f32 within 1e-4."""
+    import os
+    import subprocess
+    from pathlib import Path
+
+    exe = Path(__file__).resolve().parents[1] / "amd-versal-phylogenetic-likelihood-function_amd" / "build" / "plfx_tree"
+    taxa, n, seed = 16, 3000, 11
+
+    def lnl(*extra, env=None):
+        r = subprocess.run([str(exe), str(taxa), str(n), "2", "--seed", str(seed), *extra],
+                           capture_output=True, text=True, timeout=120,
+                           env={**os.environ, **(env or {})})
+        assert r.returncode == 0, r.stderr
+        line = [x for x in r.stdout.splitlines() if x.startswith("lnL = ")][-1]
+        return line.split("= ")[1]
+
+    expect = _tree_driver_expected(oracle, taxa, n, seed)
+    dense, coded = lnl(), lnl("--tips")
+    plain = lnl("--tips", env={"PLFX_FUSE": "0"})
+    assert dense == coded == plain
+    assert abs(float(dense) - expect) <= 1e-10 * abs(expect)
+    f32 = float(lnl("--dtype", "f32", "--tips"))
+    assert abs(f32 - expect) <= 1e-4 * abs(expect)
