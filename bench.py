@@ -140,6 +140,10 @@ def cpu_baseline(n_sites, seconds):
         rt, _ = timed(lambda: O.ref_plf(f["x1"], f["x2"], f["EV"], f["left"], f["right"], f["wgt"]),
                       1 << 16)
         res["reference_plf_O0_f32_1thread"] = rt
+        if O.ref_lib("O3") is not None:  # the same sources at -O3 (no -march, no fast-math)
+            r3, _ = timed(lambda: O.ref_plf(f["x1"], f["x2"], f["EV"], f["left"], f["right"],
+                                            f["wgt"], opt="O3"), 1 << 16)
+            res["reference_plf_O3_f32_1thread"] = r3
     return res
 
 
