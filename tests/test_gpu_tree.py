@@ -303,3 +303,62 @@ def test_tree_driver_end_to_end(oracle):
     assert abs(float(dense) - expect) <= 1e-10 * abs(expect)
     f32 = float(lnl("--dtype", "f32", "--tips"))
     assert abs(f32 - expect) <= 1e-4 * abs(expect)
+
+
+def _random_tree_ops(rng, ntips, recycle):
+    """Random topology: merge two random pool members until one is left.
+    recycle=True reuses the slots of consumed inner nodes for later parents
+    (write-after-read / write-after-write hazards for the scheduler)."""
+    pool = list(range(ntips))
+    free, nxt, ops = [], ntips, []
+    while len(pool) > 1:
+        i, j = sorted(rng.choice(len(pool), 2, replace=False))
+        a, b = pool[j], pool[i]
+        pool.pop(j)
+        pool.pop(i)
+        if recycle and free:
+            p = free.pop(0)
+        else:
+            p, nxt = nxt, nxt + 1
+        ops.append((p, a, b, len(ops)))
+        for c in (a, b):
+            if c >= ntips and recycle:
+                free.append(c)
+        pool.append(p)
+    return np.array(ops, np.int32), nxt
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_random_trees_match_oracle(ctx, oracle, seed, dtype):
+    """Random topologies (with and without slot recycling) and a random mix of
+    coded / dense tips: the scheduled (levels + fused pairs) traversal equals
+    the oracle's sequential one bit for bit, scaler sums included."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    ntips, n = 24, 1537
+    ops, nslots = _random_tree_ops(rng, ntips, recycle=bool(seed % 2))
+    nops = ops.shape[0]
+    coded = rng.random(ntips) < 0.6
+    codes = [oracle.random_tip_codes(rng, n, 0.2) for _ in range(ntips)]
+    dense = [rng.random(16 * n).astype(dtype) for _ in range(ntips)]
+    pm = (rng.random(nops * 128) * 0.3).astype(dtype)
+    EV = (rng.random(16) * 0.3).astype(dtype)
+    wgt = rng.integers(1, 4, n).astype(np.int32)
+    host = [oracle.expand_tips(codes[t], dtype) if coded[t] else dense[t].copy() for t in range(ntips)]
+    host += [np.zeros(16 * n, dtype) for _ in range(nslots - ntips)]
+    esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    clv = [None if coded[t] else dev(dense[t]) for t in range(ntips)]
+    clv += [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nslots - ntips)]
+    tips = [dev(codes[t]) if coded[t] else None for t in range(ntips)] + [None] * (nslots - ntips)
+    sums = torch.zeros(nops, dtype=torch.int64, device="cuda")
+    scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+    ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips)
+    torch.cuda.synchronize()
+    for s in range(ntips, nslots):
+        assert np.array_equal(bits(clv[s].cpu().numpy()), bits(host[s])), s
+    assert np.array_equal(sums.cpu().numpy(), esums)
+    for j in range(nops):
+        assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
