@@ -1,6 +1,6 @@
 // Probe of v_mfma_f64_4x4x4_4b_f64 on gfx950 (not product code): operand and
-// result lane maps, numerics against a k-ordered fma chain, and issue cost
-// against v_mfma_f64_16x16x4_f64.
+// result lane maps and issue cost against v_mfma_f64_16x16x4_f64 (numerics
+// not probed here).
 //   hipcc --offload-arch=gfx950 -O3 tools/probes/mfma_f64_4x4x4.hip -o build/probe_4x4
 //
 // Measured on MI355X (profiles/r01_probe_mfma_f64_4x4x4.log), block b = 0..3:
