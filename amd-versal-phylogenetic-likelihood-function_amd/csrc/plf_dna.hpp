@@ -906,5 +906,189 @@ plf_dna_cat_triple_kernel(const TripleBatch tb, const T *__restrict__ EV,
                       d.ssp);
 }
 
+// ---------------------------------------------------------------------------
+// Fused three-level subtree ("septet", f64 lane-pair mapping): four nodes A_i
+// over eight children g, their two parents B_1 = (A_1, A_2), B_2 = (A_3, A_4)
+// and the root R = (B_1, B_2) in one pass: 8 child reads + 7 writes per site
+// (15 CLV transfers for 7 nodes, 2.14 per node; a triple moves 7 for 3).  The
+// 7 nodes' matrices (128 values each) sit in LDS and every lane reads its 16
+// per node just in time (registers could not hold 7 x 16 doubles).  Results
+// are bit-identical to seven separate updates.  kTips as the triple kernel,
+// for the A level: 1 = g_1, g_3, g_5, g_7 tips; 2 = all eight.
+struct SeptetDesc {
+  const void *g[8];
+  void *x[7];               // A1..A4, B1, B2, R
+  const double *mat[14];    // left, right of A1..A4, B1, B2, R
+  uint8_t *sc[7];
+  int64_t *ss[7];
+};
+constexpr int kMaxSeptets = 8;
+struct SeptetBatch {
+  SeptetDesc d[kMaxSeptets];
+};
+
+// the lane's P rows of one node from its LDS image (left 64 | right 64)
+__device__ __forceinline__ void pair_mats_lds(const double *m, int c, int h, PairMats &M) {
+  const f64x2 *L = reinterpret_cast<const f64x2 *>(m + c * 16 + 8 * h);
+  const f64x2 *R = reinterpret_cast<const f64x2 *>(m + 64 + c * 16 + 8 * h);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const f64x2 a = L[i], b = R[i];
+    M.PL[i >> 1][2 * (i & 1)] = a.x;
+    M.PL[i >> 1][2 * (i & 1) + 1] = a.y;
+    M.PR[i >> 1][2 * (i & 1)] = b.x;
+    M.PR[i >> 1][2 * (i & 1) + 1] = b.y;
+  }
+}
+
+__device__ inline void block_ticket_sum7(const long long (&v)[7], unsigned long long *wsu,
+                                         int64_t *const (&out)[7]) {
+  __shared__ long long part7[7][kWavesPerBlock];
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    long long x = v[q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if ((threadIdx.x & 63) == 0) part7[q][threadIdx.x >> 6] = x;
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= 7) return;
+  long long tot = 0;
+#pragma unroll
+  for (int i = 0; i < kWavesPerBlock; i++) tot += part7[t][i];
+  ticket_publish(tot, wsu + (size_t)t * kWsWords, out[t]);
+}
+
+// kLds: re-read the matrices from LDS on every trip (an opaque zero offset
+// stops the compiler hoisting the 224 loop-invariant values into registers),
+// trading LDS traffic for occupancy.  U: 8-site blocks per trip (one matrix
+// read serves all U).  kPf: issue the next trip's loads before this trip's
+// arithmetic (software pipelining; twice the input registers).
+template <bool kSum, int kMinWaves, bool NTL, int kTips, bool kLds = true, int U = 1,
+          bool kPf = false>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
+                          const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
+                          const double *__restrict__ tipvec) {
+  constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
+  const SeptetDesc &d = sb.d[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 1, c = (lane >> 1) & 3, g = lane >> 3, sh = lane & 56;
+  __shared__ double mats[7][128];
+  // tip tables: [i] = A_i's left (g_{2i-1}), [4 + i] = A_i's right (g_{2i})
+  __shared__ double tab[T2 ? 8 : (T1 ? 4 : 1)][T1 ? 256 : 1];
+  for (int e = threadIdx.x; e < 7 * 128; e += kBlock) {
+    const int node = e >> 7, k = e & 127;
+    mats[node][k] = d.mat[2 * node + (k >> 6)][k & 63];
+  }
+  if constexpr (T1) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) build_tip_table<double>(d.mat[2 * i], tipvec, tab[i]);
+  }
+  if constexpr (T2) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) build_tip_table<double>(d.mat[2 * i + 1], tipvec, tab[4 + i]);
+  }
+  __syncthreads();
+  const int trow = c * 64 + 2 * h;
+  double E[4][2];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int t = 0; t < 2; t++) E[k][t] = EV[4 * k + 2 * h + t];
+  const double m = Num<double>::minlik();
+
+  long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 8 * U;
+  struct Trip {
+    f64x2 v[U][8];
+    int k8[U][8], w[U];
+  };
+  auto fetch = [&](int64_t base, Trip &t) {  // all loads of one trip
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+      const int64_t site0 = base + 8 * j;
+      const int64_t rec = site0 * 8 + lane;  // f64x2 index of this lane's pair (8 per site)
+      t.w[j] = 0;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        t.v[j][q] = f64x2{0.0, 0.0};
+        t.k8[j][q] = 0;
+      }
+      if (site0 + g < n) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const bool tip = (q & 1) ? T2 : T1;
+          if (tip) t.k8[j][q] = ((const uint8_t *)d.g[q])[site0 + g] & 15;
+          else t.v[j][q] = ld16<NTL>(reinterpret_cast<const f64x2 *>(d.g[q]) + rec);
+        }
+        if (kSum) t.w[j] = wgt ? wgt[site0 + g] : 1;
+      }
+    }
+  };
+  Trip nxt;
+  if constexpr (kPf) fetch(wave * 8 * U, nxt);
+  for (int64_t base = wave * 8 * U; base < n; base += stride) {
+    int z = 0;
+    if constexpr (kLds) asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    const double *mz = &mats[0][0] + z;
+    Trip cur;
+    if constexpr (kPf) {  // the next trip's loads stay in flight while this one computes
+      cur = nxt;
+      if (base + stride < n) fetch(base + stride, nxt);
+    } else {
+      fetch(base, cur);
+    }
+    auto &v = cur.v;
+    auto &k8 = cur.k8;
+    auto &w = cur.w;
+    bool valid[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) valid[j] = base + 8 * j + g < n;
+    f64x2 o[U][7];
+    bool sc[U][7];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      PairMats M;
+      pair_mats_lds(mz + 128 * i, c, h, M);
+#pragma unroll
+      for (int j = 0; j < U; j++)
+        o[j][i] = pair_node<T1, T2>(v[j][2 * i], v[j][2 * i + 1],
+                                    tab[T1 ? i : 0] + trow + 4 * k8[j][2 * i],
+                                    tab[T2 ? 4 + i : 0] + trow + 4 * k8[j][2 * i + 1], M, E,
+                                    valid[j], sh, m, sc[j][i]);
+    }
+#pragma unroll
+    for (int i = 4; i < 7; i++) {  // B1 = (A1, A2), B2 = (A3, A4), R = (B1, B2)
+      PairMats M;
+      pair_mats_lds(mz + 128 * i, c, h, M);
+      const int l = 2 * (i - 4);
+#pragma unroll
+      for (int j = 0; j < U; j++)
+        o[j][i] = pair_node<false, false>(o[j][l], o[j][l + 1], nullptr, nullptr, M, E, valid[j],
+                                          sh, m, sc[j][i]);
+    }
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+      if (!valid[j]) continue;
+      const int64_t site0 = base + 8 * j;
+      const int64_t rec = site0 * 8 + lane;
+#pragma unroll
+      for (int q = 0; q < 7; q++)
+        __builtin_nontemporal_store(o[j][q], reinterpret_cast<f64x2 *>(d.x[q]) + rec);
+      if ((lane & 7) == 0) {
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+          if (d.sc[q]) d.sc[q][site0 + g] = (uint8_t)sc[j][q];
+          if (kSum && sc[j][q]) acc[q] += w[j];
+        }
+      }
+    }
+  }
+  if constexpr (kSum) block_ticket_sum7(acc, ws + (size_t)blockIdx.y * 7 * kWsWords, d.ss);
+}
+
 }  // namespace dev
 }  // namespace plfx

@@ -34,6 +34,8 @@ static_assert(kMaxBatch == dev::kMaxBatch, "batch size mismatch");
 static_assert(sizeof(NodeDescH) == sizeof(dev::NodeDesc), "node descriptor mismatch");
 static_assert(sizeof(TripleDescH) == sizeof(dev::TripleDesc), "triple descriptor mismatch");
 static_assert(kMaxTriples == dev::kMaxTriples && 3 * kMaxTriples <= kMaxBatch, "triple batch size");
+static_assert(sizeof(SeptetDescH) == sizeof(dev::SeptetDesc), "septet descriptor mismatch");
+static_assert(kMaxSeptets == dev::kMaxSeptets, "septet batch size");
 
 // Tuned on MI355X (tools/tune_plf.hip, profiles/r01_tune.log):
 // f64 lane-pair kernel, 2 x 16-site steps per trip, non-temporal CLV loads
@@ -45,6 +47,9 @@ constexpr bool kNtl64 = true;
 constexpr int kMinWaves = 1;
 constexpr int kTripleU = 1;  // fused level pairs: 16 sites per trip (tools/tune_triple.hip)
 constexpr int kTripleU32 = 2;
+// fused three-level subtrees: 2 x 8-site blocks per trip, matrices re-read from
+// LDS, next trip's loads in flight (tools/tune_septet.hip, r01_tune_septet.log)
+constexpr int kSeptetU = 2;
 
 // Co-resident 256-thread blocks of `kernel` on the current device (cached per
 // kernel instantiation by the caller).
@@ -208,7 +213,40 @@ hipError_t launch_triples32_t(const dev::TripleBatch &b, int count, const float 
   return hipGetLastError();
 }
 
+template <bool kSum, int kTips>
+hipError_t launch_septets_t(const dev::SeptetBatch &b, int count, const double *EV,
+                            const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                            hipStream_t s, const double *tipvec) {
+  static int cache = 0;
+  auto kernel = &dev::plf_dna_f64_septet_kernel<kSum, 1, kNtl64, kTips, true, kSeptetU, true>;
+  const int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 8 * kSeptetU, count,
+                            max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt,
+                     n, ws, tipvec);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_plf_dna_septets(const SeptetDescH *t, int count, const double *EV,
+                                  const int32_t *wgt, int64_t n, unsigned long long *ws,
+                                  int max_blocks, hipStream_t s, int tips, const double *tipvec) {
+  if (count < 1 || count > kMaxSeptets || tips < 0 || tips > 2) return hipErrorInvalidValue;
+  dev::SeptetBatch b{};
+  bool any_sum = false;
+  for (int i = 0; i < count; i++) {
+    __builtin_memcpy(&b.d[i], &t[i], sizeof(t[i]));
+    for (int q = 0; q < 7; q++) any_sum |= t[i].ss[q] != nullptr;
+  }
+  switch ((any_sum ? 3 : 0) + tips) {
+    case 0: return launch_septets_t<false, 0>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 1: return launch_septets_t<false, 1>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 2: return launch_septets_t<false, 2>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 3: return launch_septets_t<true, 0>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 4: return launch_septets_t<true, 1>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    default: return launch_septets_t<true, 2>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+  }
+}
 
 hipError_t launch_plf_dna_triples(int dtype, const TripleDescH *t, int count, const void *EV,
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,

@@ -23,7 +23,7 @@ struct plfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
-  bool fuse = true;                 // traverse: fused level pairs (PLFX_FUSE=0 disables)
+  int fuse = 2;  // traverse: 2 three-level subtrees + level pairs, 1 level pairs, 0 none (PLFX_FUSE)
   unsigned long long *ws = nullptr; // ticket reduction words (kMaxBatch x kWsWords u64), zero at rest
   double *lnl_partials = nullptr;   // kLnlMaxGrid doubles
   unsigned long long *lnl_ticket = nullptr;
@@ -225,8 +225,9 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
     int v = std::atoi(env);
     if (v > 0) ctx->max_blocks = v;
   }
-  if (const char *env = std::getenv("PLFX_FUSE")) ctx->fuse = std::atoi(env) != 0;
-  const size_t ws_bytes = (size_t)plfx::kMaxBatch * plfx::kWsWords * sizeof(unsigned long long);
+  if (const char *env = std::getenv("PLFX_FUSE")) ctx->fuse = std::atoi(env);
+  const size_t ws_regions = std::max(plfx::kMaxBatch, 7 * plfx::kMaxSeptets);
+  const size_t ws_bytes = ws_regions * plfx::kWsWords * sizeof(unsigned long long);
   if (hipMalloc(reinterpret_cast<void **>(&ctx->ws), ws_bytes) != hipSuccess ||
       hipMemsetAsync(ctx->ws, 0, ws_bytes, ctx->stream) != hipSuccess ||
       hipMalloc(reinterpret_cast<void **>(&ctx->lnl_partials), plfx::kLnlMaxGrid * sizeof(double)) != hipSuccess ||
@@ -459,7 +460,40 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   };
   std::vector<Triple> triples;
   std::vector<char> used(nops, 0);
-  if (ctx->fuse && states == 4) {
+  // Fused three-level subtrees (f64 DNA, plf_dna.hpp SeptetDesc): root R two
+  // levels above four ops A of one tip kind, through the two ops B that R's
+  // children were last written by; R's and the B's slots free by level L.
+  // Ordered so that a[2i], a[2i+1] are b[i]'s child1, child2 and b[0], b[1]
+  // are R's.  Tried first; the remaining ops form triples.
+  struct Septet {
+    int a[4], b[2], r, kind;
+  };
+  std::vector<Septet> septets;
+  auto fusible_pair = [&](int p, int L, int &x, int &y) {  // p's writers at level L
+    x = w1[p];
+    y = w2[p];
+    return x >= 0 && y >= 0 && x != y && !used[x] && !used[y] && !used[p] && level[x] == L &&
+           level[y] == L && level[p] == L + 1;
+  };
+  if (ctx->fuse >= 2 && states == 4 && dtype == PLFX_F64) {
+    for (int r = 0; r < nops; r++) {
+      Septet t{};
+      t.r = r;
+      const int L = level[r] - 2;
+      if (L < 0 || used[r] || pdep[r] > L) continue;
+      if (!fusible_pair(r, L + 1, t.b[0], t.b[1])) continue;
+      if (pdep[t.b[0]] > L || pdep[t.b[1]] > L) continue;
+      if (!fusible_pair(t.b[0], L, t.a[0], t.a[1]) || !fusible_pair(t.b[1], L, t.a[2], t.a[3]))
+        continue;
+      int k[4];
+      for (int i = 0; i < 4; i++) node_of(t.a[i], &k[i]);
+      if (k[1] != k[0] || k[2] != k[0] || k[3] != k[0]) continue;
+      t.kind = k[0];
+      for (int j : {t.a[0], t.a[1], t.a[2], t.a[3], t.b[0], t.b[1], r}) used[j] = 1;
+      septets.push_back(t);
+    }
+  }
+  if (ctx->fuse >= 1 && states == 4) {
     for (int p = 0; p < nops; p++) {
       const int a = w1[p], b = w2[p];
       if (a < 0 || b < 0 || a == b || used[a] || used[b] || used[p]) continue;
@@ -475,10 +509,33 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   }
   std::vector<plfx_node> batch[3];  // by number of tip children
   std::vector<plfx::TripleDescH> tb[3];
+  std::vector<plfx::SeptetDescH> sb[3];
   for (int lv = 0; lv < nlev; lv++) {
     for (int k = 0; k < 3; k++) {
       batch[k].clear();
       tb[k].clear();
+      sb[k].clear();
+    }
+    for (const Septet &t : septets) {
+      if (level[t.a[0]] != lv) continue;
+      const int id[7] = {t.a[0], t.a[1], t.a[2], t.a[3], t.b[0], t.b[1], t.r};
+      plfx::SeptetDescH d{};
+      for (int q = 0; q < 7; q++) {
+        int kq;
+        const plfx_node nd = node_of(id[q], &kq);
+        const int rc = check_node(ctx, nd, kq, n, id[q]);
+        if (rc != PLFX_OK) return rc;
+        if (q < 4) {
+          d.g[2 * q] = nd.x1;
+          d.g[2 * q + 1] = nd.x2;
+        }
+        d.x[q] = nd.x3;
+        d.mat[2 * q] = (const double *)nd.left;
+        d.mat[2 * q + 1] = (const double *)nd.right;
+        d.sc[q] = nd.scaler;
+        d.ss[q] = nd.scaler_sum;
+      }
+      sb[t.kind].push_back(d);
     }
     for (const Triple &t : triples) {
       if (level[t.a] != lv) continue;
@@ -503,6 +560,19 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
       batch[kind].push_back(nd);
     }
     for (int k = 0; k < 3; k++) {
+      for (size_t i = 0; i < sb[k].size(); i += plfx::kMaxSeptets) {
+        const int c = (int)std::min<size_t>(plfx::kMaxSeptets, sb[k].size() - i);
+        if (n == 0) {
+          for (int q = 0; q < c; q++)
+            for (int64_t *ss : sb[k][i + q].ss)
+              if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
+          continue;
+        }
+        hipError_t e = plfx::launch_plf_dna_septets(sb[k].data() + i, c, (const double *)EV, wgt,
+                                                    n, ctx->ws, ctx->max_blocks, s, k,
+                                                    (const double *)tipvec);
+        if (e != hipSuccess) return hip_fail(ctx, e, "fused three-level launch");
+      }
       for (size_t i = 0; i < tb[k].size(); i += plfx::kMaxTriples) {
         const int c = (int)std::min<size_t>(plfx::kMaxTriples, tb[k].size() - i);
         if (n == 0) {

@@ -4,7 +4,7 @@
 // around it: a GTR+Gamma4 model (plfx_model_eigen, plfx_gamma_rates), a
 // balanced tree of T taxa as a post-order descriptor, and per sweep the device
 // P matrices from the branch lengths (plfx_pmatrix), the traversal
-// (plfx_traverse_tips: tips dense or as state codes, level pairs fused) and the
+// (plfx_traverse_tips: tips dense or as state codes, subtrees fused) and the
 // root log-likelihood (plfx_root_lnl), timed with HIP events.
 //
 //   usage: plfx_tree <taxa (power of 2)> <sites> <sweeps>

@@ -85,8 +85,10 @@ def parse():
                     help="protein: fused multiply-add mode (the default; f64 runs on the matrix cores)")
     ap.add_argument("--exact", action="store_true",
                     help="protein: plf()'s separate multiply/add (bit-identical to the double loop)")
-    ap.add_argument("--no-fuse", action="store_true",
-                    help="tree64: one launch per level instead of fused level pairs (PLFX_FUSE=0)")
+    ap.add_argument("--fuse", type=int, choices=[0, 1, 2], default=2,
+                    help="tree64 schedule (PLFX_FUSE): 2 fused three-level subtrees (f64) and "
+                         "level pairs, 1 level pairs only, 0 one launch per level")
+    ap.add_argument("--no-fuse", action="store_true", help="same as --fuse 0")
     ap.add_argument("--tips", action="store_true",
                     help="tree64: tips as uint8 state codes (plfx.h section 8) instead of dense CLVs")
     ap.add_argument("--workload", choices=["node", "tree64", "nodes64", "protein"], default="node",
@@ -252,19 +254,27 @@ class Tree64Workload:
         self.sites_per_step = nops * n
         # per node: read x1, x2, write x3, read wgt (scaler sums, no bytes); + lnL read of the root.
         # With coded tips a tip child reads 1 code byte instead of a CLV.  Fused level pairs:
-        # A, B and their parent P in one pass -- 4 child reads + 3 writes + wgt.
+        # A, B and their parent P in one pass -- 4 child reads + 3 writes + wgt.  Fused
+        # three-level subtrees (f64): 7 nodes in one pass -- 8 child reads + 7 writes + wgt.
         clv_b, tip_b = 16 * esz, 1
-        self.fused = not a.no_fuse
+        leaf = tip_b if a.tips else clv_b
+        fuse = 0 if a.no_fuse else a.fuse
+        if fuse == 2 and esz == 4:
+            fuse = 1  # three-level subtrees are built for f64 only
         self.bytes_per_site = 3 * clv_b + 4
-        if self.fused:  # levels (32,16), (8,4), (2,1) as 16 + 4 + 1 triples
-            first = 4 * (tip_b if a.tips else clv_b) + 3 * clv_b + 4
+        if fuse == 2:  # levels 0-2 as 8 seven-node subtrees, levels 3-5 as one
+            self.bytes_per_step = (8 * (8 * leaf + 7 * clv_b + 4) + (15 * clv_b + 4)
+                                   + (clv_b + 4)) * n
+            sched = "fused three-level subtrees: 9 seven-node passes in 2 launches"
+        elif fuse == 1:  # levels (32,16), (8,4), (2,1) as 16 + 4 + 1 triples
+            first = 4 * leaf + 3 * clv_b + 4
             self.bytes_per_step = (16 * first + 5 * (7 * clv_b + 4) + (clv_b + 4)) * n
+            sched = "fused level pairs: 21 three-node passes in 3 launch groups"
         else:
-            first = 2 * (tip_b if a.tips else clv_b) + clv_b + 4
+            first = 2 * leaf + clv_b + 4
             self.bytes_per_step = (32 * first + 31 * (3 * clv_b + 4) + (clv_b + 4)) * n
+            sched = "6 level launches"
         tipdesc = "tips as uint8 state codes" if a.tips else "dense tip CLVs"
-        sched = ("fused level pairs: 21 three-node passes in 3 launch groups" if self.fused
-                 else "6 level launches")
         self.config = {
             "workload": f"DNA 4-state, 64-taxon balanced tree post-order sweep (63 inner nodes, "
                         f"{sched}) + root lnL, {n} sites, {a.dtype}, {tipdesc} "
@@ -405,8 +415,7 @@ WORKLOADS = {"node": NodeWorkload, "tree64": Tree64Workload, "nodes64": Nodes64W
 
 def main():
     a = parse()
-    if a.no_fuse:
-        os.environ["PLFX_FUSE"] = "0"  # read by plfx_ctx_create
+    os.environ["PLFX_FUSE"] = "0" if a.no_fuse else str(a.fuse)  # read by plfx_ctx_create
     import torch
     import torch.distributed as dist
 

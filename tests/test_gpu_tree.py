@@ -179,11 +179,12 @@ def test_tree64_full_size_window(ctx, oracle):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-@pytest.mark.parametrize("coded", [False, True])
-def test_fused_level_pairs_match_unfused(ctx, oracle, coded, dtype, monkeypatch):
-    """Traversals run fused level pairs (parent + both children in one
-    pass).  A 32-taxon tree with a caterpillar tail and mixed tip kinds: the
-    fused schedule (default context) and the level-by-level one (PLFX_FUSE=0)
+@pytest.mark.parametrize("tipmode", ["dense", "mixed", "coded", "left"])
+def test_fused_level_pairs_match_unfused(ctx, oracle, tipmode, dtype, monkeypatch):
+    """Traversals run fused three-level subtrees (f64: 7 nodes in one pass)
+    and fused level pairs (parent + both children).  A 32-taxon tree with a
+    caterpillar tail and dense, mixed, all-coded or left-coded tips: the
+    default schedule, pairs only (PLFX_FUSE=1) and level by level (PLFX_FUSE=0)
     produce identical CLVs, scaler bytes and sums, equal to the oracle."""
     import plfx
     import torch
@@ -196,7 +197,8 @@ def test_fused_level_pairs_match_unfused(ctx, oracle, coded, dtype, monkeypatch)
     ops = np.array(ops, np.int32)
     nslots, nops = 66, ops.shape[0]
     codes = [oracle.random_tip_codes(rng, n, 0.2) for _ in range(32)]
-    is_coded = [coded and t % 4 != 3 for t in range(32)]
+    is_coded = [{"dense": False, "mixed": t % 4 != 3, "coded": True, "left": t % 2 == 0}[tipmode]
+                for t in range(32)]
     dense = [rng.random(16 * n).astype(dtype) for _ in range(32)]
     pm = (rng.random(nops * 128) * 0.3).astype(dtype)
     EV = (rng.random(16) * 0.3).astype(dtype)
@@ -217,20 +219,20 @@ def test_fused_level_pairs_match_unfused(ctx, oracle, coded, dtype, monkeypatch)
         torch.cuda.synchronize()
         return clv, sums.cpu().numpy(), [x.cpu().numpy() for x in scal]
 
-    fused = run(ctx)
-    monkeypatch.setenv("PLFX_FUSE", "0")
-    plain_ctx = plfx.Context(0)
-    try:
-        plain = run(plain_ctx)
-    finally:
-        plain_ctx.close()
-    for s in range(32, nslots):
-        f = fused[0][s].cpu().numpy()
-        assert np.array_equal(bits(f), bits(host[s])), s
-        assert np.array_equal(bits(f), bits(plain[0][s].cpu().numpy())), s
-    assert np.array_equal(fused[1], esums) and np.array_equal(plain[1], esums)
-    for j in range(nops):
-        assert np.array_equal(fused[2][j], escal[j]) and np.array_equal(plain[2][j], escal[j]), j
+    results = [run(ctx)]
+    for level in ("1", "0"):
+        monkeypatch.setenv("PLFX_FUSE", level)
+        c = plfx.Context(0)
+        try:
+            results.append(run(c))
+        finally:
+            c.close()
+    for r in results:
+        for s in range(32, nslots):
+            assert np.array_equal(bits(r[0][s].cpu().numpy()), bits(host[s])), s
+        assert np.array_equal(r[1], esums)
+        for j in range(nops):
+            assert np.array_equal(r[2][j], escal[j]), j
 
 
 def _tree_driver_expected(oracle, taxa, n, seed, alpha=0.5):
@@ -298,8 +300,9 @@ def test_tree_driver_end_to_end(oracle):
 
     expect = _tree_driver_expected(oracle, taxa, n, seed)
     dense, coded = lnl(), lnl("--tips")
+    pairs = lnl("--tips", env={"PLFX_FUSE": "1"})
     plain = lnl("--tips", env={"PLFX_FUSE": "0"})
-    assert dense == coded == plain
+    assert dense == coded == pairs == plain
     assert abs(float(dense) - expect) <= 1e-10 * abs(expect)
     f32 = float(lnl("--dtype", "f32", "--tips"))
     assert abs(f32 - expect) <= 1e-4 * abs(expect)
