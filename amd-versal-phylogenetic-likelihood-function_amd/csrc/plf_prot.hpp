@@ -439,11 +439,21 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
 //   X3^T[l][site]  = EV^T[l][k] . p[k][site]   (the accumulators of the first
 //                                               product ARE the B fragments:
 //                                               k-step s = tile s>>2, reg s&3)
-// A fragments (P rows, EV columns, zero-padded to 32) stay in VGPRs for the
-// whole kernel; B fragments (X^T) come from the LDS tile, conflict-free.
+// A fragments (P rows, EV columns) stay in VGPRs for the whole kernel; B
+// fragments (X^T) come from the LDS tile, conflict-free.
+// kMix4: rows 16..19 of each product (M = 20 = 16 + 4) on v_mfma_f64_4x4x4_4b_f64
+// -- four 4x4x4 blocks = the 16 sites, 20 cycles -- instead of a zero-padded
+// second 16x16x4 tile (64 cycles): 420 instead of 640 matrix-core cycles per
+// product and sub-tile.  Its operand maps make the two forms interchangeable
+// (A lane 16k+4b+i, B lane 16k+4b+j, D lane 16i+4b+j: the B fragment is the
+// same LDS value, and D lands as row 16 + lane/16 of site lane%16 -- exactly
+// the k-step-4 B fragment of the back-transform), and it too is bit-for-bit a
+// k-ordered fma chain (tools/probes/mfma_f64_4x4x4_numerics.hip).
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-template <bool kSum, int kMinWaves = 2, bool kPrefetch = true>
+// kAblate (tuning only, tools/tune_prot.hip): 0 = the kernel; 1 = no matrix-core
+// work (VALU stand-ins keep the LDS reads); 2 = no HBM loads or stores.
+template <bool kSum, int kMinWaves = 2, bool kPrefetch = true, int kAblate = 0, bool kMix4 = true>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                      double *__restrict__ x3, const double *__restrict__ EV,
@@ -457,12 +467,13 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   const int lane = threadIdx.x & 63;
   const int lo16 = lane & 15, g = lane >> 4;
   // A fragments: [mt][s] -> lane holds M[row = 16mt + lo16][col = 4s + g]
+  // (kMix4: [1][s] -> M[row = 16 + lane%4][col = 4s + g], the 4x4x4_4b form)
   double AL[2][5], AR[2][5], AE[2][5];
 #pragma unroll
   for (int mt = 0; mt < 2; mt++)
 #pragma unroll
     for (int st = 0; st < 5; st++) {
-      const int row = 16 * mt + lo16, col = 4 * st + g;
+      const int row = (kMix4 && mt == 1) ? 16 + (lane & 3) : 16 * mt + lo16, col = 4 * st + g;
       AL[mt][st] = row < S ? left[c * S * S + row * S + col] : 0.0;   // P_L[k=row][l=col]
       AR[mt][st] = row < S ? right[c * S * S + row * S + col] : 0.0;
       AE[mt][st] = row < S ? EV[col * S + row] : 0.0;                // EV^T[l=row][k=col]
@@ -477,14 +488,16 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   // one is multiplied (x2 during phase 1, the next trip's x1 during phase 2)
   f64x2 pf[PT::kChunks / kBlock];
   const int64_t stride = (int64_t)gridDim.x * 64;
-  if constexpr (kPrefetch)
+  if constexpr (kAblate == 2)
+    for (auto &q : pf) q = f64x2{1.0, 1.0};
+  if constexpr (kPrefetch && kAblate != 2)
     if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(x1, (int64_t)blockIdx.x * 64, n, pf);
   for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
     f64x4 P[4][2];  // per sub-tile: U_L^T, then p = U_L^T * U_R^T
     if constexpr (kPrefetch) {
       tile_put<double>(tile, pf);
       __syncthreads();
-      tile_fetch<double>(x2, base, n, pf);
+      if constexpr (kAblate != 2) tile_fetch<double>(x2, base, n, pf);
     } else {
       tile_load<double>(x1, base, n, tile);
       __syncthreads();
@@ -496,7 +509,11 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       for (int mt = 0; mt < 2; mt++) {
         f64x4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int st = 0; st < 5; st++) u = __builtin_amdgcn_mfma_f64_16x16x4f64(AL[mt][st], xr[4 * st], u, 0, 0, 0);
+        for (int st = 0; st < 5; st++) {
+          if constexpr (kAblate == 1) u[st & 3] += xr[4 * st] * AL[mt][st];
+          else if (kMix4 && mt == 1) u[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(AL[1][st], xr[4 * st], u[0], 0, 0, 0);
+          else u = __builtin_amdgcn_mfma_f64_16x16x4f64(AL[mt][st], xr[4 * st], u, 0, 0, 0);
+        }
         P[t][mt] = u;
       }
     }
@@ -504,7 +521,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
     if constexpr (kPrefetch) {
       tile_put<double>(tile, pf);
       __syncthreads();
-      if (base + stride < n) tile_fetch<double>(x1, base + stride, n, pf);
+      if (kAblate != 2 && base + stride < n) tile_fetch<double>(x1, base + stride, n, pf);
     } else {
       tile_load<double>(x2, base, n, tile);
       __syncthreads();
@@ -516,7 +533,11 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       for (int mt = 0; mt < 2; mt++) {
         f64x4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int st = 0; st < 5; st++) u = __builtin_amdgcn_mfma_f64_16x16x4f64(AR[mt][st], xr[4 * st], u, 0, 0, 0);
+        for (int st = 0; st < 5; st++) {
+          if constexpr (kAblate == 1) u[st & 3] += xr[4 * st] * AR[mt][st];
+          else if (kMix4 && mt == 1) u[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(AR[1][st], xr[4 * st], u[0], 0, 0, 0);
+          else u = __builtin_amdgcn_mfma_f64_16x16x4f64(AR[mt][st], xr[4 * st], u, 0, 0, 0);
+        }
         P[t][mt] = P[t][mt] * u;  // prod[k] = umpL[k] * umpR[k]
       }
     }
@@ -529,8 +550,14 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       f64x4 X0 = {0.0, 0.0, 0.0, 0.0}, X1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int st = 0; st < 5; st++) {
-        X0 = __builtin_amdgcn_mfma_f64_16x16x4f64(AE[0][st], P[t][st >> 2][st & 3], X0, 0, 0, 0);
-        X1 = __builtin_amdgcn_mfma_f64_16x16x4f64(AE[1][st], P[t][st >> 2][st & 3], X1, 0, 0, 0);
+        if constexpr (kAblate == 1) {
+          X0[st & 3] += AE[0][st] * P[t][st >> 2][st & 3];
+          X1[st & 3] += AE[1][st] * P[t][st >> 2][st & 3];
+        } else {
+          X0 = __builtin_amdgcn_mfma_f64_16x16x4f64(AE[0][st], P[t][st >> 2][st & 3], X0, 0, 0, 0);
+          if constexpr (kMix4) X1[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(AE[1][st], P[t][st >> 2][st & 3], X1[0], 0, 0, 0);
+          else X1 = __builtin_amdgcn_mfma_f64_16x16x4f64(AE[1][st], P[t][st >> 2][st & 3], X1, 0, 0, 0);
+        }
       }
       const bool small = (__builtin_fabs(X0[0]) < m) && (__builtin_fabs(X0[1]) < m) &&
                          (__builtin_fabs(X0[2]) < m) && (__builtin_fabs(X0[3]) < m) &&
@@ -566,7 +593,12 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
         v[i] = tile[sl * PT::kStride + q];
         if ((all >> sl) & 1ull) v[i] = v[i] * Num<double>::two32();
       }
-      if (base + 64 <= n) {
+      if (kAblate == 2) {
+        f64x2 t = v[0];
+#pragma unroll
+        for (int i = 1; i < K; i++) t += v[i];
+        if (t.x == -1.25) dst[threadIdx.x] = t;  // keeps the LDS reads alive
+      } else if (base + 64 <= n) {
 #pragma unroll
         for (int i = 0; i < K; i++) __builtin_nontemporal_store(v[i], dst + threadIdx.x + i * kBlock);
       } else {

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <string>
@@ -44,7 +45,13 @@ int main(int argc, char **argv) {
   double *EV, *L, *Rm; unsigned long long *ws;
   CK(hipMalloc(&EV, 400 * 8)); CK(hipMalloc(&L, 1600 * 8)); CK(hipMalloc(&Rm, 1600 * 8));
   CK(hipMalloc(&ws, kWsWords * 8)); CK(hipMemset(ws, 0, kWsWords * 8));
-  fill<<<8, 64>>>(EV, 400, 7, 1.0, 1); fill<<<32, 64>>>(L, 1600, 8, 1.0, 1); fill<<<32, 64>>>(Rm, 1600, 9, 1.0, 1);
+  fill<<<8, 64>>>(EV, 400, 7, 1.0, 1);
+  if (getenv("TUNE_EV_SHIFT")) {  // bench.py's EV = U[0,1) - 0.25 (mixed signs)
+    std::vector<double> h(400);
+    CK(hipMemcpy(h.data(), EV, 3200, hipMemcpyDeviceToHost));
+    for (double &v : h) v -= atof(getenv("TUNE_EV_SHIFT"));
+    CK(hipMemcpy(EV, h.data(), 3200, hipMemcpyHostToDevice));
+  } fill<<<32, 64>>>(L, 1600, 8, 1.0, 1); fill<<<32, 64>>>(Rm, 1600, 9, 1.0, 1);
   for (int r = 0; r < R; r++) {
     Set &s = sets[r];
     CK(hipMalloc(&s.x1, n * 640)); CK(hipMalloc(&s.x2, n * 640)); CK(hipMalloc(&s.x3, n * 640));
@@ -91,8 +98,11 @@ int main(int argc, char **argv) {
   ADD_K("product exact", (&plf_prot_kernel<double, false, true>), 64)
   ADD_K("product fma-mfma", (&plf_prot_mfma_kernel<true>), 64)
   ADD_K("product exact-lds (NS=1)", (&plf_prot_exact_f64_kernel<true>), 64)
-  ADD_K("ldsmat-c (phases 1+2 merged)", (&prot_ldsmat_c_kernel<2>), 64)
-  ADD_K("ldsmat-c minb=1", (&prot_ldsmat_c_kernel<1>), 64)
+  ADD_K("mfma ablate: no matrix cores", (&plf_prot_mfma_kernel<true, 2, true, 1>), 64)
+  ADD_K("mfma ablate: no HBM traffic", (&plf_prot_mfma_kernel<true, 2, true, 2>), 64)
+  ADD_K("mfma 16x16x4 only (padded rows)", (&plf_prot_mfma_kernel<true, 2, true, 0, false>), 64)
+  ADD_K("mfma mix4 minw=3", (&plf_prot_mfma_kernel<true, 3, true, 0, true>), 64)
+  ADD_K("mfma mix4 minw=1", (&plf_prot_mfma_kernel<true, 1, true, 0, true>), 64)
 
   // FMA-mode reference for the mfma variants
   std::vector<uint64_t> h_fref(n * 80);
