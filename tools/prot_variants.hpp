@@ -749,5 +749,199 @@ prot_ldsmat_c_kernel(const double *__restrict__ x1, const double *__restrict__ x
   block_ticket_sum(acc, ws, scaler_sum);
 }
 
+// ---------------------------------------------------------------------------
+// Measured and not adopted (profiles/r01_tune_protein_ring.log): with static
+// wait counts it keeps two tiles in flight per block, but at 2 blocks/CU it
+// ties the product kernel (91 us); the tile traffic structure alone runs at
+// 83-85 us, so the rest is the MFMA phases' issue pattern, not bytes in flight.
+// Branch-free tile traffic through buffer descriptors: one descriptor per tile
+// whose range is the tile's valid sites, so the hardware range check returns 0
+// for loads past n and drops stores past n.  Every thread then issues the same
+// number of vector memory instructions on every trip, which lets the
+// compiler's wait counting keep later loads in flight across a tile_put (the
+// bounds-checked global form branches per chunk, and its unknown count makes
+// the compiler wait for everything).  A tile past n gets an empty range: its
+// loads are issued (keeping the count static) but move no data.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const double *g, int64_t base,
+                                                             int64_t n) {
+  const int64_t left = n - base, sites = left < 0 ? 0 : (left < 64 ? left : 64);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(g + base * 80), 0,
+                                           (int)(sites * 640), 0x00020000);
+}
+template <int K>
+__device__ __forceinline__ void tile_fetch_buf(__amdgpu_buffer_rsrc_t r, f64x2 (&v)[K]) {
+#pragma unroll
+  for (int i = 0; i < K; i++)  // aux 2 = nt
+    v[i] = __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(
+                                         r, (threadIdx.x + i * kBlock) * 16, 0, 2));
+}
+
+// Depth-2 ring form of plf_prot_mfma_kernel (same arithmetic, bit-identical): the
+// A fragments are read from an LDS copy of the matrices at the start of each
+// phase (20 VGPRs live instead of 60 for the whole kernel), which makes room
+// for a second prefetch register set, so two child tiles are always in flight
+// per block -- x2(i) and x1(i+1) during phase 1, x1(i+1) and x2(i+1) during
+// phases 2 and 3 -- where the single set leaves gaps with none.
+template <bool kSum, int kMinWaves = 2>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_mfma_ring_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                          double *__restrict__ x3, const double *__restrict__ EV,
+                          const double *__restrict__ left, const double *__restrict__ right,
+                          const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler,
+                          int64_t n, unsigned long long *ws, int64_t *scaler_sum) {
+  constexpr int S = 20;
+  using PT = ProtTile<double>;
+  constexpr int K = PT::kChunks / kBlock;
+  constexpr int kRow = 2 * PT::kStride;  // doubles per site in the LDS tile (82)
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lo16 = lane & 15, g = lane >> 4;
+  __shared__ double mats[2 * 4 * S * S + S * S];  // P_L[4][400] | P_R[4][400] | EV[400]
+  for (int i = threadIdx.x; i < 4 * S * S; i += kBlock) {
+    mats[i] = left[i];
+    mats[4 * S * S + i] = right[i];
+  }
+  for (int i = threadIdx.x; i < S * S; i += kBlock) mats[8 * S * S + i] = EV[i];
+  // A fragment rows/cols of this lane: [0][s] 16x16x4 (row lo16), [1][s] 4x4x4_4b (row 16 + lane%4)
+  const int rA0 = lo16, rA1 = 16 + (lane & 3);
+  const double m = Num<double>::minlik();
+  __shared__ f64x2 tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock];
+  const double *td = reinterpret_cast<const double *>(tile);
+  double *tw = reinterpret_cast<double *>(tile);
+  long long acc = 0;
+  f64x2 pfA[K], pfB[K];  // x1 / x2 tiles in flight
+  const int64_t stride = (int64_t)gridDim.x * 64;
+  const int64_t first = (int64_t)blockIdx.x * 64;
+  tile_fetch_buf(tile_rsrc(x1, first, n), pfA);
+  tile_fetch_buf(tile_rsrc(x2, first, n), pfB);
+  {  // the trip's trailing stores, mimicked with an empty range (they move no data), so
+     // the loop entry and the back edge see the same vector-memory counts: the compiler
+     // merges the two and would otherwise wait for both prefetched tiles every trip
+    const __amdgpu_buffer_rsrc_t er = __builtin_amdgcn_make_buffer_rsrc(x3, 0, 0, 0x00020000);
+    if (c == 0) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, er, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b128(u32x4{0, 0, 0, 0}, er, 0, 0, 2);
+  }
+  __syncthreads();  // mats
+  for (int64_t base = first; base < n; base += stride) {
+    int z = 0;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keeps the fragment reads per phase
+    const double *mL = mats + z + c * S * S, *mR = mats + z + 4 * S * S + c * S * S;
+    const double *mE = mats + z + 8 * S * S;
+    // this trip's site weights, issued before the prefetches so that waiting
+    // for them does not wait for the tiles in flight (the counter is in order)
+    int wv = 0;
+    if constexpr (kSum) {
+      const int64_t vs = n - base < 64 ? n - base : 64;
+      const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<int32_t *>(wgt ? wgt + base : wgt), 0, wgt ? (int)(vs * 4) : 0, 0x00020000);
+      wv = __builtin_amdgcn_raw_buffer_load_b32(wr, lane * 4, 0, 0);
+    }
+    f64x4 P[4][2];
+    tile_put<double>(tile, pfA);
+    __syncthreads();
+    tile_fetch_buf(tile_rsrc(x1, base + stride, n), pfA);  // unconditional: see tile_rsrc
+    {
+      double A[2][5];
+#pragma unroll
+      for (int st = 0; st < 5; st++) {
+        A[0][st] = mL[rA0 * S + 4 * st + g];
+        A[1][st] = mL[rA1 * S + 4 * st + g];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
+        f64x4 u = {0.0, 0.0, 0.0, 0.0}, v = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 5; st++) {
+          u = __builtin_amdgcn_mfma_f64_16x16x4f64(A[0][st], xr[4 * st], u, 0, 0, 0);
+          v[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(A[1][st], xr[4 * st], v[0], 0, 0, 0);
+        }
+        P[t][0] = u;
+        P[t][1] = v;
+      }
+    }
+    __syncthreads();
+    tile_put<double>(tile, pfB);
+    __syncthreads();
+    tile_fetch_buf(tile_rsrc(x2, base + stride, n), pfB);
+    {
+      double A[2][5];
+#pragma unroll
+      for (int st = 0; st < 5; st++) {
+        A[0][st] = mR[rA0 * S + 4 * st + g];
+        A[1][st] = mR[rA1 * S + 4 * st + g];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
+        f64x4 u = {0.0, 0.0, 0.0, 0.0}, v = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 5; st++) {
+          u = __builtin_amdgcn_mfma_f64_16x16x4f64(A[0][st], xr[4 * st], u, 0, 0, 0);
+          v[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(A[1][st], xr[4 * st], v[0], 0, 0, 0);
+        }
+        P[t][0] = P[t][0] * u;  // prod[k] = umpL[k] * umpR[k]
+        P[t][1] = P[t][1] * v;
+      }
+    }
+    __syncthreads();  // every wave is done reading x2: the tile takes X3 now
+    unsigned long long mine = 0;
+    {
+      double A[2][5];  // EV^T[l = row][k = col]
+#pragma unroll
+      for (int st = 0; st < 5; st++) {
+        A[0][st] = mE[(4 * st + g) * S + rA0];
+        A[1][st] = mE[(4 * st + g) * S + rA1];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        f64x4 X0 = {0.0, 0.0, 0.0, 0.0};
+        double X1 = 0.0;
+#pragma unroll
+        for (int st = 0; st < 5; st++) {
+          X0 = __builtin_amdgcn_mfma_f64_16x16x4f64(A[0][st], P[t][st >> 2][st & 3], X0, 0, 0, 0);
+          X1 = __builtin_amdgcn_mfma_f64_4x4x4f64(A[1][st], P[t][st >> 2][st & 3], X1, 0, 0, 0);
+        }
+        const bool small = (__builtin_fabs(X0[0]) < m) && (__builtin_fabs(X0[1]) < m) &&
+                           (__builtin_fabs(X0[2]) < m) && (__builtin_fabs(X0[3]) < m) &&
+                           (__builtin_fabs(X1) < m);
+        const unsigned long long b = __ballot(small);
+        mine |= (b & (b >> 16) & (b >> 32) & (b >> 48) & 0xFFFFull) << (16 * t);
+        double *w = tw + (16 * t + lo16) * kRow + c * S;
+#pragma unroll
+        for (int r = 0; r < 4; r++) w[g + 4 * r] = X0[r];
+        w[16 + g] = X1;
+      }
+    }
+    if (lane == 0) small_mask[c] = mine;
+    __syncthreads();
+    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+    if (c == 0) {  // scaler bytes through a range-checked descriptor (no divergent store)
+      const bool sc = (all >> lane) & 1ull;
+      const int64_t vs = n - base < 64 ? n - base : 64;
+      const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+          scaler ? scaler + base : scaler, 0, scaler ? (int)vs : 0, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sc, sr, lane, 0, 0);
+      if (kSum && sc && base + lane < n) acc += wgt ? (long long)wv : 1ll;
+    }
+    {
+      const __amdgpu_buffer_rsrc_t r = tile_rsrc(x3, base, n);
+#pragma unroll
+      for (int i = 0; i < K; i++) {
+        const int j = threadIdx.x + i * kBlock;
+        const int sl = j / PT::kChunksPerSite, q = j - sl * PT::kChunksPerSite;
+        f64x2 v = tile[sl * PT::kStride + q];
+        if ((all >> sl) & 1ull) v = v * Num<double>::two32();
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, j * 16, 0, 2);
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
 }  // namespace dev
 }  // namespace plfx

@@ -35,6 +35,62 @@ __global__ void fill(double *p, int64_t n, uint64_t seed, double scale_every4, i
 
 struct Set { double *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
 
+// Structure probes (not PLF): the ring kernel's memory traffic alone, with and
+// without its LDS round trip and barriers.  kLds 0: x3 = x1 + x2 from registers;
+// 1: x1 and x2 through the padded LDS tile and back, barriers as the kernel.
+template <int kLds>
+__global__ void __launch_bounds__(256, 2)
+probe_tiles(const double *__restrict__ x1, const double *__restrict__ x2, double *__restrict__ x3,
+            const double *, const double *, const double *, const int32_t *, uint8_t *, int64_t n,
+            unsigned long long *, int64_t *) {
+  using PT = ProtTile<double>;
+  constexpr int K = PT::kChunks / kBlock;
+  __shared__ f64x2 tile[64 * PT::kStride];
+  __shared__ double pad[(70848 - 64 * PT::kStride * 16) / 8];  // same LDS footprint as the kernel
+  if (threadIdx.x == 1000) pad[0] = 0;
+  f64x2 pfA[K], pfB[K];
+  const int64_t stride = (int64_t)gridDim.x * 64, first = (int64_t)blockIdx.x * 64;
+  tile_fetch_buf(tile_rsrc(x1, first, n), pfA);
+  tile_fetch_buf(tile_rsrc(x2, first, n), pfB);
+  {
+    const __amdgpu_buffer_rsrc_t er = __builtin_amdgcn_make_buffer_rsrc(x3, 0, 0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b128(u32x4{0, 0, 0, 0}, er, 0, 0, 2);
+  }
+  for (int64_t base = first; base < n; base += stride) {
+    f64x2 o[K];
+    if constexpr (kLds) {
+      tile_put<double>(tile, pfA);
+      __syncthreads();
+      tile_fetch_buf(tile_rsrc(x1, base + stride, n), pfA);
+#pragma unroll
+      for (int i = 0; i < K; i++) o[i] = tile[(threadIdx.x * 7 + i * 256) % (64 * PT::kStride)];
+      __syncthreads();
+      tile_put<double>(tile, pfB);
+      __syncthreads();
+      tile_fetch_buf(tile_rsrc(x2, base + stride, n), pfB);
+#pragma unroll
+      for (int i = 0; i < K; i++) o[i] += tile[(threadIdx.x * 7 + i * 256) % (64 * PT::kStride)];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < K; i++) tile[(threadIdx.x * 5 + i * 256) % (64 * PT::kStride)] = o[i];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < K; i++) o[i] = tile[(threadIdx.x * 3 + i * 256) % (64 * PT::kStride)];
+    } else {
+#pragma unroll
+      for (int i = 0; i < K; i++) o[i] = pfA[i] + pfB[i];
+      tile_fetch_buf(tile_rsrc(x1, base + stride, n), pfA);
+      tile_fetch_buf(tile_rsrc(x2, base + stride, n), pfB);
+    }
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(x3, base, n);
+#pragma unroll
+    for (int i = 0; i < K; i++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o[i]), r, (threadIdx.x + i * kBlock) * 16, 0, 2);
+    if constexpr (kLds) __syncthreads();
+  }
+}
+
 int main(int argc, char **argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : (1 << 18);
   const int R = 4, reps = argc > 2 ? atoi(argv[2]) : 40, rounds = 3;
@@ -101,8 +157,10 @@ int main(int argc, char **argv) {
   ADD_K("mfma ablate: no matrix cores", (&plf_prot_mfma_kernel<true, 2, true, 1>), 64)
   ADD_K("mfma ablate: no HBM traffic", (&plf_prot_mfma_kernel<true, 2, true, 2>), 64)
   ADD_K("mfma 16x16x4 only (padded rows)", (&plf_prot_mfma_kernel<true, 2, true, 0, false>), 64)
-  ADD_K("mfma mix4 minw=3", (&plf_prot_mfma_kernel<true, 3, true, 0, true>), 64)
-  ADD_K("mfma mix4 minw=1", (&plf_prot_mfma_kernel<true, 1, true, 0, true>), 64)
+  ADD_K("mfma ring (2 tiles in flight)", (&plf_prot_mfma_ring_kernel<true, 2>), 64)
+  ADD_K("mfma probe: ring traffic only", (&probe_tiles<0>), 64)
+  ADD_K("mfma probe: ring traffic + LDS + barriers", (&probe_tiles<1>), 64)
+  ADD_K("mfma ring minw=1", (&plf_prot_mfma_ring_kernel<true, 1>), 64)
 
   // FMA-mode reference for the mfma variants
   std::vector<uint64_t> h_fref(n * 80);
