@@ -82,6 +82,16 @@ __device__ __forceinline__ long long decode_count(long long word) {
 }
 
 // The two round trips for one block total `tot` (one thread).
+// Site weight, loaded unconditionally: wgt == nullptr (all weights 1) reads a
+// dummy word instead of branching round the load.  A load inside a branch got
+// its value sign-extended inside the branch, i.e. an s_waitcnt vmcnt(0) right
+// after it -- every CLV load of the trip issued so far had to land first.
+__device__ __forceinline__ int wgt_at(const int32_t *wgt, int64_t site, const void *dummy) {
+  const int32_t *p = wgt ? wgt + site : static_cast<const int32_t *>(dummy);
+  const int v = __builtin_nontemporal_load(p);
+  return wgt ? v : 1;
+}
+
 __device__ inline void ticket_publish(long long tot, unsigned long long *wsu, int64_t *out) {
   long long *ws = reinterpret_cast<long long *>(wsu);
   const long long G = gridDim.x;
@@ -277,7 +287,7 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
       else Num<T>::template load4<NT>(x1 + site * 16 + c * 4, a[u]);
       if constexpr (T2) k2[u] = tip2[site] & 15;
       else Num<T>::template load4<NT>(x2 + site * 16 + c * 4, b[u]);
-      if (kSum) w[u] = wgt ? wgt[site] : 1;
+      if (kSum) w[u] = wgt_at(wgt, site, ws);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -488,7 +498,7 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
         else a[u][j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(x1 + site0 * 16) + lane);
         if constexpr (T2) k2[u][j] = tip2[site0 + g] & 15;
         else b[u][j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
-        if (kSum) w[u][j] = wgt ? wgt[site0 + g] : 1;
+        if (kSum) w[u][j] = wgt ? wgt[site0 + g] : 1;  // (wgt_at measured 1.6 % slower here)
       }
 #pragma unroll
     for (int u = 0; u < U; u++)
@@ -727,27 +737,27 @@ plf_dna_f64_triple_kernel(const TripleBatch tb, const double *__restrict__ EV,
     for (int j = 0; j < 2 * U; j++) {  // all loads of the 16*U sites first
       const int64_t site0 = base + j * 8;
       valid[j] = site0 + g < n;
+      // past n: reload the last site (unconditional loads, no wait-all; results unused)
+      const int64_t sq = valid[j] ? site0 + g : n - 1;
+      const int64_t rec = sq * 8 + (lane & 7);  // f64x2 index of this lane's pair (8 per site)
       va1[j] = va2[j] = vb1[j] = vb2[j] = f64x2{0.0, 0.0};
       ka1[j] = ka2[j] = kb1[j] = kb2[j] = 0;
       w[j] = 0;
-      if (valid[j]) {
-        const int64_t rec = site0 * 8 + lane;  // f64x2 index of this lane's pair (8 per site)
-        if constexpr (T1) {
-          ka1[j] = ta1[site0 + g] & 15;
-          kb1[j] = tb1[site0 + g] & 15;
-        } else {
-          va1[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xa1) + rec);
-          vb1[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xb1) + rec);
-        }
-        if constexpr (T2) {
-          ka2[j] = ta2[site0 + g] & 15;
-          kb2[j] = tb2[site0 + g] & 15;
-        } else {
-          va2[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xa2) + rec);
-          vb2[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xb2) + rec);
-        }
-        if (kSum) w[j] = wgt ? wgt[site0 + g] : 1;
+      if constexpr (T1) {
+        ka1[j] = ta1[sq] & 15;
+        kb1[j] = tb1[sq] & 15;
+      } else {
+        va1[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xa1) + rec);
+        vb1[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xb1) + rec);
       }
+      if constexpr (T2) {
+        ka2[j] = ta2[sq] & 15;
+        kb2[j] = tb2[sq] & 15;
+      } else {
+        va2[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xa2) + rec);
+        vb2[j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(xb2) + rec);
+      }
+      if (kSum) w[j] = wgt_at(wgt, sq, ws);
     }
 #pragma unroll
     for (int j = 0; j < 2 * U; j++) {
@@ -851,27 +861,26 @@ plf_dna_cat_triple_kernel(const TripleBatch tb, const T *__restrict__ EV,
     for (int u = 0; u < U; u++) {
       const int64_t site = base + u * 16 + q;
       valid[u] = site < n;
+      const int64_t sq = valid[u] ? site : n - 1;  // past n: reload the last site (unused)
       ka1[u] = ka2[u] = kb1[u] = kb2[u] = w[u] = 0;
 #pragma unroll
       for (int l = 0; l < 4; l++) va1[u][l] = va2[u][l] = vb1[u][l] = vb2[u][l] = T(0);
-      if (valid[u]) {
-        const int64_t off = site * 16 + c * 4;
-        if constexpr (T1) {
-          ka1[u] = ta1[site] & 15;
-          kb1[u] = tb1[site] & 15;
-        } else {
-          Num<T>::template load4<NT>(xa1 + off, va1[u]);
-          Num<T>::template load4<NT>(xb1 + off, vb1[u]);
-        }
-        if constexpr (T2) {
-          ka2[u] = ta2[site] & 15;
-          kb2[u] = tb2[site] & 15;
-        } else {
-          Num<T>::template load4<NT>(xa2 + off, va2[u]);
-          Num<T>::template load4<NT>(xb2 + off, vb2[u]);
-        }
-        if (kSum) w[u] = wgt ? wgt[site] : 1;
+      const int64_t off = sq * 16 + c * 4;
+      if constexpr (T1) {
+        ka1[u] = ta1[sq] & 15;
+        kb1[u] = tb1[sq] & 15;
+      } else {
+        Num<T>::template load4<NT>(xa1 + off, va1[u]);
+        Num<T>::template load4<NT>(xb1 + off, vb1[u]);
       }
+      if constexpr (T2) {
+        ka2[u] = ta2[sq] & 15;
+        kb2[u] = tb2[sq] & 15;
+      } else {
+        Num<T>::template load4<NT>(xa2 + off, va2[u]);
+        Num<T>::template load4<NT>(xb2 + off, vb2[u]);
+      }
+      if (kSum) w[u] = wgt_at(wgt, sq, ws);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -1010,22 +1019,23 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
 #pragma unroll
     for (int j = 0; j < U; j++) {
       const int64_t site0 = base + 8 * j;
-      const int64_t rec = site0 * 8 + lane;  // f64x2 index of this lane's pair (8 per site)
+      // past n (or a trip past the end, when prefetching): reload the last site;
+      // unconditional loads keep the compiler's wait counts exact (results unused)
+      const int64_t sq = site0 + g < n ? site0 + g : n - 1;
+      const int64_t rec = sq * 8 + (lane & 7);  // f64x2 index of this lane's pair (8 per site)
       t.w[j] = 0;
 #pragma unroll
       for (int q = 0; q < 8; q++) {
         t.v[j][q] = f64x2{0.0, 0.0};
         t.k8[j][q] = 0;
       }
-      if (site0 + g < n) {
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-          const bool tip = (q & 1) ? T2 : T1;
-          if (tip) t.k8[j][q] = ((const uint8_t *)d.g[q])[site0 + g] & 15;
-          else t.v[j][q] = ld16<NTL>(reinterpret_cast<const f64x2 *>(d.g[q]) + rec);
-        }
-        if (kSum) t.w[j] = wgt ? wgt[site0 + g] : 1;
+      for (int q = 0; q < 8; q++) {
+        const bool tip = (q & 1) ? T2 : T1;
+        if (tip) t.k8[j][q] = ((const uint8_t *)d.g[q])[sq] & 15;
+        else t.v[j][q] = ld16<NTL>(reinterpret_cast<const f64x2 *>(d.g[q]) + rec);
       }
+      if (kSum) t.w[j] = wgt_at(wgt, sq, ws);
     }
   };
   Trip nxt;
@@ -1037,7 +1047,7 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
     Trip cur;
     if constexpr (kPf) {  // the next trip's loads stay in flight while this one computes
       cur = nxt;
-      if (base + stride < n) fetch(base + stride, nxt);
+      fetch(base + stride, nxt);  // unconditional (see fetch)
     } else {
       fetch(base, cur);
     }

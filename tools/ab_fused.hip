@@ -1,0 +1,125 @@
+// ab_fused.hip -- interleaved A/B of two versions of the fused DNA kernels
+// (tuning only).  Version A is the header in csrc/, version B a second copy of
+// plf_dna.hpp (e.g. the previous commit's) included under the namespace
+// plfx::dev_b, so both run in one process, round-robin over 5 rounds -- box to
+// box and run to run drift is several percent, more than the effects measured.
+//
+//   git show HEAD~1:amd-versal-phylogenetic-likelihood-function_amd/csrc/plf_dna.hpp > /tmp/b/plf_dna.hpp
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//     -I amd-versal-phylogenetic-likelihood-function_amd/csrc -DB_HEADER='"/tmp/b/plf_dna.hpp"' \
+//     tools/ab_fused.hip -o build/ab_fused
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "plf_dna.hpp"
+#define dev dev_b
+#include B_HEADER
+#undef dev
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+__global__ void fill(double *p, int64_t n, uint64_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    p[i] = (double)(z >> 11) * (1.0 / 9007199254740992.0) * 0.5;
+  }
+}
+
+template <typename SB, typename TB>
+void make(SB &sb, TB &tb, const std::vector<double *> &in, const std::vector<double *> &out,
+          double *mats, int64_t *sums) {
+  for (int t = 0; t < 8; t++) {
+    auto &d = sb.d[t];
+    for (int q = 0; q < 8; q++) d.g[q] = in[8 * t + q];
+    for (int q = 0; q < 7; q++) {
+      d.x[q] = out[7 * t + q];
+      d.mat[2 * q] = mats + (14 * t + 2 * q) * 64;
+      d.mat[2 * q + 1] = mats + (14 * t + 2 * q + 1) * 64;
+      d.sc[q] = nullptr;
+      d.ss[q] = sums + 7 * t + q;
+    }
+  }
+  for (int t = 0; t < 10; t++) {  // triples over the first 40 inputs
+    const double *M = mats + 6 * t * 64;
+    tb.d[t] = {in[4 * t], in[4 * t + 1], in[4 * t + 2], in[4 * t + 3], out[3 * t], out[3 * t + 1],
+               out[3 * t + 2], M, M + 64, M + 128, M + 192, M + 256, M + 320,
+               nullptr, nullptr, nullptr, sums + 3 * t, sums + 3 * t + 1, sums + 3 * t + 2};
+  }
+}
+
+int main(int argc, char **argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : (1 << 20);
+  const int reps = argc > 2 ? atoi(argv[2]) : 10, rounds = 5;
+  hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
+  const int CUs = prop.multiProcessorCount;
+  std::vector<double *> in(64), out(56);
+  for (auto &p : in) CK(hipMalloc(&p, n * 128));
+  for (auto &p : out) CK(hipMalloc(&p, n * 128));
+  for (int i = 0; i < 64; i++) fill<<<1024, 256>>>(in[i], n * 16, 100 + i);
+  double *mats, *EV; int *wgt; unsigned long long *ws; int64_t *sums;
+  CK(hipMalloc(&mats, 14 * 8 * 64 * 8)); CK(hipMalloc(&EV, 16 * 8));
+  fill<<<16, 256>>>(mats, 14 * 8 * 64, 7); fill<<<1, 64>>>(EV, 16, 8);
+  CK(hipMalloc(&wgt, n * 4)); CK(hipMemset(wgt, 0, n * 4));
+  CK(hipMalloc(&ws, 56 * plfx::dev::kWsWords * 8)); CK(hipMemset(ws, 0, 56 * plfx::dev::kWsWords * 8));
+  CK(hipMalloc(&sums, 56 * 8));
+  CK(hipDeviceSynchronize());
+  plfx::dev::SeptetBatch sa{}; plfx::dev::TripleBatch ta{};
+  plfx::dev_b::SeptetBatch sb{}; plfx::dev_b::TripleBatch tb{};
+  make(sa, ta, in, out, mats, sums);
+  make(sb, tb, in, out, mats, sums);
+  auto occ = [&](const void *k) { int b = 0; CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, 256, 0)); return b; };
+  struct V { std::string name; double bytes; std::function<void()> run; std::vector<float> us; };
+  std::vector<V> vs;
+#define ADD(NAME, K, BATCH, COUNT, BYTES)                                                           \
+  {                                                                                                \
+    auto k = K;                                                                                    \
+    const int64_t gx = std::max<int64_t>(1, (int64_t)occ((const void *)k) * CUs / COUNT);          \
+    vs.push_back({NAME, (double)(BYTES) * n * COUNT, [=]() {                                       \
+      hipLaunchKernelGGL(k, dim3((unsigned)gx, COUNT), dim3(256), 0, 0, BATCH, EV, wgt, n, ws, nullptr); }, {}}); \
+  }
+  const double kSep = 15 * 128 + 4, kTri = 7 * 128 + 4;
+  ADD("A septet U=2 pf  x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, true>), sa, 8, kSep)
+  ADD("B septet U=2 pf  x8", (&plfx::dev_b::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, true>), sb, 8, kSep)
+  ADD("A septet U=2     x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, false>), sa, 8, kSep)
+  ADD("B septet U=2     x8", (&plfx::dev_b::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, false>), sb, 8, kSep)
+  ADD("A septet U=4     x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 4, false>), sa, 8, kSep)
+  ADD("A septet U=2 pf  x1", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, true>), sa, 1, kSep)
+  ADD("B septet U=2 pf  x1", (&plfx::dev_b::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, true>), sb, 1, kSep)
+  ADD("A septet U=2     x1", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, false>), sa, 1, kSep)
+  ADD("A septet U=1     x1", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 1, false>), sa, 1, kSep)
+  ADD("A triple x10", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 0, 1>), ta, 10, kTri)
+  ADD("B triple x10", (&plfx::dev_b::plf_dna_f64_triple_kernel<true, 1, true, 0, 1>), tb, 10, kTri)
+  ADD("A triple x4", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 0, 1>), ta, 4, kTri)
+  ADD("B triple x4", (&plfx::dev_b::plf_dna_f64_triple_kernel<true, 1, true, 0, 1>), tb, 4, kTri)
+  ADD("A triple x1", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 0, 1>), ta, 1, kTri)
+  ADD("B triple x1", (&plfx::dev_b::plf_dna_f64_triple_kernel<true, 1, true, 0, 1>), tb, 1, kTri)
+  ADD("A triple U=2 x1", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 0, 2>), ta, 1, kTri)
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; r++)
+    for (auto &v : vs) {
+      v.run();
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < reps; i++) v.run();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      v.us.push_back(ms * 1000.f / reps);
+    }
+  CK(hipGetLastError());
+  printf("n=%lld sites, %d rounds interleaved; A = csrc, B = " B_HEADER "\n", (long long)n, rounds);
+  for (auto &v : vs) {
+    std::sort(v.us.begin(), v.us.end());
+    const double t = v.us[v.us.size() / 2] * 1e-6;
+    printf("%-24s median %9.1f us (min %9.1f)  %5.1f%% of 8 TB/s\n", v.name.c_str(), v.us[v.us.size() / 2],
+           v.us[0], 100.0 * v.bytes / t / 8e12);
+  }
+  return 0;
+}
