@@ -365,3 +365,48 @@ def test_random_trees_match_oracle(ctx, oracle, seed, dtype):
     assert np.array_equal(sums.cpu().numpy(), esums)
     for j in range(nops):
         assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+
+
+@pytest.mark.parametrize("n", [1, 5, 8, 9, 15, 17, 33, 257])
+@pytest.mark.parametrize("tipmode", ["dense", "left", "coded"])
+@pytest.mark.parametrize("taxa,dtype", [(8, np.float64), (4, np.float64), (8, np.float32),
+                                        (4, np.float32)])
+def test_single_subtree_tails(ctx, oracle, n, tipmode, taxa, dtype):
+    """An 8-taxon balanced tree is exactly one fused seven-node pass (f64; f32:
+    two level-pair passes and a node), a 4-taxon tree one level-pair pass.
+    Site counts around the kernels' 8- and 16-site blocks (tails, n < one
+    block, clamped loads past n) with each tip kind, against the oracle; the
+    weights and the scaling threshold are exercised (P x0.02 makes the deeper
+    nodes underflow), and nothing may be written past n."""
+    import torch
+
+    rng = np.random.default_rng(1000 + n)
+    ops = oracle.balanced_tree_ops(taxa)
+    nops = taxa - 1
+    nslots = taxa + nops
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    coded = [{"dense": False, "left": t % 2 == 0, "coded": True}[tipmode] for t in range(taxa)]
+    codes = [oracle.random_tip_codes(rng, n, 0.3) for _ in range(taxa)]
+    dense = [rng.random(16 * n).astype(dtype) for _ in range(taxa)]
+    pm = (rng.random(nops * 128) * 0.02).astype(dtype)
+    EV = rng.random(16).astype(dtype)
+    wgt = rng.integers(0, 7, n).astype(np.int32)
+    host = [oracle.expand_tips(codes[t], dtype) if coded[t] else dense[t].copy() for t in range(taxa)]
+    host += [np.zeros(16 * n, dtype) for _ in range(nops)]
+    esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
+    clv = [None if coded[t] else dev(dense[t]) for t in range(taxa)]
+    big = [torch.full((16 * (n + 8),), -1.0, dtype=tt, device="cuda") for _ in range(nops)]
+    clv += [b[:16 * n] for b in big]  # views: nothing may land past n
+    tips = [dev(codes[t]) if coded[t] else None for t in range(taxa)] + [None] * nops
+    sums = torch.full((nops,), -5, dtype=torch.int64, device="cuda")
+    scal = [torch.full((n + 8,), 7, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+    ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), [s[:n] for s in scal], sums, tips=tips)
+    torch.cuda.synchronize()
+    for s in range(taxa, nslots):
+        assert np.array_equal(bits(clv[s].cpu().numpy()), bits(host[s])), s
+        assert (big[s - taxa][16 * n:].cpu().numpy() == -1.0).all(), s
+    assert np.array_equal(sums.cpu().numpy(), esums)
+    for j in range(nops):
+        got = scal[j].cpu().numpy()
+        assert np.array_equal(got[:n], escal[j]), j
+        assert (got[n:] == 7).all(), j  # nothing written past n
