@@ -927,7 +927,7 @@ plf_dna_cat_triple_kernel(const TripleBatch tb, const T *__restrict__ EV,
 struct SeptetDesc {
   const void *g[8];
   void *x[7];               // A1..A4, B1, B2, R
-  const double *mat[14];    // left, right of A1..A4, B1, B2, R
+  const void *mat[14];      // left, right of A1..A4, B1, B2, R (element type T)
   uint8_t *sc[7];
   int64_t *ss[7];
 };
@@ -989,15 +989,15 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
   __shared__ double tab[T2 ? 8 : (T1 ? 4 : 1)][T1 ? 256 : 1];
   for (int e = threadIdx.x; e < 7 * 128; e += kBlock) {
     const int node = e >> 7, k = e & 127;
-    mats[node][k] = d.mat[2 * node + (k >> 6)][k & 63];
+    mats[node][k] = static_cast<const double *>(d.mat[2 * node + (k >> 6)])[k & 63];
   }
   if constexpr (T1) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) build_tip_table<double>(d.mat[2 * i], tipvec, tab[i]);
+    for (int i = 0; i < 4; i++) build_tip_table<double>((const double *)d.mat[2 * i], tipvec, tab[i]);
   }
   if constexpr (T2) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) build_tip_table<double>(d.mat[2 * i + 1], tipvec, tab[4 + i]);
+    for (int i = 0; i < 4; i++) build_tip_table<double>((const double *)d.mat[2 * i + 1], tipvec, tab[4 + i]);
   }
   __syncthreads();
   const int trow = c * 64 + 2 * h;
@@ -1093,6 +1093,108 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
         for (int q = 0; q < 7; q++) {
           if (d.sc[q]) d.sc[q][site0 + g] = (uint8_t)sc[j][q];
           if (kSum && sc[j][q]) acc[q] += w[j];
+        }
+      }
+    }
+  }
+  if constexpr (kSum) block_ticket_sum7(acc, ws + (size_t)blockIdx.y * 7 * kWsWords, d.ss);
+}
+
+// Fused three-level subtree in the lane = category mapping (f32; any T): the
+// same seven-node pass as plf_dna_f64_septet_kernel, lane = (site q, category
+// c), 16 sites per wave and block of U.  A lane needs 32 matrix values per
+// node (its category's P_L and P_R rows): the 7 nodes' matrices sit in LDS
+// (3.5 KB f32) and are read per node and trip (4 distinct 16-B addresses per
+// read, one per category, on disjoint banks); an opaque zero offset keeps the
+// reads inside the loop (hoisted they need 224 VGPRs).
+template <typename T, bool kSum, int kMinWaves, bool NT, int kTips, int U = 2>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_dna_cat_septet_kernel(const SeptetBatch sb, const T *__restrict__ EV,
+                          const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
+                          const T *__restrict__ tipvec) {
+  constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
+  const SeptetDesc &d = sb.d[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 3, q = lane >> 2, nib = lane & 60;
+  __shared__ T mats[7 * 128];  // node i: left [c][16] | right [c][16]
+  __shared__ T tab[T2 ? 8 : (T1 ? 4 : 1)][T1 ? 256 : 1];
+  for (int e = threadIdx.x; e < 7 * 128; e += kBlock) {
+    const int node = e >> 7, k = e & 127;
+    mats[e] = static_cast<const T *>(d.mat[2 * node + (k >> 6)])[k & 63];
+  }
+  if constexpr (T1) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) build_tip_table<T>((const T *)d.mat[2 * i], tipvec, tab[i]);
+  }
+  if constexpr (T2) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) build_tip_table<T>((const T *)d.mat[2 * i + 1], tipvec, tab[4 + i]);
+  }
+  __syncthreads();
+  T E[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) E[i] = EV[i];
+  const T m = Num<T>::minlik();
+  const int trow = c * 64;
+
+  long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  for (int64_t base = wave * 16 * U; base < n; base += stride) {
+    int z = 0;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    const T *mz = mats + z;
+    T v[U][8][4];
+    int k8[U][8], w[U];
+    bool valid[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {  // all loads of the trip first, unconditional (clamped)
+      const int64_t site = base + u * 16 + q;
+      valid[u] = site < n;
+      const int64_t sq = valid[u] ? site : n - 1;
+#pragma unroll
+      for (int g = 0; g < 8; g++) {
+        const bool tip = (g & 1) ? T2 : T1;
+        k8[u][g] = 0;
+#pragma unroll
+        for (int l = 0; l < 4; l++) v[u][g][l] = T(0);
+        if (tip) k8[u][g] = ((const uint8_t *)d.g[g])[sq] & 15;
+        else Num<T>::template load4<NT>((const T *)d.g[g] + sq * 16 + c * 4, v[u][g]);
+      }
+      w[u] = kSum ? wgt_at(wgt, sq, ws) : 0;
+    }
+    T o[U][7][4];
+    bool sc[U][7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      T PL[16], PR[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        PL[j] = mz[128 * i + c * 16 + j];
+        PR[j] = mz[128 * i + 64 + c * 16 + j];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (i < 4)
+          cat_node<T, T1, T2>(v[u][2 * i], v[u][2 * i + 1], tab[T1 ? (i & 3) : 0] + trow + 4 * k8[u][2 * i],
+                              tab[T2 ? 4 + (i & 3) : 0] + trow + 4 * k8[u][2 * i + 1], PL, PR, E,
+                              valid[u], nib, m, o[u][i], sc[u][i]);
+        else  // B1 = (A1, A2), B2 = (A3, A4), R = (B1, B2)
+          cat_node<T, false, false>(o[u][2 * (i - 4)], o[u][2 * (i - 4) + 1], nullptr, nullptr, PL,
+                                    PR, E, valid[u], nib, m, o[u][i], sc[u][i]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (!valid[u]) continue;
+      const int64_t site = base + u * 16 + q;
+#pragma unroll
+      for (int i = 0; i < 7; i++) Num<T>::store4_nt((T *)d.x[i] + site * 16 + c * 4, o[u][i]);
+      if (c == 0) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+          if (d.sc[i]) d.sc[i][site] = (uint8_t)sc[u][i];
+          if (kSum && sc[u][i]) acc[i] += w[u];
         }
       }
     }

@@ -50,6 +50,7 @@ constexpr int kTripleU32 = 2;
 // fused three-level subtrees: 2 x 8-site blocks per trip, matrices re-read from
 // LDS, next trip's loads in flight (tools/tune_septet.hip, r01_tune_septet.log)
 constexpr int kSeptetU = 2;
+constexpr int kSeptetU32 = 2;  // f32 (lane = category): 2 x 16-site blocks per trip
 
 // Co-resident 256-thread blocks of `kernel` on the current device (cached per
 // kernel instantiation by the caller).
@@ -226,11 +227,24 @@ hipError_t launch_septets_t(const dev::SeptetBatch &b, int count, const double *
   return hipGetLastError();
 }
 
+template <bool kSum, int kTips>
+hipError_t launch_septets32_t(const dev::SeptetBatch &b, int count, const float *EV,
+                              const int32_t *wgt, int64_t n, unsigned long long *ws,
+                              int max_blocks, hipStream_t s, const float *tipvec) {
+  static int cache = 0;
+  auto kernel = &dev::plf_dna_cat_septet_kernel<float, kSum, 1, kNt, kTips, kSeptetU32>;
+  const int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 16 * kSeptetU32,
+                            count, max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt,
+                     n, ws, tipvec);
+  return hipGetLastError();
+}
+
 }  // namespace
 
-hipError_t launch_plf_dna_septets(const SeptetDescH *t, int count, const double *EV,
+hipError_t launch_plf_dna_septets(int dtype, const SeptetDescH *t, int count, const void *EV,
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,
-                                  int max_blocks, hipStream_t s, int tips, const double *tipvec) {
+                                  int max_blocks, hipStream_t s, int tips, const void *tipvec) {
   if (count < 1 || count > kMaxSeptets || tips < 0 || tips > 2) return hipErrorInvalidValue;
   dev::SeptetBatch b{};
   bool any_sum = false;
@@ -238,13 +252,21 @@ hipError_t launch_plf_dna_septets(const SeptetDescH *t, int count, const double 
     __builtin_memcpy(&b.d[i], &t[i], sizeof(t[i]));
     for (int q = 0; q < 7; q++) any_sum |= t[i].ss[q] != nullptr;
   }
-  switch ((any_sum ? 3 : 0) + tips) {
-    case 0: return launch_septets_t<false, 0>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    case 1: return launch_septets_t<false, 1>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    case 2: return launch_septets_t<false, 2>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    case 3: return launch_septets_t<true, 0>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    case 4: return launch_septets_t<true, 1>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    default: return launch_septets_t<true, 2>(b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+  const double *E64 = (const double *)EV, *V64 = (const double *)tipvec;
+  const float *E32 = (const float *)EV, *V32 = (const float *)tipvec;
+  switch ((dtype == 1 ? 6 : 0) + (any_sum ? 3 : 0) + tips) {
+    case 0: return launch_septets32_t<false, 0>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 1: return launch_septets32_t<false, 1>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 2: return launch_septets32_t<false, 2>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 3: return launch_septets32_t<true, 0>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 4: return launch_septets32_t<true, 1>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 5: return launch_septets32_t<true, 2>(b, count, E32, wgt, n, ws, max_blocks, s, V32);
+    case 6: return launch_septets_t<false, 0>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    case 7: return launch_septets_t<false, 1>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    case 8: return launch_septets_t<false, 2>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    case 9: return launch_septets_t<true, 0>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    case 10: return launch_septets_t<true, 1>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
+    default: return launch_septets_t<true, 2>(b, count, E64, wgt, n, ws, max_blocks, s, V64);
   }
 }
 

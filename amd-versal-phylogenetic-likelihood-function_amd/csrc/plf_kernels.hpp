@@ -75,18 +75,18 @@ hipError_t launch_plf_dna_triples(int dtype, const TripleDescH *t, int count, co
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,
                                   int max_blocks, hipStream_t s, int tips, const void *tipvec);
 
-// Fused three-level subtrees (plf_dna.hpp SeptetDesc), f64 only; <= kMaxSeptets per
-// launch, ws >= 7 * count regions.  tips as plf_dna_f64_septet_kernel's kTips.
+// Fused three-level subtrees (plf_dna.hpp SeptetDesc), dtype 0 f32 / 1 f64; <= kMaxSeptets
+// per launch, ws >= 7 * count regions.  tips as plf_dna_f64_septet_kernel's kTips.
 struct SeptetDescH {
   const void *g[8];
   void *x[7];
-  const double *mat[14];
+  const void *mat[14];
   uint8_t *sc[7];
   int64_t *ss[7];
 };
 constexpr int kMaxSeptets = 8;
-hipError_t launch_plf_dna_septets(const SeptetDescH *t, int count, const double *EV,
+hipError_t launch_plf_dna_septets(int dtype, const SeptetDescH *t, int count, const void *EV,
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,
-                                  int max_blocks, hipStream_t s, int tips, const double *tipvec);
+                                  int max_blocks, hipStream_t s, int tips, const void *tipvec);
 
 }  // namespace plfx

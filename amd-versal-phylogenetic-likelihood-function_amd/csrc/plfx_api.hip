@@ -460,7 +460,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   };
   std::vector<Triple> triples;
   std::vector<char> used(nops, 0);
-  // Fused three-level subtrees (f64 DNA, plf_dna.hpp SeptetDesc): root R two
+  // Fused three-level subtrees (DNA, plf_dna.hpp SeptetDesc): root R two
   // levels above four ops A of one tip kind, through the two ops B that R's
   // children were last written by; R's and the B's slots free by level L.
   // Ordered so that a[2i], a[2i+1] are b[i]'s child1, child2 and b[0], b[1]
@@ -475,7 +475,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
     return x >= 0 && y >= 0 && x != y && !used[x] && !used[y] && !used[p] && level[x] == L &&
            level[y] == L && level[p] == L + 1;
   };
-  if (ctx->fuse >= 2 && states == 4 && dtype == PLFX_F64) {
+  if (ctx->fuse >= 2 && states == 4) {
     for (int r = 0; r < nops; r++) {
       Septet t{};
       t.r = r;
@@ -530,8 +530,8 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
           d.g[2 * q + 1] = nd.x2;
         }
         d.x[q] = nd.x3;
-        d.mat[2 * q] = (const double *)nd.left;
-        d.mat[2 * q + 1] = (const double *)nd.right;
+        d.mat[2 * q] = nd.left;
+        d.mat[2 * q + 1] = nd.right;
         d.sc[q] = nd.scaler;
         d.ss[q] = nd.scaler_sum;
       }
@@ -568,9 +568,8 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
               if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
           continue;
         }
-        hipError_t e = plfx::launch_plf_dna_septets(sb[k].data() + i, c, (const double *)EV, wgt,
-                                                    n, ctx->ws, ctx->max_blocks, s, k,
-                                                    (const double *)tipvec);
+        hipError_t e = plfx::launch_plf_dna_septets(dtype, sb[k].data() + i, c, EV, wgt, n,
+                                                    ctx->ws, ctx->max_blocks, s, k, tipvec);
         if (e != hipSuccess) return hip_fail(ctx, e, "fused three-level launch");
       }
       for (size_t i = 0; i < tb[k].size(); i += plfx::kMaxTriples) {

@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--exact", action="store_true",
                     help="protein: plf()'s separate multiply/add (bit-identical to the double loop)")
     ap.add_argument("--fuse", type=int, choices=[0, 1, 2], default=2,
-                    help="tree64 schedule (PLFX_FUSE): 2 fused three-level subtrees (f64) and "
+                    help="tree64 schedule (PLFX_FUSE): 2 fused three-level subtrees and "
                          "level pairs, 1 level pairs only, 0 one launch per level")
     ap.add_argument("--no-fuse", action="store_true", help="same as --fuse 0")
     ap.add_argument("--tips", action="store_true",
@@ -255,12 +255,10 @@ class Tree64Workload:
         # per node: read x1, x2, write x3, read wgt (scaler sums, no bytes); + lnL read of the root.
         # With coded tips a tip child reads 1 code byte instead of a CLV.  Fused level pairs:
         # A, B and their parent P in one pass -- 4 child reads + 3 writes + wgt.  Fused
-        # three-level subtrees (f64): 7 nodes in one pass -- 8 child reads + 7 writes + wgt.
+        # three-level subtrees: 7 nodes in one pass -- 8 child reads + 7 writes + wgt.
         clv_b, tip_b = 16 * esz, 1
         leaf = tip_b if a.tips else clv_b
         fuse = 0 if a.no_fuse else a.fuse
-        if fuse == 2 and esz == 4:
-            fuse = 1  # three-level subtrees are built for f64 only
         self.bytes_per_site = 3 * clv_b + 4
         if fuse == 2:  # levels 0-2 as 8 seven-node subtrees, levels 3-5 as one
             self.bytes_per_step = (8 * (8 * leaf + 7 * clv_b + 4) + (15 * clv_b + 4)

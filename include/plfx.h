@@ -206,7 +206,7 @@ int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void 
  * pointers (or NULL = no tips); a slot with tips[s] != NULL is a tip (clv[s] is
  * not read) and may not be an op's parent (tips: DNA only).  Each level is
  * issued as up to three batched launches (tip/tip, tip/inner, inner/inner),
- * three-level subtrees (f64) and level pairs fused where possible
+ * three-level subtrees and level pairs fused where possible
  * (bit-identical results; env PLFX_FUSE=1 pairs only, 0 none).  states 4 or 20; flags as
  * plfx_plf_dev_gen (PLFX_FMA: protein nodes on the f64 matrix cores; DNA is
  * always exact).  plfx_traverse == flags PLFX_EXACT, no tips, no tipvec. */

@@ -67,13 +67,15 @@ int main(int argc, char **argv) {
     const SeptetDesc &d = sb.d[t];
     for (int i = 0; i < 2; i++) {
       TripleDesc &x = (2 * t + i < kMaxTriples ? tb0.d[2 * t + i] : tb1.d[2 * t + i - kMaxTriples]);
+      auto M = [&](int j) { return static_cast<const double *>(d.mat[j]); };
       x = TripleDesc{d.g[4 * i], d.g[4 * i + 1], d.g[4 * i + 2], d.g[4 * i + 3],
                      d.x[2 * i], d.x[2 * i + 1], d.x[4 + i],
-                     d.mat[4 * i], d.mat[4 * i + 1], d.mat[4 * i + 2], d.mat[4 * i + 3],
-                     d.mat[8 + 2 * i], d.mat[9 + 2 * i],
+                     M(4 * i), M(4 * i + 1), M(4 * i + 2), M(4 * i + 3),
+                     M(8 + 2 * i), M(9 + 2 * i),
                      nullptr, nullptr, nullptr, d.ss[2 * i], d.ss[2 * i + 1], d.ss[4 + i]};
     }
-    nr.d[t] = NodeDesc{d.x[4], d.x[5], d.x[6], d.mat[12], d.mat[13], nullptr, d.ss[6]};
+    nr.d[t] = NodeDesc{d.x[4], d.x[5], d.x[6], static_cast<const double *>(d.mat[12]),
+                       static_cast<const double *>(d.mat[13]), nullptr, d.ss[6]};
   }
   auto occ = [&](const void *k) { int b = 0; CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, 256, 0)); return b; };
   struct V { std::string name; double bytes; std::function<void()> run; std::vector<float> us; };
