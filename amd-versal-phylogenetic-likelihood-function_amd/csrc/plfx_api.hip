@@ -19,6 +19,8 @@
 #include "plf_kernels.hpp"
 #include "testbench.hpp"
 
+constexpr int kHostChunksMax = 16;
+
 struct plfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -30,6 +32,9 @@ struct plfx_ctx {
   // grow-only staging for the synchronous host entry points
   void *d_buf = nullptr;
   size_t d_cap = 0;
+  // host entry pipelining: D2H of chunk i on its own stream while chunk i+1 uploads
+  hipStream_t d2h_stream = nullptr;
+  hipEvent_t chunk_done[kHostChunksMax] = {};
   std::string err;
 };
 
@@ -110,8 +115,12 @@ int ensure_dbuf(plfx_ctx *ctx, size_t bytes) {
 
 size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-// plf()-shaped synchronous host entry: H2D -> fused kernel -> D2H
-// (the reference's hm / msm / mh regions, host_mem.cpp:293-318).
+// plf()-shaped synchronous host entry (the reference's hm / msm / mh regions,
+// host_mem.cpp:293-318): H2D -> fused kernel -> D2H, pipelined over up to
+// kHostChunksMax site chunks -- chunk i's results go back on a second stream
+// while chunk i+1 uploads, so the two PCIe directions overlap (the reference
+// overlaps its two uploads and its two downloads, host_mem.cpp:297-314).  The
+// chunks are independent sites; the scaler sum is the sum of the chunk sums.
 template <typename T>
 int plf_host(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int n, const T *left,
              const T *right, const int *wgt, int *scalerIncrement) {
@@ -119,34 +128,59 @@ int plf_host(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int n,
   if (n < 0) return fail(ctx, PLFX_ERR_INVALID, "n < 0 (%d)", n);
   if (n > 0 && (!x1 || !x2 || !x3 || !EV || !left || !right))
     return fail(ctx, PLFX_ERR_INVALID, "null argument");
+  constexpr int64_t kMinChunk = 1 << 17;  // sites; smaller chunks pay per-copy overheads
+  const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(kHostChunksMax, n / kMinChunk));
+  const int64_t chunk = ((int64_t)n + nch - 1) / nch;
   const size_t clv = (size_t)n * 16 * sizeof(T);
   const size_t o_x1 = 0, o_x2 = round_up(clv, 256), o_x3 = o_x2 + round_up(clv, 256);
   const size_t o_mat = o_x3 + round_up(clv, 256);  // EV 16 | left 64 | right 64
   const size_t o_wgt = o_mat + round_up(144 * sizeof(T), 256);
-  const size_t o_sum = o_wgt + round_up((size_t)n * sizeof(int32_t), 256);
-  const size_t total = o_sum + 256;
+  const size_t o_sum = o_wgt + round_up((size_t)n * sizeof(int32_t), 256);  // int64 per chunk
+  const size_t total = o_sum + round_up(kHostChunksMax * sizeof(int64_t), 256);
   int rc = ensure_dbuf(ctx, total);
   if (rc != PLFX_OK) return rc;
+  if (!ctx->d2h_stream) {
+    PLFX_HIP(ctx, hipStreamCreateWithFlags(&ctx->d2h_stream, hipStreamNonBlocking));
+    for (hipEvent_t &e : ctx->chunk_done) PLFX_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   char *d = static_cast<char *>(ctx->d_buf);
-  hipStream_t s = ctx->stream;
+  hipStream_t s = ctx->stream, s2 = ctx->d2h_stream;
+  const T *dm = reinterpret_cast<const T *>(d + o_mat);
+  int64_t *dsum = reinterpret_cast<int64_t *>(d + o_sum);
   if (n > 0) {
-    PLFX_HIP(ctx, hipMemcpyAsync(d + o_x1, x1, clv, hipMemcpyHostToDevice, s));
-    PLFX_HIP(ctx, hipMemcpyAsync(d + o_x2, x2, clv, hipMemcpyHostToDevice, s));
     PLFX_HIP(ctx, hipMemcpyAsync(d + o_mat, EV, 16 * sizeof(T), hipMemcpyHostToDevice, s));
     PLFX_HIP(ctx, hipMemcpyAsync(d + o_mat + 16 * sizeof(T), left, 64 * sizeof(T), hipMemcpyHostToDevice, s));
     PLFX_HIP(ctx, hipMemcpyAsync(d + o_mat + 80 * sizeof(T), right, 64 * sizeof(T), hipMemcpyHostToDevice, s));
-    if (wgt) PLFX_HIP(ctx, hipMemcpyAsync(d + o_wgt, wgt, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, s));
   }
-  const T *dm = reinterpret_cast<const T *>(d + o_mat);
-  rc = plf_dev<T>(ctx, reinterpret_cast<const T *>(d + o_x1), reinterpret_cast<const T *>(d + o_x2),
-                  reinterpret_cast<T *>(d + o_x3), dm, n, dm + 16, dm + 80,
-                  wgt ? reinterpret_cast<const int32_t *>(d + o_wgt) : nullptr, nullptr,
-                  reinterpret_cast<int64_t *>(d + o_sum), s);
-  if (rc != PLFX_OK) return rc;
-  int64_t sum = 0;
-  if (n > 0) PLFX_HIP(ctx, hipMemcpyAsync(x3, d + o_x3, clv, hipMemcpyDeviceToHost, s));
-  PLFX_HIP(ctx, hipMemcpyAsync(&sum, d + o_sum, sizeof sum, hipMemcpyDeviceToHost, s));
+  int used = 0;
+  for (int64_t lo = 0; lo < n || (n == 0 && used == 0); lo += chunk, used++) {
+    const int64_t m = std::min<int64_t>(chunk, n - lo);
+    const size_t off = (size_t)lo * 16 * sizeof(T), bytes = (size_t)m * 16 * sizeof(T);
+    if (m > 0) {
+      PLFX_HIP(ctx, hipMemcpyAsync(d + o_x1 + off, x1 + lo * 16, bytes, hipMemcpyHostToDevice, s));
+      PLFX_HIP(ctx, hipMemcpyAsync(d + o_x2 + off, x2 + lo * 16, bytes, hipMemcpyHostToDevice, s));
+      if (wgt)
+        PLFX_HIP(ctx, hipMemcpyAsync(d + o_wgt + lo * 4, wgt + lo, (size_t)m * 4, hipMemcpyHostToDevice, s));
+    }
+    rc = plf_dev<T>(ctx, reinterpret_cast<const T *>(d + o_x1 + off),
+                    reinterpret_cast<const T *>(d + o_x2 + off), reinterpret_cast<T *>(d + o_x3 + off),
+                    dm, std::max<int64_t>(m, 0), dm + 16, dm + 80,
+                    wgt ? reinterpret_cast<const int32_t *>(d + o_wgt + lo * 4) : nullptr, nullptr,
+                    dsum + used, s);
+    if (rc != PLFX_OK) return rc;
+    if (m > 0) {
+      PLFX_HIP(ctx, hipEventRecord(ctx->chunk_done[used], s));
+      PLFX_HIP(ctx, hipStreamWaitEvent(s2, ctx->chunk_done[used], 0));
+      PLFX_HIP(ctx, hipMemcpyAsync(x3 + lo * 16, d + o_x3 + off, bytes, hipMemcpyDeviceToHost, s2));
+    }
+    if (n == 0) break;
+  }
+  int64_t sums[kHostChunksMax] = {};
+  PLFX_HIP(ctx, hipMemcpyAsync(sums, dsum, (size_t)used * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   PLFX_HIP(ctx, hipStreamSynchronize(s));
+  PLFX_HIP(ctx, hipStreamSynchronize(s2));
+  int64_t sum = 0;
+  for (int i = 0; i < used; i++) sum += sums[i];
   if (scalerIncrement) *scalerIncrement = (int)sum;
   return PLFX_OK;
 }
@@ -250,6 +284,12 @@ int plfx_ctx_destroy(plfx_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->d_buf) (void)hipFree(ctx->d_buf);
+  if (ctx->d2h_stream) {
+    (void)hipStreamSynchronize(ctx->d2h_stream);
+    (void)hipStreamDestroy(ctx->d2h_stream);
+  }
+  for (hipEvent_t e : ctx->chunk_done)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->lnl_partials) (void)hipFree(ctx->lnl_partials);
   if (ctx->lnl_ticket) (void)hipFree(ctx->lnl_ticket);

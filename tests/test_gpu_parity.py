@@ -93,9 +93,13 @@ def test_plf_f32_edge_sites(ctx):
     assert np.array_equal(bits(o3.cpu().numpy()), bits(g["x3"]))
 
 
-@pytest.mark.parametrize("n", [0, 1, 3, 15, 16, 17, 63, 64, 65, 127, 129, 1000, 4097, 65537])
+@pytest.mark.parametrize("n", [0, 1, 3, 15, 16, 17, 63, 64, 65, 127, 129, 1000, 4097, 65537,
+                               (1 << 18) + 37, (1 << 20) + 5, (1 << 21) + 3])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_plf_host_ragged_sizes(ctx, oracle, n, dtype):
+    """The host-array entry (plf()'s shape) at ragged sizes, including sizes that
+    it pipelines in 2, 8 and 16 site chunks (H2D of one chunk while the previous
+    one downloads): x3 and the scaler sum bit-exact against the oracle."""
     d = oracle.gen_hostmem(max(n, 1), dtype, 11 + n)
     w = ((np.arange(max(n, 1)) * 13) % 9).astype(np.int32)
     x3 = np.full(16 * max(n, 1), 7.0, dtype)
