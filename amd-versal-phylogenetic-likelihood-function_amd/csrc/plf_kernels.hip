@@ -138,7 +138,16 @@ hipError_t launch_lnl_t(const T *x, int64_t n, const double *catw, const double 
                         unsigned long long *ticket, double *out, double *site_lnl, hipStream_t s) {
   static int cache = 0;
   auto kernel = &dev::root_lnl_kernel<T, S, C>;
-  int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 64, 1, 0);  // C steps of 64/C sites
+  // C steps of 64/C sites per wave trip; 2 blocks per CU (more trips per wave: the
+  // kernel is short and its ramp and final reduction weigh; tools/ab_lnl.hip)
+  int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 64, 1, 0);
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  if (cus > 0 && gx > 2 * (int64_t)cus) gx = 2 * (int64_t)cus;
   if (gx > kLnlMaxGrid) gx = kLnlMaxGrid;
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, x, n, catw, freq, wgt, sums,
                      nsums, partials, ticket, out, site_lnl);

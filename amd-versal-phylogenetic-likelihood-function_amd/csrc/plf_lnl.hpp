@@ -52,33 +52,37 @@ root_lnl_kernel(const T *__restrict__ x, int64_t n, const double *__restrict__ c
   double acc = 0.0;
   const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * SPW * C;
+  const int64_t nlast = n - 1;
   for (int64_t base = wave * SPW * C; base < n; base += stride) {
+    // every load of the trip first and unconditionally (clamped to the last site,
+    // results unused past n), the weight of this lane's log site with them: one
+    // memory latency per trip (a conditional weight load after the math was a
+    // second one, and the kernel runs only a few trips per wave)
     T v[C][S];
 #pragma unroll
     for (int u = 0; u < C; u++) {
       const int64_t site = base + u * SPW + q;
-      if (site < n) {
-        const T *xs = x + site * V + c * S;  // 16-B aligned: S*sizeof(T) is a multiple of 16
-        if constexpr (sizeof(T) == 8) {
+      const T *xs = x + (site < n ? site : nlast) * V + c * S;  // 16-B aligned: S*sizeof(T) % 16 == 0
+      if constexpr (sizeof(T) == 8) {
 #pragma unroll
-          for (int s = 0; s < S; s += 2) {
-            const f64x2 w = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(xs + s));
-            v[u][s] = w.x;
-            v[u][s + 1] = w.y;
-          }
-        } else {
-#pragma unroll
-          for (int s = 0; s < S; s += 4) {
-            const f32x4 w = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(xs + s));
-            v[u][s] = w.x; v[u][s + 1] = w.y; v[u][s + 2] = w.z; v[u][s + 3] = w.w;
-          }
+        for (int s = 0; s < S; s += 2) {
+          const f64x2 w = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(xs + s));
+          v[u][s] = w.x;
+          v[u][s + 1] = w.y;
         }
       } else {
 #pragma unroll
-        for (int s = 0; s < S; s++) v[u][s] = T(0);
+        for (int s = 0; s < S; s += 4) {
+          const f32x4 w = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(xs + s));
+          v[u][s] = w.x; v[u][s + 1] = w.y; v[u][s + 2] = w.z; v[u][s + 3] = w.w;
+        }
       }
     }
-    double mine = 1.0;  // L of step c's site (this lane's log)
+    const int64_t site = base + c * SPW + q;  // this lane's log site (step c)
+    const bool valid = site < n;
+    const int wv = wgt_at(wgt, valid ? site : nlast, partials);
+    __builtin_amdgcn_sched_barrier(0);  // keeps the weight load with the CLV loads
+    double mine = 1.0;  // L of step c's site
 #pragma unroll
     for (int u = 0; u < C; u++) {
       double t = 0.0;
@@ -89,11 +93,10 @@ root_lnl_kernel(const T *__restrict__ x, int64_t n, const double *__restrict__ c
       for (int k = 0; k < C; k++) L += cw[k] * __shfl(t, (lane / C) * C + k);
       if (u == c) mine = L;
     }
-    const int64_t site = base + c * SPW + q;
-    if (site < n) {
+    if (valid) {
       const double l = log(mine);
       if (site_lnl) site_lnl[site] = l;
-      acc += (wgt ? (double)wgt[site] : 1.0) * l;
+      acc += (double)wv * l;
     }
   }
   // fixed-order block reduction
