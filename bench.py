@@ -509,6 +509,14 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None
+        ttp = Path(a.traffic_json).with_name(Path(a.traffic_json).name.replace("pmc_traffic", "tree_pmc_traffic"))
+        if a.workload == "tree64" and ttp.exists():  # per step (all of the step's launches)
+            try:
+                tj = json.loads(ttp.read_text())
+                if abs(tj.get("algorithmic_bytes_per_step", 0) - wl.bytes_per_step) < 1:
+                    traffic = tj.get("hbm_bytes_per_step")
+            except (ValueError, OSError):
+                traffic = None
         value = world * wl.sites_per_step * a.steps / (wall_ms * 1e-3)
         cfg = dict(wl.config)
         par = (f"alignment sites sharded x{world} (each GPU sweeps the whole tree over its "
@@ -538,6 +546,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "bytes_per_site": wl.bytes_per_site,
+                "bytes_per_step": wl.bytes_per_step,
                 "kernel_avg_us": per_step_ms * 1e3,
             },
             "check": "ok" if check_ok else "CHECK_FAILED",

@@ -30,3 +30,13 @@ step prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/prof_fetch -o run --ou
 step prof_write 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/prof_write -o run --output-format csv -- python3 $R/bench.py --steps 40 --warmup 4 --no-cpu-baseline --launch bound
 find $OUT/prof_trace $OUT/prof_fetch $OUT/prof_write -name "*.csv" | head -20
 python3 $R/tools/pmc_traffic.py $OUT/prof_fetch/run_counter_collection.csv $OUT/prof_write/run_counter_collection.csv $OUT/pmc_traffic.json > /dev/null && echo traffic ok
+# tree64 (configs[2], fused three-level subtrees): kernel trace and the two PMC passes
+TREE="$R/bench.py --workload tree64 --no-cpu-baseline"
+step tree_bench 300 python $TREE --steps 50 --warmup 5
+tail -1 $OUT/tree_bench.log
+step tree_trace 300 rocprofv3 --kernel-trace --stats -T -d $OUT/tree_trace -o run --output-format csv -- python3 $TREE --steps 50 --warmup 5
+step tree_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/tree_fetch -o run --output-format csv -- python3 $TREE --steps 20 --warmup 2 --launch bound
+step tree_write 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/tree_write -o run --output-format csv -- python3 $TREE --steps 20 --warmup 2 --launch bound
+ALG=$(python3 -c "import json; d=json.loads(open('$OUT/tree_bench.log').read().strip().splitlines()[-1]); print(d['roofline']['bytes_per_step'])")
+python3 $R/tools/pmc_step.py $OUT/tree_fetch/run_counter_collection.csv $OUT/tree_write/run_counter_collection.csv $OUT/tree_pmc_traffic.json --steps 22 --alg-bytes $ALG > /dev/null && echo tree traffic ok
+

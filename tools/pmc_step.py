@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""HBM traffic of one bench step from two rocprofv3 PMC passes (FETCH_SIZE,
+WRITE_SIZE), for multi-kernel steps (tree64): the PLF kernels' dispatches
+(the two fused launches of a step share a total grid size, so they are told
+apart by neither name nor grid) are summed per kernel name, corrected as
+MI355X_MICROARCH.md's HBM section prescribes (x1024; FETCH_SIZE x2 for 16-B/lane
+streaming reads, which these kernels' CLV traffic is), and divided by the
+profiled steps (warm-up included).
+
+usage: tools/pmc_step.py FETCH_CSV WRITE_CSV OUT_JSON --steps K --alg-bytes B
+  (K = steps profiled incl. warm-up, B = algorithmic bytes per step from the
+  bench JSON: bytes_per_site x sites, or roofline.achieved x ms_per_step)
+"""
+import argparse
+import collections
+import csv
+import json
+import statistics as st
+
+
+PLF_KERNELS = ("plf_dna", "root_lnl", "plf_prot", "pmatrix")
+
+
+def groups(path, name):
+    g = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != name or not r["Kernel_Name"].startswith(PLF_KERNELS):
+            continue
+        g[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+    return g
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("out")
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--alg-bytes", type=float, required=True)
+    a = ap.parse_args()
+    fg, wg = groups(a.fetch, "FETCH_SIZE"), groups(a.write, "WRITE_SIZE")
+    rows, tot = [], 0.0
+    for key in sorted(set(fg) & set(wg)):
+        f = sum(fg[key]) * 1024 * 2 / a.steps
+        w = sum(wg[key]) * 1024 / a.steps
+        tot += f + w
+        rows.append({"kernel": key, "dispatches": len(fg[key]), "per_step": len(fg[key]) / a.steps,
+                     "hbm_read_bytes_per_step": f, "hbm_write_bytes_per_step": w,
+                     "fetch_KiB_per_dispatch": sorted(set(round(v) for v in fg[key]))[:8]})
+    rec = {"groups": rows, "hbm_bytes_per_step": tot, "algorithmic_bytes_per_step": a.alg_bytes,
+           "traffic_over_algorithmic": tot / a.alg_bytes,
+           "correction": "FETCH_SIZE x1024 x2, WRITE_SIZE x1024 (MI355X_MICROARCH.md, HBM section)"}
+    json.dump(rec, open(a.out, "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
