@@ -46,6 +46,8 @@ constexpr bool kNt = true;   // f32: NT CLV loads (74.8% vs 70.2% of HBM peak, r
 constexpr bool kNtl64 = true;
 constexpr int kMinWaves = 1;
 constexpr int kTripleU = 1;  // fused level pairs: 16 sites per trip (tools/tune_triple.hip)
+constexpr int kTripleUTips = 2;  // with coded tips: 32 sites per trip (+13-19 % for 2 tip
+                                 // children, equal for 1; profiles/r01_ab_fused_tips.log)
 constexpr int kTripleU32 = 2;
 // fused three-level subtrees: 2 x 8-site blocks per trip, matrices re-read from
 // LDS, next trip's loads in flight (tools/tune_septet.hip, r01_tune_septet.log)
@@ -200,7 +202,7 @@ hipError_t launch_triples_t(const dev::TripleBatch &b, int count, const double *
                             const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
                             hipStream_t s, const double *tipvec) {
   static int cache = 0;
-  constexpr int U = kTripleU;
+  constexpr int U = kTips ? kTripleUTips : kTripleU;
   auto kernel = &dev::plf_dna_f64_triple_kernel<kSum, 1, kNtl64, kTips, U>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 16 * U, count,
                             max_blocks);
@@ -228,7 +230,9 @@ hipError_t launch_septets_t(const dev::SeptetBatch &b, int count, const double *
                             const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
                             hipStream_t s, const double *tipvec) {
   static int cache = 0;
-  auto kernel = &dev::plf_dna_f64_septet_kernel<kSum, 1, kNtl64, kTips, true, kSeptetU, true>;
+  // next-trip prefetch for dense leaves only: with coded leaves the pass is
+  // write-bound and the prefetch registers cost 4-4.5 % (r01_ab_fused_tips.log)
+  auto kernel = &dev::plf_dna_f64_septet_kernel<kSum, 1, kNtl64, kTips, true, kSeptetU, kTips == 0>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 8 * kSeptetU, count,
                             max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt,
