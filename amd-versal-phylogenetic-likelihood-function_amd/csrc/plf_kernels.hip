@@ -156,45 +156,63 @@ hipError_t launch_lnl_t(const T *x, int64_t n, const double *catw, const double 
   return hipGetLastError();
 }
 
-template <typename T, bool kFma, bool kSum>
-hipError_t launch_prot_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
+template <typename T, bool kFma, bool kSum, int kTips>
+hipError_t launch_prot_t(const DnaArgs &a, int max_blocks, hipStream_t s, const T *tipvec) {
   static int cache = 0;
-  auto kernel = &dev::plf_prot_kernel<T, kFma, kSum>;
+  auto kernel = &dev::plf_prot_kernel<T, kFma, kSum, 0, 2, kTips>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
                      (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,
-                     (const T *)a.right, a.wgt, a.scaler, a.n, a.ws, a.scaler_sum);
+                     (const T *)a.right, a.wgt, a.scaler, a.n, a.ws, a.scaler_sum, tipvec);
   return hipGetLastError();
 }
 
-template <typename T, bool kFma>
-hipError_t launch_prot_s(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  return a.scaler_sum ? launch_prot_t<T, kFma, true>(a, max_blocks, s)
-                      : launch_prot_t<T, kFma, false>(a, max_blocks, s);
-}
-
-template <bool kSum>
-hipError_t launch_prot_mfma_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
+template <bool kSum, int kTips>
+hipError_t launch_prot_mfma_t(const DnaArgs &a, int max_blocks, hipStream_t s,
+                              const double *tipvec) {
   static int cache = 0;
-  auto kernel = &dev::plf_prot_mfma_kernel<kSum>;
+  auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, true, 0, true, kTips>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV,
                      (const double *)a.left, (const double *)a.right, a.wgt, a.scaler, a.n, a.ws,
-                     a.scaler_sum);
+                     a.scaler_sum, tipvec);
   return hipGetLastError();
 }
 
-template <bool kSum>
-hipError_t launch_prot_exact64_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
+template <bool kSum, int kTips>
+hipError_t launch_prot_exact64_t(const DnaArgs &a, int max_blocks, hipStream_t s,
+                                 const double *tipvec) {
   static int cache = 0;
-  auto kernel = &dev::plf_prot_exact_f64_kernel<kSum>;
+  auto kernel = &dev::plf_prot_exact_f64_kernel<kSum, 2, kTips>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV,
                      (const double *)a.left, (const double *)a.right, a.wgt, a.scaler, a.n, a.ws,
-                     a.scaler_sum);
+                     a.scaler_sum, tipvec);
   return hipGetLastError();
+}
+
+// dtype x mode x scaler-sum x tips dispatch of the protein kernels
+template <int kTips>
+hipError_t launch_prot_tips(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s,
+                            const void *tipvec) {
+  const bool sum = a.scaler_sum != nullptr;
+  const double *V64 = (const double *)tipvec;
+  const float *V32 = (const float *)tipvec;
+  if (dtype == 1) {
+    if (fma)  // matrix cores: bit-identical to the fused VALU chain (plf_prot.hpp)
+      return sum ? launch_prot_mfma_t<true, kTips>(a, max_blocks, s, V64)
+                 : launch_prot_mfma_t<false, kTips>(a, max_blocks, s, V64);
+    // exact: matrices broadcast from LDS (plf_prot.hpp)
+    return sum ? launch_prot_exact64_t<true, kTips>(a, max_blocks, s, V64)
+               : launch_prot_exact64_t<false, kTips>(a, max_blocks, s, V64);
+  }
+  if (fma)
+    return sum ? launch_prot_t<float, true, true, kTips>(a, max_blocks, s, V32)
+               : launch_prot_t<float, true, false, kTips>(a, max_blocks, s, V32);
+  return sum ? launch_prot_t<float, false, true, kTips>(a, max_blocks, s, V32)
+             : launch_prot_t<float, false, false, kTips>(a, max_blocks, s, V32);
 }
 
 template <bool kSum, int kTips>
@@ -312,17 +330,14 @@ hipError_t launch_plf_dna_triples(int dtype, const TripleDescH *t, int count, co
   }
 }
 
-hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s) {
-  if (dtype == 1) {
-    if (fma)  // matrix cores: bit-identical to the fused VALU chain (plf_prot.hpp)
-      return a.scaler_sum ? launch_prot_mfma_t<true>(a, max_blocks, s)
-                          : launch_prot_mfma_t<false>(a, max_blocks, s);
-    // exact: matrices broadcast from LDS (plf_prot.hpp)
-    return a.scaler_sum ? launch_prot_exact64_t<true>(a, max_blocks, s)
-                        : launch_prot_exact64_t<false>(a, max_blocks, s);
+hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s,
+                           int tips, const void *tipvec) {
+  switch (tips) {
+    case 0: return launch_prot_tips<0>(dtype, fma, a, max_blocks, s, tipvec);
+    case 1: return launch_prot_tips<1>(dtype, fma, a, max_blocks, s, tipvec);
+    case 2: return launch_prot_tips<2>(dtype, fma, a, max_blocks, s, tipvec);
+    default: return hipErrorInvalidValue;
   }
-  return fma ? launch_prot_s<float, true>(a, max_blocks, s)
-             : launch_prot_s<float, false>(a, max_blocks, s);
 }
 
 hipError_t launch_plf_dna_f32(const DnaArgs &a, int max_blocks, hipStream_t s) {

@@ -27,7 +27,8 @@ hipError_t launch_plf_dna_f64(const DnaArgs &a, int max_blocks, hipStream_t s);
 
 // sum_j scaler[j]*wgt[j] (host_mem.cpp:384-388), self-resetting ws as above.
 // Protein (S=20, C=4) kernel; fma selects fused multiply-add.
-hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s);
+hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s,
+                           int tips = 0, const void *tipvec = nullptr);
 
 // Batched nodes (<= kMaxBatch per launch) sharing EV, n, wgt.  dtype: 0 f32, 1 f64.
 // tips: 0 dense children; 1 x1 of every node is a tip (uint8 state codes);

@@ -211,18 +211,61 @@ __device__ __forceinline__ void row_write(typename ProtTile<T>::V *lds, int site
   }
 }
 
+// ---------------------------------------------------------------------------
+// Protein tips (extension of SURVEY section 8f row 4 to S = 20): a leaf is one
+// uint8 code per site, index into a table of kProtCodes dense rows of 20 values
+// (tipvec, codes x 20, device, dtype of the CLVs), codes >= kProtCodes read row
+// kProtCodes-1.  Default table (tipvec == NULL), states in ARNDCQEGHILKMFPSTWYV
+// order: codes 0..19 one state, 20 = B (N|D), 21 = Z (Q|E), 22 = X / unknown,
+// 23 = gap (all states).  A tip child's ump[c][k] = sum_l tv[code][l] * P_c[k][l]
+// (ascending l from +0.0, the kernel's multiply-add) comes from a per-block LDS
+// table built with exactly plf()'s operations on the expanded row, so results
+// are bit-identical to plf() on the dense CLV x[i][c][s] = tv[code_i][s].
+constexpr int kProtCodes = 24;
+
+template <typename T>
+__device__ __forceinline__ T prot_tip_value(const T *tipvec, int code, int l) {
+  if (tipvec) return tipvec[code * 20 + l];
+  if (code < 20) return l == code ? T(1) : T(0);
+  if (code == 20) return (l == 2 || l == 3) ? T(1) : T(0);  // B = N | D
+  if (code == 21) return (l == 5 || l == 6) ? T(1) : T(0);  // Z = Q | E
+  return T(1);                                               // X, gap
+}
+
+__device__ __forceinline__ int prot_code(uint8_t v) { return v < kProtCodes ? v : kProtCodes - 1; }
+
+// tab[c * kProtCodes * 20 + code * 20 + k] for the 4 categories of P (C x 400)
+template <typename T, bool kFma>
+__device__ void build_prot_tip_table(const T *__restrict__ P, const T *__restrict__ tipvec,
+                                     T *tab) {
+  for (int e = threadIdx.x; e < 4 * kProtCodes * 20; e += kBlock) {
+    const int c = e / (kProtCodes * 20), r = e % (kProtCodes * 20), code = r / 20, k = r % 20;
+    T u = T(0);
+#pragma unroll 4
+    for (int l = 0; l < 20; l++) u = madd<T, kFma>(prot_tip_value<T>(tipvec, code, l), P[c * 400 + k * 20 + l], u);
+    tab[e] = u;
+  }
+}
+
 // kAblate (tuning only, tools/tune_plf.hip): 0 = the kernel; 1 = skip the
 // arithmetic (o = a + b); 2 = skip the child-tile traffic (a, b synthesised).
-template <typename T, bool kFma, bool kSum, int kAblate = 0, int kMinWaves = 2>
+// kTips: 1 = x1 is a tip (uint8 codes), 2 = both children are tips.
+template <typename T, bool kFma, bool kSum, int kAblate = 0, int kMinWaves = 2, int kTips = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
                 const T *__restrict__ EV, const T *__restrict__ left, const T *__restrict__ right,
                 const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                unsigned long long *ws, int64_t *scaler_sum) {
+                unsigned long long *ws, int64_t *scaler_sum, const T *__restrict__ tipvec = nullptr) {
   constexpr int S = 20;
+  constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
   using PT = ProtTile<T>;
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform category
   const int lane = threadIdx.x & 63;
+  __shared__ T tabs[(T1 ? 1 : 0) + (T2 ? 1 : 0) + (T1 ? 0 : 1)][T1 ? 4 * kProtCodes * 20 : 1];
+  if constexpr (T1) build_prot_tip_table<T, kFma>(left, tipvec, tabs[0]);
+  if constexpr (T2) build_prot_tip_table<T, kFma>(right, tipvec, tabs[1]);
+  if constexpr (T1) __syncthreads();
+  const T *tabL = tabs[0] + c * kProtCodes * 20, *tabR = tabs[T2 ? 1 : 0] + c * kProtCodes * 20;
   constexpr int R = (S * S + 63) / 64;  // registers per lane-distributed matrix
   T ML[R], MR[R], ME[R];
 #pragma unroll
@@ -240,27 +283,36 @@ plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restric
     const int64_t site = base + lane;
     const bool valid = site < n;
     T a[S], b[S], o[S];
+    const int64_t sq = valid ? site : n - 1;
+    const int code1 = T1 ? prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) : 0;
+    const int code2 = T2 ? prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) : 0;
     if constexpr (kAblate == 2) {
 #pragma unroll
       for (int l = 0; l < S; l++) { a[l] = T(site + l) * T(1e-3); b[l] = T(lane + l) * T(1e-3); }
     } else {
-      tile_load<T>(x1, base, n, tile);
-      __syncthreads();
-      row_read<T>(tile, lane, c, a);
-      __syncthreads();
-      tile_load<T>(x2, base, n, tile);
-      __syncthreads();
-      row_read<T>(tile, lane, c, b);
+      if constexpr (!T1) {
+        tile_load<T>(x1, base, n, tile);
+        __syncthreads();
+        row_read<T>(tile, lane, c, a);
+        __syncthreads();
+      }
+      if constexpr (!T2) {
+        tile_load<T>(x2, base, n, tile);
+        __syncthreads();
+        row_read<T>(tile, lane, c, b);
+      }
     }
 #pragma unroll
     for (int l = 0; l < S; l++) o[l] = kAblate == 1 ? a[l] + b[l] : T(0);
 #pragma unroll
     for (int k = 0; k < (kAblate == 1 ? 0 : S); k++) {
       T u1 = T(0), u2 = T(0);
+      if constexpr (T1) u1 = tabL[code1 * 20 + k];
+      if constexpr (T2) u2 = tabR[code2 * 20 + k];
 #pragma unroll
       for (int l = 0; l < S; l++) {
-        u1 = madd<T, kFma>(a[l], bcast<T>(ML, k * S + l), u1);
-        u2 = madd<T, kFma>(b[l], bcast<T>(MR, k * S + l), u2);
+        if constexpr (!T1) u1 = madd<T, kFma>(a[l], bcast<T>(ML, k * S + l), u1);
+        if constexpr (!T2) u2 = madd<T, kFma>(b[l], bcast<T>(MR, k * S + l), u2);
       }
       const T p = u1 * u2;
 #pragma unroll
@@ -305,27 +357,35 @@ plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restric
 // that consumes the previous row's result pins that distance (left alone, the
 // compiler hoists a phase's 200 reads to its start and spills them), and an
 // opaque per-trip offset keeps the reads inside the site loop.
-template <bool kSum, int kMinWaves = 2>
+template <bool kSum, int kMinWaves = 2, int kTips = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                           double *__restrict__ x3, const double *__restrict__ EV,
                           const double *__restrict__ left, const double *__restrict__ right,
                           const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                          unsigned long long *ws, int64_t *scaler_sum) {
+                          unsigned long long *ws, int64_t *scaler_sum,
+                          const double *__restrict__ tipvec = nullptr) {
   constexpr int S = 20;
+  constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
+  __shared__ double tabs[(T1 ? 1 : 0) + (T2 ? 1 : 0) + (T1 ? 0 : 1)][T1 ? 4 * kProtCodes * 20 : 1];
+  if constexpr (T1) build_prot_tip_table<double, false>(left, tipvec, tabs[0]);
+  if constexpr (T2) build_prot_tip_table<double, false>(right, tipvec, tabs[1]);
   using PT = ProtTile<double>;
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  __shared__ f64x2 mats[(2 * 4 * S * S + S * S) / 2];  // P_L[4][400] | P_R[4][400] | EV[400]
+  // P_L[4][400] (unless x1 is a tip) | P_R[4][400] (unless x2 is a tip) | EV[400]:
+  // a tip child's matrix lives in its table instead (2 blocks per CU still fit)
+  constexpr int oR = T1 ? 0 : 800, oE = oR + (T2 ? 0 : 800);
+  __shared__ f64x2 mats[oE + 200];
   {
     const f64x2 *gl = reinterpret_cast<const f64x2 *>(left);
     const f64x2 *gr = reinterpret_cast<const f64x2 *>(right);
     const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
     for (int i = threadIdx.x; i < 800; i += kBlock) {
-      mats[i] = gl[i];
-      mats[800 + i] = gr[i];
+      if constexpr (!T1) mats[i] = gl[i];
+      if constexpr (!T2) mats[oR + i] = gr[i];
     }
-    for (int i = threadIdx.x; i < 200; i += kBlock) mats[1600 + i] = ge[i];
+    for (int i = threadIdx.x; i < 200; i += kBlock) mats[oE + i] = ge[i];
   }
   const double m = Num<double>::minlik();
   __shared__ PT::V tile[64 * PT::kStride];
@@ -354,9 +414,14 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
   for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
     int off = 0;
     asm volatile("" : "+v"(off));
-    const f64x2 *mL = mats + off + c * 200, *mR = mats + off + 800 + c * 200, *mE = mats + off + 1600;
+    const f64x2 *mL = mats + off + c * 200, *mR = mats + off + oR + c * 200, *mE = mats + off + oE;
     double U[S];
-    {
+    const int64_t sq = base + lane < n ? base + lane : n - 1;
+    if constexpr (T1) {  // tip: U from the table row of the site's code
+      const double *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
+#pragma unroll
+      for (int k = 0; k < S; k++) U[k] = r[k];
+    } else {
       double a[S];
       tile_load<double>(x1, base, n, tile);
       __syncthreads();
@@ -373,7 +438,11 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
         return u;
       });
     }
-    {
+    if constexpr (T2) {
+      const double *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
+#pragma unroll
+      for (int k = 0; k < S; k++) U[k] = U[k] * r[k];
+    } else {
       double b[S];
       tile_load<double>(x2, base, n, tile);
       __syncthreads();
@@ -453,14 +522,19 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 // kAblate (tuning only, tools/tune_prot.hip): 0 = the kernel; 1 = no matrix-core
 // work (VALU stand-ins keep the LDS reads); 2 = no HBM loads or stores.
-template <bool kSum, int kMinWaves = 2, bool kPrefetch = true, int kAblate = 0, bool kMix4 = true>
+template <bool kSum, int kMinWaves = 2, bool kPrefetch = true, int kAblate = 0, bool kMix4 = true,
+          int kTips = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                      double *__restrict__ x3, const double *__restrict__ EV,
                      const double *__restrict__ left, const double *__restrict__ right,
                      const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                     unsigned long long *ws, int64_t *scaler_sum) {
+                     unsigned long long *ws, int64_t *scaler_sum,
+                     const double *__restrict__ tipvec = nullptr) {
   constexpr int S = 20;
+  // tips (kTips 1: x1, 2: both): the child's U^T comes from its LDS table in the
+  // accumulator layout (lane: rows g + 4r and 16 + g of site lo16), no MFMA, no tile
+  constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
   using PT = ProtTile<double>;
   constexpr int kRow = 2 * PT::kStride;  // doubles per site in the LDS tile (82)
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -479,6 +553,16 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       AE[mt][st] = row < S ? EV[col * S + row] : 0.0;                // EV^T[l=row][k=col]
     }
   const double m = Num<double>::minlik();
+  __shared__ double tabs[(T1 ? 1 : 0) + (T2 ? 1 : 0) + (T1 ? 0 : 1)][T1 ? 4 * kProtCodes * 20 : 1];
+  if constexpr (T1) build_prot_tip_table<double, true>(left, tipvec, tabs[0]);
+  if constexpr (T2) build_prot_tip_table<double, true>(right, tipvec, tabs[1]);
+  if constexpr (T1) __syncthreads();
+  // U^T of a tip child for sub-tile t, in the MFMA accumulator layout
+  auto tip_u = [&](const double *tab, int code_lane, int t, f64x4 &u0, f64x4 &u1) {
+    const double *r = tab + c * kProtCodes * 20 + __shfl(code_lane, 16 * t + lo16) * 20;
+    u0 = f64x4{r[g], r[g + 4], r[g + 8], r[g + 12]};
+    u1 = f64x4{r[16 + g], 0.0, 0.0, 0.0};
+  };
   __shared__ f64x2 tile[64 * PT::kStride];
   __shared__ unsigned long long small_mask[kWavesPerBlock];
   const double *td = reinterpret_cast<const double *>(tile);
@@ -490,11 +574,17 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   const int64_t stride = (int64_t)gridDim.x * 64;
   if constexpr (kAblate == 2)
     for (auto &q : pf) q = f64x2{1.0, 1.0};
-  if constexpr (kPrefetch && kAblate != 2)
-    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(x1, (int64_t)blockIdx.x * 64, n, pf);
+  if constexpr (kPrefetch && kAblate != 2 && !T2)  // the first dense child's first tile
+    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
   for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
     f64x4 P[4][2];  // per sub-tile: U_L^T, then p = U_L^T * U_R^T
-    if constexpr (kPrefetch) {
+    const int64_t sq = base + lane < n ? base + lane : n - 1;
+    const int code1 = T1 ? prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) : 0;
+    const int code2 = T2 ? prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) : 0;
+    if constexpr (T1) {
+#pragma unroll
+      for (int t = 0; t < 4; t++) tip_u(tabs[0], code1, t, P[t][0], P[t][1]);
+    } else if constexpr (kPrefetch) {
       tile_put<double>(tile, pf);
       __syncthreads();
       if constexpr (kAblate != 2) tile_fetch<double>(x2, base, n, pf);
@@ -502,26 +592,38 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       tile_load<double>(x1, base, n, tile);
       __syncthreads();
     }
+    if constexpr (!T1) {
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
+      for (int t = 0; t < 4; t++) {
+        const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
 #pragma unroll
-      for (int mt = 0; mt < 2; mt++) {
-        f64x4 u = {0.0, 0.0, 0.0, 0.0};
+        for (int mt = 0; mt < 2; mt++) {
+          f64x4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int st = 0; st < 5; st++) {
-          if constexpr (kAblate == 1) u[st & 3] += xr[4 * st] * AL[mt][st];
-          else if (kMix4 && mt == 1) u[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(AL[1][st], xr[4 * st], u[0], 0, 0, 0);
-          else u = __builtin_amdgcn_mfma_f64_16x16x4f64(AL[mt][st], xr[4 * st], u, 0, 0, 0);
+          for (int st = 0; st < 5; st++) {
+            if constexpr (kAblate == 1) u[st & 3] += xr[4 * st] * AL[mt][st];
+            else if (kMix4 && mt == 1) u[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(AL[1][st], xr[4 * st], u[0], 0, 0, 0);
+            else u = __builtin_amdgcn_mfma_f64_16x16x4f64(AL[mt][st], xr[4 * st], u, 0, 0, 0);
+          }
+          P[t][mt] = u;
         }
-        P[t][mt] = u;
       }
+      __syncthreads();
     }
-    __syncthreads();
+    if constexpr (T2) {
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        f64x4 u0, u1;
+        tip_u(tabs[1], code2, t, u0, u1);
+        P[t][0] = P[t][0] * u0;  // prod[k] = umpL[k] * umpR[k]
+        P[t][1] = P[t][1] * u1;
+      }
+    } else {
     if constexpr (kPrefetch) {
       tile_put<double>(tile, pf);
       __syncthreads();
-      if (kAblate != 2 && base + stride < n) tile_fetch<double>(x1, base + stride, n, pf);
+      // next trip's first dense child: x1, or x2 when x1 is a tip
+      if (kAblate != 2 && base + stride < n) tile_fetch<double>(T1 ? x2 : x1, base + stride, n, pf);
     } else {
       tile_load<double>(x2, base, n, tile);
       __syncthreads();
@@ -542,6 +644,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       }
     }
     __syncthreads();  // every wave is done reading x2: the tile takes X3 now
+    }
     // back-transform: lane holds X3[site 16t+lo16][l = 16mt + g + 4r]; written
     // unscaled into the tile, the x2^32 rescale happens in the store pass
     unsigned long long mine = 0;

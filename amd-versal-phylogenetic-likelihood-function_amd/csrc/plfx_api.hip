@@ -215,7 +215,8 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
     for (int i = 0; i < count; i++) {
       const plfx_node &d = nodes[i];
       plfx::DnaArgs a{d.x1, d.x2, d.x3, EV, d.left, d.right, wgt, d.scaler, d.scaler_sum, ctx->ws, n};
-      hipError_t e = plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s);
+      hipError_t e = plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s,
+                                           tips, tipvec);
       if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot launch");
     }
     return PLFX_OK;
@@ -401,12 +402,16 @@ int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *no
   return batch_impl(ctx, dtype, nodes, count, EV, n, wgt, pick(ctx, stream), 0, nullptr, states);
 }
 
-int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void *x1,
-                      const uint8_t *tip2, const void *x2, void *x3, const void *EV, int64_t n,
-                      const void *left, const void *right, const int32_t *wgt, uint8_t *scaler,
-                      int64_t *scaler_sum, const void *tipvec, void *stream) {
+int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const uint8_t *tip1,
+                          const void *x1, const uint8_t *tip2, const void *x2, void *x3,
+                          const void *EV, int64_t n, const void *left, const void *right,
+                          const int32_t *wgt, uint8_t *scaler, int64_t *scaler_sum,
+                          const void *tipvec, void *stream) {
   if (!ctx) return PLFX_ERR_INVALID;
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if (states != 4 && states != 20)
+    return fail(ctx, PLFX_ERR_UNSUPPORTED, "states=%d not built (4, 20)", states);
+  if (flags & ~PLFX_FMA) return fail(ctx, PLFX_ERR_INVALID, "bad flags %d", flags);
   if ((tip1 != nullptr) == (x1 != nullptr) || (tip2 != nullptr) == (x2 != nullptr))
     return fail(ctx, PLFX_ERR_INVALID, "each child needs exactly one of tip / CLV");
   plfx_node nd{tip1 ? (const void *)tip1 : x1, tip2 ? (const void *)tip2 : x2, x3, left, right,
@@ -416,7 +421,15 @@ int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void 
     std::swap(nd.x1, nd.x2);
     std::swap(nd.left, nd.right);
   }
-  return batch_impl(ctx, dtype, &nd, 1, EV, n, wgt, pick(ctx, stream), tips, tipvec);
+  return batch_impl(ctx, dtype, &nd, 1, EV, n, wgt, pick(ctx, stream), tips, tipvec, states, flags);
+}
+
+int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void *x1,
+                      const uint8_t *tip2, const void *x2, void *x3, const void *EV, int64_t n,
+                      const void *left, const void *right, const int32_t *wgt, uint8_t *scaler,
+                      int64_t *scaler_sum, const void *tipvec, void *stream) {
+  return plfx_plf_tips_dev_gen(ctx, dtype, 4, PLFX_EXACT, tip1, x1, tip2, x2, x3, EV, n, left,
+                               right, wgt, scaler, scaler_sum, tipvec, stream);
 }
 
 int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops, int nops,
@@ -440,9 +453,6 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   if (flags & ~PLFX_FMA) return fail(ctx, PLFX_ERR_INVALID, "bad flags %d", flags);
   if (nops < 0 || (nops > 0 && (!ops || !clv || !pmats || !EV)))
     return fail(ctx, PLFX_ERR_INVALID, "bad traverse arguments");
-  if (states != 4 && tips)
-    for (int sl = 0; sl < nslots; sl++)
-      if (tips[sl]) return fail(ctx, PLFX_ERR_UNSUPPORTED, "tip codes are DNA only (states=%d)", states);
   const size_t es = dtype == PLFX_F32 ? 4 : 8;
   const size_t mat = (size_t)states * states * 4;  // C*S*S values per matrix
   auto is_tip = [&](int sl) { return tips && tips[sl]; };

@@ -48,12 +48,13 @@ EXPORTS = (
     "plfx_tb_instance_active_elements_left", "plfx_tb_instance_active_elements_right",
     "plfx_tb_num_windows_per_instance", "plfx_pack_instance",
     "plfx_plf_batch_dev", "plfx_traverse", "plfx_root_lnl", "plfx_plf_dev_gen",
-    "plfx_plf_tips_dev", "plfx_traverse_tips",
+    "plfx_plf_tips_dev", "plfx_plf_tips_dev_gen", "plfx_traverse_tips",
     "plfx_model_eigen", "plfx_gamma_rates", "plfx_model_ev", "plfx_model_root_weights",
     "plfx_pmatrix", "plfx_model_tip_vectors",
 )
 PMAT_STATE, PMAT_EIGEN = 0, 1
 EXACT, FMA = 0, 1
+PROT_CODES = 24  # protein tip codes: rows of the tip-vector table (plfx.h section 8)
 
 
 class PlfxError(RuntimeError):
@@ -135,6 +136,8 @@ def load():
     L.plfx_model_tip_vectors.argtypes = [i32, i32, dp, dp]
     L.plfx_plf_tips_dev.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp,
                                     vp]
+    L.plfx_plf_tips_dev_gen.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp,
+                                        vp, vp, vp, vp]
     L.plfx_traverse_tips.argtypes = [vp, i32, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp),
                                      C.POINTER(vp), i32, vp, i32, vp, i64, vp, C.POINTER(vp), vp, vp,
                                      vp]
@@ -353,10 +356,11 @@ class Context:
         """Run a post-order traversal descriptor.  ops: (nops, 4) int array of
         [parent, child1, child2, pmat]; clv: list of torch CLV tensors (slots;
         None where the slot is a tip); pmats: tensor of 2*npmat matrices (64
-        values each for DNA); tips: optional list (per slot) of uint8 state-code
-        tensors or None (plfx.h section 8); tipvec: optional device table of
-        16 x 4 tip vectors (dtype of the CLVs); states 4 or 20 (protein: no
-        tips), fma: PLFX_FMA for protein nodes."""
+        values each for DNA); tips: optional list (per slot) of uint8 code
+        tensors or None (plfx.h section 8: DNA state bits, protein code
+        indices); tipvec: optional device table of tip vectors (16 x 4 DNA,
+        PROT_CODES x 20 protein; dtype of the CLVs); states 4 or 20, fma:
+        PLFX_FMA for protein nodes."""
         import torch
 
         ops = np.ascontiguousarray(ops, dtype=np.int32).reshape(-1, 4)
@@ -392,35 +396,40 @@ class Context:
             C.c_void_p(EV.data_ptr()), int(n),
             C.c_void_p(None if wgt is None else wgt.data_ptr()), sc,
             C.c_void_p(None if scaler_sums is None else scaler_sums.data_ptr()),
-            self._tipvec(tipvec, dt), _stream_handle(stream)))
+            self._tipvec(tipvec, dt, states), _stream_handle(stream)))
 
     @staticmethod
-    def _tipvec(tipvec, dt):
+    def _tipvec(tipvec, dt, states=4):
         if tipvec is None:
             return C.c_void_p(None)
-        if tipvec.dtype != dt or tipvec.numel() < 64 or not tipvec.is_contiguous():
-            raise PlfxError(ERR_INVALID, "tipvec must be a contiguous device table of 16 x 4 values")
+        rows, width = (16, 4) if states == 4 else (PROT_CODES, 20)
+        if tipvec.dtype != dt or tipvec.numel() < rows * width or not tipvec.is_contiguous():
+            raise PlfxError(ERR_INVALID, f"tipvec must be a contiguous device table of "
+                                         f"{rows} x {width} values")
         return C.c_void_p(tipvec.data_ptr())
 
     def plf_tips_dev(self, x3, EV, n, left, right, x1=None, x2=None, tip1=None, tip2=None,
-                     wgt=None, scaler=None, scaler_sum=None, tipvec=None, stream=None):
-        """One DNA inner node with tip children (plfx.h section 8): for each
-        child pass exactly one of the dense CLV (x1/x2) or the uint8 state
-        codes (tip1/tip2)."""
+                     wgt=None, scaler=None, scaler_sum=None, tipvec=None, stream=None, states=4,
+                     fma=False):
+        """One inner node with tip children (plfx.h section 8): for each child
+        pass exactly one of the dense CLV (x1/x2) or the uint8 codes
+        (tip1/tip2).  states 4 (DNA state bits) or 20 (protein code indices,
+        PROT_CODES rows); fma: PLFX_FMA (protein)."""
         import torch
 
         dt = EV.dtype
+        V = 4 * states
         for k, t in (("x3", x3), ("x1", x1), ("x2", x2)):
-            if t is not None and (t.dtype != dt or t.numel() < 16 * n or not t.is_contiguous()):
-                raise PlfxError(ERR_INVALID, f"{k} must be contiguous {dt} >= 16*n")
+            if t is not None and (t.dtype != dt or t.numel() < V * n or not t.is_contiguous()):
+                raise PlfxError(ERR_INVALID, f"{k} must be contiguous {dt} >= {V}*n")
         for k, t in (("tip1", tip1), ("tip2", tip2)):
             if t is not None and (t.dtype != torch.uint8 or t.numel() < n or not t.is_contiguous()):
                 raise PlfxError(ERR_INVALID, f"{k} must be contiguous uint8 >= n")
         p = lambda t: C.c_void_p(None if t is None else t.data_ptr())  # noqa: E731
-        self._check(self._L.plfx_plf_tips_dev(
-            self.h, F32 if dt == torch.float32 else F64, p(tip1), p(x1), p(tip2), p(x2), p(x3),
-            p(EV), int(n), p(left), p(right), p(wgt), p(scaler), p(scaler_sum),
-            self._tipvec(tipvec, dt), _stream_handle(stream)))
+        self._check(self._L.plfx_plf_tips_dev_gen(
+            self.h, F32 if dt == torch.float32 else F64, states, FMA if fma else EXACT, p(tip1),
+            p(x1), p(tip2), p(x2), p(x3), p(EV), int(n), p(left), p(right), p(wgt), p(scaler),
+            p(scaler_sum), self._tipvec(tipvec, dt, states), _stream_handle(stream)))
 
     # -- (9) P matrices from branch lengths --------------------------------
     def pmatrix(self, eigen, rates, blen, out, states=4, convention=PMAT_STATE, stream=None):

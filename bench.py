@@ -373,25 +373,38 @@ class ProteinWorkload:
         self.EV = torch.rand(400, dtype=tdt, device=dev, generator=g) - 0.25
         self.left = torch.rand(1600, dtype=tdt, device=dev, generator=g)
         self.right = torch.rand(1600, dtype=tdt, device=dev, generator=g)
+        self.tips = a.tips
         self.sets = []
         for _ in range(R):
             x1 = torch.rand(n * V, dtype=tdt, device=dev, generator=g)
             x1.view(-1, V)[0::4] *= 1e-14
-            self.sets.append(dict(x1=x1, x2=torch.rand(n * V, dtype=tdt, device=dev, generator=g),
-                                  x3=torch.empty_like(x1),
+            x2 = torch.rand(n * V, dtype=tdt, device=dev, generator=g)
+            codes = None
+            if a.tips:  # coded left child: the underflowing sites come from x2 instead
+                codes = torch.randint(0, 24, (n,), device=dev, generator=g).to(torch.uint8)
+                x2.view(-1, V)[0::4] *= 1e-14
+            self.sets.append(dict(x1=x1, x2=x2, x3=torch.empty_like(x1), codes=codes,
                                   wgt=torch.ones(n, dtype=torch.int32, device=dev),
                                   sc=torch.empty(n, dtype=torch.uint8, device=dev),
                                   s=torch.zeros(1, dtype=torch.int64, device=dev)))
         self.sites_per_step = n
-        self.bytes_per_site = 3 * V * esz + 1 + 4
+        # --tips: the left child is a tip (one code byte per site, plfx.h section 8)
+        self.bytes_per_site = (1 if a.tips else V * esz) + 2 * V * esz + 1 + 4
         self.bytes_per_step = self.bytes_per_site * n
+        mode = ('FMA (within 1e-12 of exact)' if esz == 8 else 'FMA') if self.fma else 'exact'
         self.config = {
             "workload": f"Protein 20-state x 4 Gamma cats, 1 inner node per GPU per step, {n} sites, "
-                        f"{a.dtype}, {('FMA (within 1e-12 of exact)' if esz == 8 else 'FMA') if self.fma else 'exact'} (BASELINE configs[4])",
+                        f"{a.dtype}, {mode}{', tip/inner (coded left child)' if a.tips else ''} "
+                        f"(BASELINE configs[4])",
             "sites_per_gpu_per_step": n, "nodes_per_gpu_per_step": 1, "buffer_sets": R}
 
     def step(self, i, sh):
         b = self.sets[i % self.R]
+        if self.tips:
+            self.ctx.plf_tips_dev(b["x3"], self.EV, self.n, self.left, self.right, tip1=b["codes"],
+                                  x2=b["x2"], wgt=b["wgt"], scaler=b["sc"], scaler_sum=b["s"],
+                                  stream=sh, states=20, fma=self.fma)
+            return
         self.ctx.plf_dev_gen(b["x1"], b["x2"], b["x3"], self.EV, self.left, self.right, 20,
                              b["wgt"], b["sc"], b["s"], fma=self.fma, stream=sh)
 

@@ -188,7 +188,15 @@ int plfx_traverse(plfx_ctx *ctx, int dtype, int states, const plfx_trav_op *ops,
  * unknown; the upper nibble is ignored), the RAxML/PLL encoding -- instead of
  * a dense CLV of 16 values per site (16x/32x less traffic for that child).
  * Results are bit-identical to plf() on the expanded dense CLV
- * x[i][c][s] = (code_i >> s) & 1 for every category c.  DNA (4 states) only. */
+ * x[i][c][s] = (code_i >> s) & 1 for every category c.
+ *
+ * Protein (states = 20, plfx_plf_tips_dev_gen / plfx_traverse_tips): a code is
+ * an index into a table of 24 dense rows of 20 values (codes >= 24 read row
+ * 23); the default table (tipvec NULL), states in ARNDCQEGHILKMFPSTWYV order:
+ * 0..19 one state, 20 = B (N|D), 21 = Z (Q|E), 22 = X, 23 = gap (all states);
+ * tipvec = a device table of 24 x 20 values of dtype replaces it.  Exact and
+ * FMA modes as plfx_plf_dev_gen, bit-identical to the dense computation on
+ * x[i][c][s] = tv[code_i][s] in that mode. */
 
 /* tipvec: NULL, or a device table of 16 x 4 values of dtype -- the dense
  * per-category CLV entry of each code, tipvec[code*4 + s] (the default is the
@@ -202,9 +210,18 @@ int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void 
                       const void *left, const void *right, const int32_t *wgt, uint8_t *scaler,
                       int64_t *scaler_sum, const void *tipvec, void *stream);
 
+/* plfx_plf_tips_dev for states 4 or 20 and flags as plfx_plf_dev_gen
+ * (PLFX_FMA: protein f64 nodes on the matrix cores; DNA is always exact). */
+int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const uint8_t *tip1,
+                          const void *x1, const uint8_t *tip2, const void *x2, void *x3,
+                          const void *EV, int64_t n, const void *left, const void *right,
+                          const int32_t *wgt, uint8_t *scaler, int64_t *scaler_sum,
+                          const void *tipvec, void *stream);
+
 /* plfx_traverse with tip slots and flags: tips is a host array of nslots device
  * pointers (or NULL = no tips); a slot with tips[s] != NULL is a tip (clv[s] is
- * not read) and may not be an op's parent (tips: DNA only).  Each level is
+ * not read) and may not be an op's parent (codes and tipvec as above for the
+ * states).  Each level is
  * issued as up to three batched launches (tip/tip, tip/inner, inner/inner),
  * three-level subtrees and level pairs fused where possible
  * (bit-identical results; env PLFX_FUSE=1 pairs only, 0 none).  states 4 or 20; flags as

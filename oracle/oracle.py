@@ -245,6 +245,39 @@ def expand_tips(codes, dtype=np.float64, Ccat=4, tipvec=None):
     return np.ascontiguousarray(np.repeat(rows[:, None, :], Ccat, axis=1).reshape(-1))
 
 
+PROT_CODES = 24
+
+
+def protein_tip_table(dtype=np.float64, tipvec=None):
+    """The protein tip-vector table (plfx.h section 8): PROT_CODES rows of 20
+    states in ARNDCQEGHILKMFPSTWYV order -- 0..19 one state, 20 = B (N|D),
+    21 = Z (Q|E), 22 = X, 23 = gap (all states) -- or the caller's table."""
+    if tipvec is not None:
+        return np.asarray(tipvec, dtype).reshape(PROT_CODES, 20)
+    t = np.zeros((PROT_CODES, 20), dtype)
+    t[np.arange(20), np.arange(20)] = 1
+    t[20, [2, 3]] = 1
+    t[21, [5, 6]] = 1
+    t[22:] = 1
+    return t
+
+
+def expand_protein_tips(codes, dtype=np.float64, Ccat=4, tipvec=None):
+    """Dense protein CLV of a tip stored as code indices (codes >= PROT_CODES
+    read the last row): x[i][c][s] = table[code_i][s] for every category."""
+    codes = np.minimum(np.asarray(codes, np.uint8), PROT_CODES - 1)
+    rows = protein_tip_table(dtype, tipvec)[codes]
+    return np.ascontiguousarray(np.repeat(rows[:, None, :], Ccat, axis=1).reshape(-1))
+
+
+def random_protein_codes(rng, n, ambiguous=0.1):
+    """Mostly single amino acids (0..19), a fraction of B/Z/X/gap and junk >= 24."""
+    codes = rng.integers(0, 20, n).astype(np.uint8)
+    amb = rng.random(n) < ambiguous
+    codes[amb] = rng.integers(20, 256, int(amb.sum())).astype(np.uint8)
+    return codes
+
+
 def random_tip_codes(rng, n, ambiguous=0.1):
     """Tip codes: mostly unambiguous A/C/G/T (1, 2, 4, 8), a fraction of
     random bytes (ambiguity codes, gaps 15, code 0, junk in the upper nibble)."""

@@ -193,3 +193,97 @@ def test_protein_model_pipeline_lnl(ctx, oracle):
     torch.cuda.synchronize()
     got = float(out.item())
     assert abs(got - exp_lnl) <= 1e-10 * abs(exp_lnl), (got, exp_lnl)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("kind", ["tip1", "tip2", "both"])
+@pytest.mark.parametrize("n", [1, 65, 3001])
+def test_protein_tip_children(ctx, oracle, dtype, fma, kind, n):
+    """Protein tips (uint8 code indices into the 24-row table: one amino acid,
+    B, Z, X, gap, junk >= 24): bit-identical to the same mode's computation on
+    the expanded dense CLVs (the oracle's restatement, exact or fma)."""
+    import torch
+
+    rng = np.random.default_rng(77 + n)
+    x1, x2, EV, left, right, w = gen(n, dtype, 11 + n)
+    c1, c2 = oracle.random_protein_codes(rng, n, 0.3), oracle.random_protein_codes(rng, n, 0.3)
+    e1 = oracle.expand_protein_tips(c1, dtype) if kind in ("tip1", "both") else x1
+    e2 = oracle.expand_protein_tips(c2, dtype) if kind in ("tip2", "both") else x2
+    f3, fsc, finc = oracle.plf_generic(S, CAT, e1, e2, EV, left, right, w, fma=fma)
+    t = [dev(a) for a in (x1, x2, EV, left, right, w)]
+    x3 = torch.empty(V * n, dtype=t[0].dtype, device="cuda")
+    sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    kw = dict(x1=t[0]) if kind == "tip2" else dict(tip1=dev(c1))
+    kw.update(x2=t[1]) if kind == "tip1" else kw.update(tip2=dev(c2))
+    ctx.plf_tips_dev(x3, t[2], n, t[3], t[4], wgt=t[5], scaler=sc, scaler_sum=s, states=S,
+                     fma=fma, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(x3.cpu().numpy()), bits(f3))
+    assert np.array_equal(sc.cpu().numpy(), fsc) and int(s.item()) == finc
+
+
+def test_protein_tip_vector_table(ctx, oracle):
+    """A caller tip-vector table (24 x 20, e.g. eigen coordinates or a
+    different ambiguity model) replaces the default one."""
+    import torch
+
+    n = 777
+    rng = np.random.default_rng(5)
+    x1, x2, EV, left, right, w = gen(n, np.float64, 9)
+    tv = rng.random((oracle.PROT_CODES, S)) - 0.3
+    c1 = oracle.random_protein_codes(rng, n, 0.5)
+    e1 = oracle.expand_protein_tips(c1, np.float64, tipvec=tv)
+    f3, fsc, finc = oracle.plf_generic(S, CAT, e1, x2, EV, left, right, w)
+    x3 = torch.empty(V * n, dtype=torch.float64, device="cuda")
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.plf_tips_dev(x3, dev(EV), n, dev(left), dev(right), tip1=dev(c1), x2=dev(x2), wgt=dev(w),
+                     scaler_sum=s, tipvec=dev(tv), states=S)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(x3.cpu().numpy()), bits(f3)) and int(s.item()) == finc
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_protein_traverse_with_tips(ctx, oracle, dtype):
+    """Protein tree with coded tips (a mix of coded and dense leaves): the
+    exact traversal is bit-exact against the oracle's sequential traversal on
+    the expanded leaves; the FMA traversal's root lnL is within 1e-10."""
+    import torch
+
+    n, ntips = 700, 16
+    rng = np.random.default_rng(8)
+    ops = oracle.balanced_tree_ops(ntips)
+    nops, nslots = ops.shape[0], ntips + ops.shape[0]
+    coded = [t % 3 != 2 for t in range(ntips)]
+    codes = [oracle.random_protein_codes(rng, n, 0.2) for _ in range(ntips)]
+    dense = [rng.random(V * n).astype(dtype) for _ in range(ntips)]
+    pm = (rng.random(nops * 2 * CAT * S * S) * 0.05).astype(dtype)
+    EV = (rng.random(S * S) * 0.05).astype(dtype)
+    wgt = rng.integers(1, 4, n).astype(np.int32)
+    host = [oracle.expand_protein_tips(codes[t], dtype) if coded[t] else dense[t].copy()
+            for t in range(ntips)] + [np.zeros(V * n, dtype) for _ in range(nops)]
+    esums, escal = oracle.traverse(S, CAT, ops, host, pm, EV, n, wgt, want_scalers=True)
+    assert esums.sum() > 0
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    lnl = {}
+    for fma in (False, True) if dtype == np.float64 else (False,):
+        clv = [None if coded[t] else dev(dense[t]) for t in range(ntips)]
+        clv += [torch.zeros(V * n, dtype=tt, device="cuda") for _ in range(nops)]
+        tips = [dev(codes[t]) if coded[t] else None for t in range(ntips)] + [None] * nops
+        sums = torch.zeros(nops, dtype=torch.int64, device="cuda")
+        scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+        ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips, states=S,
+                     fma=fma)
+        out = torch.zeros(1, dtype=torch.float64, device="cuda")
+        ctx.root_lnl(clv[-1], n, out, wgt=dev(wgt), scaler_sums=sums, states=S)
+        torch.cuda.synchronize()
+        lnl[fma] = float(out.item())
+        if not fma:
+            for s in range(ntips, nslots):
+                assert np.array_equal(bits(clv[s].cpu().numpy()), bits(host[s])), s
+            assert np.array_equal(sums.cpu().numpy(), esums)
+            for j in range(nops):
+                assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+    if True in lnl:
+        assert abs(lnl[True] - lnl[False]) <= 1e-10 * abs(lnl[False])

@@ -263,3 +263,21 @@ def test_tip_table_identity(oracle, dtype):
     assert np.array_equal(bits(o.reshape(-1)), bits(x3))
     assert np.array_equal(sc, small.astype(np.uint8))
     assert int(inc) == int(small.sum())
+
+
+def test_protein_tip_expansion():
+    """The protein tip table (plfx.h section 8): one-hot rows, B = N|D,
+    Z = Q|E, X and gap all ones, codes >= 24 read row 23."""
+    import numpy as np
+
+    import oracle as O
+
+    t = O.protein_tip_table()
+    assert t.shape == (24, 20) and (t[:20] == np.eye(20)).all()
+    assert list(np.flatnonzero(t[20])) == [2, 3] and list(np.flatnonzero(t[21])) == [5, 6]
+    assert (t[22:] == 1).all()
+    x = O.expand_protein_tips(np.array([3, 20, 200], np.uint8))
+    assert x.shape == (3 * 80,)
+    r = x.reshape(3, 4, 20)
+    assert (r[:, 0] == r[:, 3]).all() and r[0, 0, 3] == 1 and r[0, 0].sum() == 1
+    assert r[1, 2].sum() == 2 and (r[2] == 1).all()
