@@ -59,11 +59,14 @@ int main(int argc, char **argv) {
     const int64_t grid = std::min<int64_t>((n + 63) / 64, (int64_t)occ((const void *)k) * CUs);   \
     vs.push_back({NAME, [=](const Set &s) {                                                        \
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
-                         s.wgt, s.sc, n, ws, s.sum); }, {}, 0});                                   \
+                         s.wgt, s.sc, n, ws, s.sum, nullptr); }, {}, 0});                          \
   }
   ADD("A mfma (csrc)", (&plfx::dev::plf_prot_mfma_kernel<true>))
   ADD("B mfma (" B_HEADER ")", (&plfx::dev_b::plf_prot_mfma_kernel<true>))
   ADD("A exact (csrc)", (&plfx::dev::plf_prot_exact_f64_kernel<true>))
+  ADD("A mfma tip/inner (codes in x1)", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 0, true, 1>))
+  ADD("B mfma tip/inner (codes in x1)", (&plfx::dev_b::plf_prot_mfma_kernel<true, 2, true, 0, true, 1>))
+  ADD("A exact tip/inner", (&plfx::dev::plf_prot_exact_f64_kernel<true, 2, 1>))
   ADD("B exact (" B_HEADER ")", (&plfx::dev_b::plf_prot_exact_f64_kernel<true>))
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int r = 0; r < rounds; r++)
