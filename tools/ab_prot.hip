@@ -67,6 +67,10 @@ int main(int argc, char **argv) {
   ADD("A mfma tip/inner (codes in x1)", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 0, true, 1>))
   ADD("B mfma tip/inner (codes in x1)", (&plfx::dev_b::plf_prot_mfma_kernel<true, 2, true, 0, true, 1>))
   ADD("A exact tip/inner", (&plfx::dev::plf_prot_exact_f64_kernel<true, 2, 1>))
+  ADD("A mfma tip/inner ablate: no MFMA", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 1, true, 1>))
+  ADD("A mfma tip/inner ablate: no HBM", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 2, true, 1>))
+  ADD("A mfma ablate: no MFMA", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 1, true, 0>))
+  ADD("A mfma ablate: no HBM", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 2, true, 0>))
   ADD("B exact (" B_HEADER ")", (&plfx::dev_b::plf_prot_exact_f64_kernel<true>))
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int r = 0; r < rounds; r++)
