@@ -151,11 +151,15 @@ __device__ inline void block_ticket_sum3(long long v0, long long v1, long long v
 
 // Swap 64-bit values between adjacent lanes with DPP quad_perm patterns:
 // dpp_even(x) = x of lane (l & ~1), dpp_odd(x) = x of lane (l | 1).
+// mov_dpp with bound_ctrl: every lane has a valid quad_perm source, so no
+// "old" value is needed (update_dpp(0, ...) made the compiler zero the
+// destination first: one extra v_mov_b32 per DPP move, ~15 % of the VALU
+// issue of the headline kernel's loop).
 template <int kCtrl>
 __device__ __forceinline__ double dpp_f64(double x) {
   const long long b = __builtin_bit_cast(long long, x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), kCtrl, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), kCtrl, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), kCtrl, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), kCtrl, 0xf, 0xf, true);
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 constexpr int kQuadEven = 0 | (0 << 2) | (2 << 4) | (2 << 6);  // quad_perm [0,0,2,2]
@@ -184,15 +188,25 @@ __device__ __forceinline__ void build_tip_table(const T *__restrict__ P, const T
 // One site-category (4 values of x1, 4 of x2) -> 4 values of x3, before the
 // scale test.  plf.cpp:31-50: ump from +0.0 ascending l, product per k, x3 from
 // +0.0 ascending k.
+//
+// Leading +0.0 of the ump chains.  plf() sums ump = ((0 + q0) + q1) + ... ; here
+// the chains start at q0.  The two differ only in the sign of a zero (0 + q0
+// turns -0 into +0 and is the identity otherwise, NaN payloads included), and
+// an ump value reaches x3 only through p = ump1*ump2 and the x3 chain, which
+// DOES start at +0.0: (+0 + r) maps +0 and -0 to +0 and every later term of a
+// chain that has reached +0 or a nonzero value ignores the sign of a zero
+// term.  So x3, the scale test and the scaler bytes are bit-identical to
+// plf()'s; the x3 chain keeps its +0.0.  (Saves 2 of the 14 f64 ops per
+// site-category-k in the headline kernel; the GPU tests compare bit-for-bit.)
 template <typename T>
 __device__ __forceinline__ void site_cat(const T (&a)[4], const T (&b)[4], const T (&PL)[16],
                                          const T (&PR)[16], const T (&E)[16], T (&o)[4]) {
   T p[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    T u1 = T(0), u2 = T(0);
+    T u1 = a[0] * PL[k * 4], u2 = b[0] * PR[k * 4];  // chains start at q0 (see above)
 #pragma unroll
-    for (int l = 0; l < 4; l++) {
+    for (int l = 1; l < 4; l++) {
       u1 += a[l] * PL[k * 4 + l];
       u2 += b[l] * PR[k * 4 + l];
     }
@@ -215,18 +229,20 @@ __device__ __forceinline__ void site_cat_tips(const T (&a)[4], const T (&b)[4], 
   T p[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    T u1 = T(0), u2 = T(0);
+    T u1, u2;
     if constexpr (T1) {
       u1 = row1[k];
     } else {
+      u1 = a[0] * PL[k * 4];  // chains start at q0 (site_cat)
 #pragma unroll
-      for (int l = 0; l < 4; l++) u1 += a[l] * PL[k * 4 + l];
+      for (int l = 1; l < 4; l++) u1 += a[l] * PL[k * 4 + l];
     }
     if constexpr (T2) {
       u2 = row2[k];
     } else {
+      u2 = b[0] * PR[k * 4];
 #pragma unroll
-      for (int l = 0; l < 4; l++) u2 += b[l] * PR[k * 4 + l];
+      for (int l = 1; l < 4; l++) u2 += b[l] * PR[k * 4 + l];
     }
     p[k] = u1 * u2;
   }
@@ -437,8 +453,8 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
       const double a2 = dpp_f64<kQuadOdd>(a.x), a3 = dpp_f64<kQuadOdd>(a.y);
 #pragma unroll
       for (int kk = 0; kk < 2; kk++) {
-        double v = 0.0;
-        v += a0 * PL[kk][0]; v += a1 * PL[kk][1]; v += a2 * PL[kk][2]; v += a3 * PL[kk][3];
+        double v = a0 * PL[kk][0];  // chain starts at q0 (site_cat)
+        v += a1 * PL[kk][1]; v += a2 * PL[kk][2]; v += a3 * PL[kk][3];
         u1[kk] = v;
       }
     }
@@ -450,8 +466,8 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
       const double b2 = dpp_f64<kQuadOdd>(b.x), b3 = dpp_f64<kQuadOdd>(b.y);
 #pragma unroll
       for (int kk = 0; kk < 2; kk++) {
-        double v = 0.0;
-        v += b0 * PR[kk][0]; v += b1 * PR[kk][1]; v += b2 * PR[kk][2]; v += b3 * PR[kk][3];
+        double v = b0 * PR[kk][0];  // chain starts at q0 (site_cat)
+        v += b1 * PR[kk][1]; v += b2 * PR[kk][2]; v += b3 * PR[kk][3];
         u2[kk] = v;
       }
     }
@@ -648,8 +664,8 @@ __device__ __forceinline__ f64x2 pair_node(const f64x2 a, const f64x2 b, const d
     const double a2 = dpp_f64<kQuadOdd>(a.x), a3 = dpp_f64<kQuadOdd>(a.y);
 #pragma unroll
     for (int kk = 0; kk < 2; kk++) {
-      double v = 0.0;
-      v += a0 * M.PL[kk][0]; v += a1 * M.PL[kk][1]; v += a2 * M.PL[kk][2]; v += a3 * M.PL[kk][3];
+      double v = a0 * M.PL[kk][0];  // chain starts at q0 (site_cat)
+      v += a1 * M.PL[kk][1]; v += a2 * M.PL[kk][2]; v += a3 * M.PL[kk][3];
       u1[kk] = v;
     }
   }
@@ -661,8 +677,8 @@ __device__ __forceinline__ f64x2 pair_node(const f64x2 a, const f64x2 b, const d
     const double b2 = dpp_f64<kQuadOdd>(b.x), b3 = dpp_f64<kQuadOdd>(b.y);
 #pragma unroll
     for (int kk = 0; kk < 2; kk++) {
-      double v = 0.0;
-      v += b0 * M.PR[kk][0]; v += b1 * M.PR[kk][1]; v += b2 * M.PR[kk][2]; v += b3 * M.PR[kk][3];
+      double v = b0 * M.PR[kk][0];  // chain starts at q0 (site_cat)
+      v += b1 * M.PR[kk][1]; v += b2 * M.PR[kk][2]; v += b3 * M.PR[kk][3];
       u2[kk] = v;
     }
   }

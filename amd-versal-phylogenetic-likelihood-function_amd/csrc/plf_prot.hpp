@@ -306,11 +306,15 @@ plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restric
     for (int l = 0; l < S; l++) o[l] = kAblate == 1 ? a[l] + b[l] : T(0);
 #pragma unroll
     for (int k = 0; k < (kAblate == 1 ? 0 : S); k++) {
-      T u1 = T(0), u2 = T(0);
+      // ump chains start at q0 (fma(a, b, +0) and a*b differ only in the sign
+      // of a zero, which the x3 chain from +0 absorbs: site_cat, plf_dna.hpp)
+      T u1, u2;
       if constexpr (T1) u1 = tabL[code1 * 20 + k];
+      else u1 = a[0] * bcast<T>(ML, k * S);
       if constexpr (T2) u2 = tabR[code2 * 20 + k];
+      else u2 = b[0] * bcast<T>(MR, k * S);
 #pragma unroll
-      for (int l = 0; l < S; l++) {
+      for (int l = 1; l < S; l++) {
         if constexpr (!T1) u1 = madd<T, kFma>(a[l], bcast<T>(ML, k * S + l), u1);
         if constexpr (!T2) u2 = madd<T, kFma>(b[l], bcast<T>(MR, k * S + l), u2);
       }
@@ -428,9 +432,10 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
       row_read<double>(tile, lane, c, a);
       __syncthreads();
       phase(mL, [&](int k, const f64x2 (&p)[10]) {
-        double u = 0.0;
+        double u = a[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
+        u += a[1] * p[0].y;
 #pragma unroll
-        for (int i = 0; i < 10; i++) {
+        for (int i = 1; i < 10; i++) {
           u += a[2 * i] * p[i].x;
           u += a[2 * i + 1] * p[i].y;
         }
@@ -449,9 +454,10 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
       row_read<double>(tile, lane, c, b);
       __syncthreads();
       phase(mR, [&](int k, const f64x2 (&p)[10]) {
-        double u = 0.0;
+        double u = b[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
+        u += b[1] * p[0].y;
 #pragma unroll
-        for (int i = 0; i < 10; i++) {
+        for (int i = 1; i < 10; i++) {
           u += b[2 * i] * p[i].x;
           u += b[2 * i + 1] * p[i].y;
         }
