@@ -287,3 +287,29 @@ def test_protein_traverse_with_tips(ctx, oracle, dtype):
                 assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
     if True in lnl:
         assert abs(lnl[True] - lnl[False]) <= 1e-10 * abs(lnl[False])
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("fma", [False, True])
+def test_protein_signed_zero_inputs(ctx, oracle, dtype, fma):
+    """Inputs full of +-0.0, negative matrix entries and underflowing products:
+    the exact kernels start their ump chains at the first product (plf_dna.hpp,
+    site_cat) and still equal the oracle's plf() order bit for bit; FMA mode
+    equals the fma() restatement."""
+    rng = np.random.default_rng(5)
+    n = 1000
+
+    def field(size):
+        v = (rng.random(size) - 0.5).astype(dtype)
+        r = rng.random(size)
+        v[r < 0.3] = dtype(0.0)
+        v[(r >= 0.3) & (r < 0.5)] = dtype(-0.0)
+        v[(r >= 0.5) & (r < 0.55)] *= np.finfo(dtype).tiny
+        return v
+
+    x1, x2, EV, left, right = field(V * n), field(V * n), field(S * S), field(CAT * S * S), field(CAT * S * S)
+    w = rng.integers(0, 4, n).astype(np.int32)
+    x3, sc, s = run(ctx, x1, x2, EV, left, right, w, n, fma=fma)
+    e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=fma)
+    assert np.array_equal(bits(x3), bits(e3))
+    assert np.array_equal(sc, esc) and s == einc

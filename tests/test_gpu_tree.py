@@ -410,3 +410,63 @@ def test_single_subtree_tails(ctx, oracle, n, tipmode, taxa, dtype):
         got = scal[j].cpu().numpy()
         assert np.array_equal(got[:n], escal[j]), j
         assert (got[n:] == 7).all(), j  # nothing written past n
+
+
+def _signed_zero_field(rng, size, dtype, neg=True):
+    """Values built to hit the sign of zero: +-0.0 entries, negative entries,
+    products that underflow (see test_oracle.test_ump_chain_start_is_exact)."""
+    v = rng.random(size).astype(dtype)
+    if neg:
+        v = v - dtype(0.5)
+    r = rng.random(size)
+    v[r < 0.3] = dtype(0.0)
+    v[(r >= 0.3) & (r < 0.5)] = dtype(-0.0)
+    v[(r >= 0.5) & (r < 0.55)] *= np.finfo(dtype).tiny
+    return v
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("fuse", ["0", "1", "2"])
+def test_signed_zero_inputs_bitexact(ctx, oracle, dtype, fuse, monkeypatch):
+    """The kernels start ump chains at the first product (plf_dna.hpp,
+    site_cat); on inputs full of +-0.0, negative matrix entries and underflow,
+    the node kernel and every traversal schedule (one launch per level, fused
+    level pairs, fused three-level subtrees) still equal the oracle's plf()
+    order bit for bit."""
+    import plfx
+    import torch
+
+    rng = np.random.default_rng(99)
+    n = 3001
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    # one node through plf_dev
+    x1, x2 = _signed_zero_field(rng, 16 * n, dtype), _signed_zero_field(rng, 16 * n, dtype)
+    EV, L, R = (_signed_zero_field(rng, s, dtype) for s in (16, 64, 64))
+    e3, esc, einc = oracle.plf(x1, x2, EV, L, R)
+    o3 = torch.empty(16 * n, dtype=tt, device="cuda")
+    sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.plf_dev(dev(x1), dev(x2), o3, dev(EV), dev(L), dev(R), None, sc, s)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(o3.cpu().numpy()), bits(e3))
+    assert np.array_equal(sc.cpu().numpy(), esc) and int(s.item()) == einc
+    # a 16-taxon tree under the schedule PLFX_FUSE selects (read at context creation)
+    monkeypatch.setenv("PLFX_FUSE", fuse)
+    with plfx.Context(0) as c2:
+        ops = oracle.balanced_tree_ops(16)
+        nops = ops.shape[0]
+        tips = [_signed_zero_field(rng, 16 * n, dtype) for _ in range(16)]
+        pm = _signed_zero_field(rng, nops * 128, dtype)
+        wgt = rng.integers(0, 5, n).astype(np.int32)
+        host = [t.copy() for t in tips] + [np.zeros(16 * n, dtype) for _ in range(nops)]
+        esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
+        clv = [dev(t) for t in tips] + [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nops)]
+        sums = torch.zeros(nops, dtype=torch.int64, device="cuda")
+        scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+        c2.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums)
+        torch.cuda.synchronize()
+        for j in range(16, 16 + nops):
+            assert np.array_equal(bits(clv[j].cpu().numpy()), bits(host[j])), j
+        assert np.array_equal(sums.cpu().numpy(), esums)
+        for j in range(nops):
+            assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j

@@ -281,3 +281,65 @@ def test_protein_tip_expansion():
     r = x.reshape(3, 4, 20)
     assert (r[:, 0] == r[:, 3]).all() and r[0, 0, 3] == 1 and r[0, 0].sum() == 1
     assert r[1, 2].sum() == 2 and (r[2] == 1).all()
+
+
+def _adversarial_inputs(n, dtype, seed):
+    """CLVs and matrices built to hit the sign of zero: many +-0.0 entries,
+    negative matrix entries and zeros, products that underflow."""
+    rng = np.random.default_rng(seed)
+    tiny = np.finfo(dtype).tiny
+
+    def field(size, neg):
+        v = rng.random(size).astype(dtype)
+        if neg:
+            v = v - dtype(0.5)
+        r = rng.random(size)
+        v[r < 0.3] = dtype(0.0)
+        v[(r >= 0.3) & (r < 0.5)] = dtype(-0.0)
+        v[(r >= 0.5) & (r < 0.55)] *= tiny  # products underflow to +-0
+        return v
+
+    return (field(16 * n, True), field(16 * n, True), field(16, True),
+            field(64, True), field(64, True))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_ump_chain_start_is_exact(oracle, dtype):
+    """The kernels start each ump chain at its first product instead of +0.0
+    (plf_dna.hpp, site_cat).  Proof by exhaustion over adversarial inputs:
+    numpy restatement of both chain forms, element-wise in plf()'s order, gives
+    bit-identical x3 -- and both equal the C oracle."""
+    n = 20000
+    x1, x2, EV, left, right = _adversarial_inputs(n, dtype, 7)
+    a = x1.reshape(n, 4, 4)
+    b = x2.reshape(n, 4, 4)
+    PL = left.reshape(4, 4, 4)
+    PR = right.reshape(4, 4, 4)
+    E = EV.reshape(4, 4)
+    z = dtype(0.0)
+    out = {}
+    for form in ("zero", "first"):
+        p = np.empty((n, 4, 4), dtype)
+        for k in range(4):
+            u1 = (z + a[:, :, 0] * PL[None, :, k, 0]) if form == "zero" else a[:, :, 0] * PL[None, :, k, 0]
+            u2 = (z + b[:, :, 0] * PR[None, :, k, 0]) if form == "zero" else b[:, :, 0] * PR[None, :, k, 0]
+            for l in range(1, 4):
+                u1 = u1 + a[:, :, l] * PL[None, :, k, l]
+                u2 = u2 + b[:, :, l] * PR[None, :, k, l]
+            p[:, :, k] = u1 * u2
+        x3 = np.empty((n, 4, 4), dtype)
+        for l in range(4):
+            o = np.full((n, 4), z)
+            for k in range(4):
+                o = o + p[:, :, k] * E[k, l]
+            x3[:, :, l] = o
+        out[form] = x3.reshape(-1)
+    assert np.array_equal(bits(out["zero"]), bits(out["first"]))
+    # the first products include -0.0, where 0 + q0 and q0 differ: the test bites
+    q0 = a[:, :, 0] * PL[None, :, 0, 0]
+    assert np.any((q0 == 0) & np.signbit(q0))
+    e3, _, _ = oracle.plf(x1, x2, EV, left, right)
+    small = np.abs(out["zero"]).reshape(n, 16).max(axis=1) < (2.0 ** -32)
+    exp = out["zero"].reshape(n, 16).copy()
+    exp[small] *= dtype(2.0 ** 32)
+    assert np.array_equal(bits(exp.reshape(-1)), bits(e3))
