@@ -1,0 +1,200 @@
+// tune_f32.hip -- tuning only: the f32 DNA node kernel (lane = category,
+// csrc dna_cat_body) against variants with the next trip's loads issued
+// before this trip's arithmetic (software pipelining) and other trip sizes /
+// grids, checked bit-for-bit against csrc before timing.  f32 is the
+// reference's own precision; at 2^20 sites its 39-us launch loses ~15 % to
+// per-launch costs (start-up with every wave computing at once, tail).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//     -I amd-versal-phylogenetic-likelihood-function_amd/csrc tools/tune_f32.hip -o build/tune_f32
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "plf_dna.hpp"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+using namespace plfx::dev;
+
+// pipelined lane = category body (no tips; n must be a multiple of 16U*... no:
+// full trips only, the harness uses n multiple of 4096)
+template <int U, int MINW>
+__global__ void __launch_bounds__(256, MINW)
+cat_pf(const float *__restrict__ x1, const float *__restrict__ x2, float *__restrict__ x3,
+       const float *__restrict__ EV, const float *__restrict__ left, const float *__restrict__ right,
+       const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+       int64_t *scaler_sum) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 3, q = lane >> 2, nib = lane & 60;
+  float PL[16], PR[16], E[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) { PL[i] = left[c * 16 + i]; PR[i] = right[c * 16 + i]; E[i] = EV[i]; }
+  const float m = Num<float>::minlik();
+  long long acc = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  float a[U][4], b[U][4];
+  int w[U];
+  auto load = [&](int64_t base) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      Num<float>::load4<true>(x1 + site * 16 + c * 4, a[u]);
+      Num<float>::load4<true>(x2 + site * 16 + c * 4, b[u]);
+      w[u] = wgt_at(wgt, site, ws);
+    }
+  };
+  int64_t base = wave * 16 * U;
+  if (base < n) load(base);
+  for (; base < n; base += stride) {
+    float A[U][4], B[U][4];
+    int W[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+#pragma unroll
+      for (int l = 0; l < 4; l++) { A[u][l] = a[u][l]; B[u][l] = b[u][l]; }
+      W[u] = w[u];
+    }
+    if (base + stride < n) load(base + stride);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      float o[4];
+      site_cat<float>(A[u], B[u], PL, PR, E, o);
+      const bool small = (o[0] < m && o[0] > -m) && (Num<float>::abs(o[1]) < m) &&
+                         (Num<float>::abs(o[2]) < m) && (Num<float>::abs(o[3]) < m);
+      const unsigned long long mask = __ballot(small);
+      const bool sc = ((mask >> nib) & 0xFull) == 0xFull;
+#pragma unroll
+      for (int l = 0; l < 4; l++) { const float s = o[l] * Num<float>::two32(); o[l] = sc ? s : o[l]; }
+      Num<float>::store4_nt(x3 + site * 16 + c * 4, o);
+      if (c == 0 && scaler) scaler[site] = (uint8_t)sc;
+      acc += (c == 0 && sc) ? (long long)W[u] : 0ll;
+    }
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
+__global__ void fill(float *p, int64_t n, uint64_t seed, float scale4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    float v = (float)((double)(z >> 11) * (1.0 / 9007199254740992.0));
+    if (scale4 != 1.0f && ((i / 16) % 4) == 0) v *= scale4;
+    p[i] = v;
+  }
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) stream3(const f32x4v *__restrict__ a, const f32x4v *__restrict__ b,
+                                               f32x4v *__restrict__ c, int64_t nrec) {
+  constexpr int V = 4;
+  const int64_t stride = (int64_t)gridDim.x * 256 * V;
+  for (int64_t i = (int64_t)blockIdx.x * 256 * V + threadIdx.x; i < nrec; i += stride) {
+    f32x4v x[V], y[V];
+#pragma unroll
+    for (int v = 0; v < V; v++) {
+      x[v] = __builtin_nontemporal_load(a + i + 256 * v);
+      y[v] = __builtin_nontemporal_load(b + i + 256 * v);
+    }
+#pragma unroll
+    for (int v = 0; v < V; v++) __builtin_nontemporal_store(x[v] + y[v], c + i + 256 * v);
+  }
+}
+
+struct Set { float *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
+
+int main(int argc, char **argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : (1 << 20);
+  const int reps = argc > 2 ? atoi(argv[2]) : 60, rounds = 5, R = 6;
+  if (n % 4096) { printf("n must be a multiple of 4096\n"); return 1; }
+  hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
+  const int CUs = prop.multiProcessorCount;
+  float *EV, *L, *Rm; unsigned long long *ws;
+  CK(hipMalloc(&EV, 64)); CK(hipMalloc(&L, 256)); CK(hipMalloc(&Rm, 256));
+  CK(hipMalloc(&ws, kWsWords * 8)); CK(hipMemset(ws, 0, kWsWords * 8));
+  fill<<<1, 64>>>(EV, 16, 1, 1.f); fill<<<1, 64>>>(L, 64, 2, 1.f); fill<<<1, 64>>>(Rm, 64, 3, 1.f);
+  std::vector<Set> sets(R);
+  for (int r = 0; r < R; r++) {
+    Set &s = sets[r];
+    CK(hipMalloc(&s.x1, n * 64)); CK(hipMalloc(&s.x2, n * 64)); CK(hipMalloc(&s.x3, n * 64));
+    CK(hipMalloc(&s.wgt, n * 4)); CK(hipMalloc(&s.sc, n)); CK(hipMalloc(&s.sum, 8));
+    fill<<<2048, 256>>>(s.x1, n * 16, 10 + r, 1e-12f);
+    fill<<<2048, 256>>>(s.x2, n * 16, 20 + r, 1.f);
+    std::vector<int> wv(n);
+    for (int64_t i = 0; i < n; i++) wv[i] = 1 + (int)(i % 3);
+    CK(hipMemcpy(s.wgt, wv.data(), n * 4, hipMemcpyHostToDevice));
+  }
+  CK(hipDeviceSynchronize());
+  auto occ = [&](const void *k) { int b = 0; CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, 256, 0)); return b; };
+  struct V { std::string name; double bytes; std::function<void(const Set &)> run; std::vector<float> us; };
+  std::vector<V> vs;
+  vs.push_back({"stream 2R+1W V=4 grid 4/CU", 192.0 * n, [&](const Set &s) {
+    stream3<<<CUs * 4, 256>>>((const f32x4v *)s.x1, (const f32x4v *)s.x2, (f32x4v *)s.x3, n * 4); }, {}});
+#define ADD(NAME, K, SPB, MUL)                                                                     \
+  {                                                                                                \
+    auto k = K;                                                                                    \
+    const int o = occ((const void *)k);                                                            \
+    const int64_t grid = std::min<int64_t>((n + SPB - 1) / SPB, (int64_t)(o * CUs * MUL));         \
+    vs.push_back({std::string(NAME) + " occ " + std::to_string(o) + " grid " + std::to_string(grid), 197.0 * n, \
+                  [=](const Set &s) {                                                              \
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
+                         s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
+  }
+  ADD("csrc cat U=4", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 1)
+  ADD("csrc cat U=2", (&plf_dna_kernel<float, 2, true, true, 1>), 128, 1)
+  ADD("csrc cat U=8", (&plf_dna_kernel<float, 8, true, true, 1>), 512, 1)
+  ADD("pf U=2", (&cat_pf<2, 1>), 128, 1)
+  ADD("pf U=4", (&cat_pf<4, 1>), 256, 1)
+  ADD("pf U=1", (&cat_pf<1, 1>), 64, 1)
+  ADD("pf U=2 grid/2", (&cat_pf<2, 1>), 128, 0.5)
+  ADD("pf U=4 grid/2", (&cat_pf<4, 1>), 256, 0.5)
+  ADD("csrc cat U=4 grid/2", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 0.5)
+  {
+    const size_t bytes = n * 64;
+    std::vector<char> ref(bytes), got(bytes), rsc(n), gsc(n);
+    int64_t rsum = 0, gsum = 0;
+    vs[1].run(sets[0]);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(ref.data(), sets[0].x3, bytes, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(rsc.data(), sets[0].sc, n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(&rsum, sets[0].sum, 8, hipMemcpyDeviceToHost));
+    for (size_t i = 2; i < vs.size(); i++) {
+      CK(hipMemset(sets[0].x3, 0xFF, bytes)); CK(hipMemset(sets[0].sc, 7, n)); CK(hipMemset(sets[0].sum, 0, 8));
+      vs[i].run(sets[0]);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(got.data(), sets[0].x3, bytes, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(gsc.data(), sets[0].sc, n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(&gsum, sets[0].sum, 8, hipMemcpyDeviceToHost));
+      const bool ok = !memcmp(ref.data(), got.data(), bytes) && !memcmp(rsc.data(), gsc.data(), n) && rsum == gsum;
+      printf("check %-40s %s\n", vs[i].name.c_str(), ok ? "bit-exact" : "MISMATCH");
+    }
+  }
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; r++)
+    for (auto &v : vs) {
+      for (int i = 0; i < 3; i++) v.run(sets[i % R]);
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < reps; i++) v.run(sets[i % R]);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      v.us.push_back(ms * 1000.f / reps);
+    }
+  CK(hipGetLastError());
+  printf("n=%lld sites f32, %d reps x %d rounds interleaved, %d buffer sets\n", (long long)n, reps, rounds, R);
+  for (auto &v : vs) {
+    std::sort(v.us.begin(), v.us.end());
+    const double t = v.us[v.us.size() / 2] * 1e-6;
+    printf("%-40s median %8.2f us (min %8.2f)  %5.1f%% of 8 TB/s\n", v.name.c_str(), v.us[v.us.size() / 2], v.us[0],
+           100.0 * v.bytes / t / 8e12);
+  }
+  return 0;
+}

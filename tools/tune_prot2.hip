@@ -1,0 +1,439 @@
+// tune_prot2.hip -- tuning only: a protein (S = 20) FMA-mode kernel without
+// LDS tiles or barriers.  v_mfma_f64_4x4x4_4b_f64 computes FOUR independent
+// 4x4x4 products, one per block b of 16 lanes, each with its own A operand --
+// so block b can be Gamma category b, and one wave instruction covers 4 sites
+// x 4 categories straight from HBM:
+//   B operand  lane 16k + 4b + j = x[site j][cat b][state 4s + k]   (k-step s)
+//   A operand  lane 16k + 4b + i = P_b[row 4m + i][col 4s + k]        (row tile m)
+//   D          lane 16i + 4b + j = U_b[row 4m + i][site j]
+// D of row tile m is exactly the B operand of k-step m of the next product
+// (i -> k), so U_L, the product U_L*U_R and the back-transform X3 = EV^T p all
+// stay in registers; every wave is independent (no LDS, no barriers).  Same
+// k-ordered fma chains as the product MFMA kernel (bit-identical to it and to
+// the oracle's fma() restatement), checked before timing.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//     -I amd-versal-phylogenetic-likelihood-function_amd/csrc tools/tune_prot2.hip -o build/tune_prot2
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "plf_prot.hpp"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+using namespace plfx::dev;
+
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// T = 4-site sub-tiles per wave trip; MINW = launch_bounds min waves per SIMD
+template <int T, int MINW, bool PF, int NT = 3>
+__global__ void __launch_bounds__(256, MINW)
+prot_blk4(const double *__restrict__ x1, const double *__restrict__ x2, double *__restrict__ x3,
+          const double *__restrict__ EV, const double *__restrict__ left, const double *__restrict__ right,
+          const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+          int64_t *scaler_sum) {
+  constexpr int S = 20;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4;        // k (operand K index) / i (result row)
+  const int b = (lane >> 2) & 3;  // block = Gamma category
+  const int j = lane & 3;         // site within the 4-site sub-tile (B, D); row i for A
+  double AL[5][5], AR[5][5], AE[5][5];  // [row tile m][k-step s]
+#pragma unroll
+  for (int m = 0; m < 5; m++)
+#pragma unroll
+    for (int s = 0; s < 5; s++) {
+      AL[m][s] = left[b * S * S + (4 * m + j) * S + 4 * s + q];
+      AR[m][s] = right[b * S * S + (4 * m + j) * S + 4 * s + q];
+      AE[m][s] = EV[(4 * s + q) * S + 4 * m + j];  // EV^T[l = 4m+i][k = 4s+kk]
+    }
+  const double mlim = Num<double>::minlik();
+  const unsigned long long pat = 0x1111111111111111ull;
+  long long acc = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 4 * T;
+  const int off = b * S + q;  // this lane's (category, k) offset inside a site's 80 values
+
+  double a[T][5], c[T][5];
+  int w[T];
+  auto load = [&](int64_t base) {
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+      const int64_t site = base + 4 * t + j;
+      const int64_t sq = site < n ? site : n - 1;
+      const double *p1 = x1 + sq * 80 + off;
+      const double *p2 = x2 + sq * 80 + off;
+#pragma unroll
+      for (int s = 0; s < 5; s++) {
+        if constexpr (NT & 1) {
+          a[t][s] = __builtin_nontemporal_load(p1 + 4 * s);
+          c[t][s] = __builtin_nontemporal_load(p2 + 4 * s);
+        } else {
+          a[t][s] = p1[4 * s];
+          c[t][s] = p2[4 * s];
+        }
+      }
+      w[t] = wgt_at(wgt, sq, ws);
+    }
+  };
+  int64_t base = wave * 4 * T;
+  if (PF && base < n) load(base);
+  for (; base < n; base += stride) {
+    double A1[T][5], A2[T][5];
+    int W[T];
+    if constexpr (PF) {
+#pragma unroll
+      for (int t = 0; t < T; t++) {
+#pragma unroll
+        for (int s = 0; s < 5; s++) { A1[t][s] = a[t][s]; A2[t][s] = c[t][s]; }
+        W[t] = w[t];
+      }
+      if (base + stride < n) load(base + stride);
+    } else {
+      load(base);
+#pragma unroll
+      for (int t = 0; t < T; t++) {
+#pragma unroll
+        for (int s = 0; s < 5; s++) { A1[t][s] = a[t][s]; A2[t][s] = c[t][s]; }
+        W[t] = w[t];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+      double p[5];
+#pragma unroll
+      for (int m = 0; m < 5; m++) {
+        double uL = 0.0, uR = 0.0;
+#pragma unroll
+        for (int s = 0; s < 5; s++) uL = mfma4(AL[m][s], A1[t][s], uL);
+#pragma unroll
+        for (int s = 0; s < 5; s++) uR = mfma4(AR[m][s], A2[t][s], uR);
+        p[m] = uL * uR;
+      }
+      double o[5];
+      bool small = true;
+#pragma unroll
+      for (int m = 0; m < 5; m++) {
+        double x = 0.0;
+#pragma unroll
+        for (int s = 0; s < 5; s++) x = mfma4(AE[m][s], p[s], x);
+        o[m] = x;
+        small = small && (__builtin_fabs(x) < mlim);
+      }
+      const int64_t site = base + 4 * t + j;
+      const bool valid = site < n;
+      const unsigned long long mk = __ballot(small && valid);
+      const bool sc = ((mk >> j) & pat) == pat;
+      if (valid) {
+        double *dst = x3 + site * 80 + off;
+#pragma unroll
+        for (int m = 0; m < 5; m++) {
+          const double v = sc ? o[m] * Num<double>::two32() : o[m];
+          if constexpr (NT & 2) __builtin_nontemporal_store(v, dst + 4 * m);
+          else dst[4 * m] = v;
+        }
+        if (lane < 4) {
+          if (scaler) scaler[site] = (uint8_t)sc;
+          if (sc) acc += W[t];
+        }
+      }
+    }
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
+
+// The same 4x4x4_4b math with contiguous global traffic: each wave moves its
+// 8-site chunk of a child with 16-B loads (1 KiB per wave instruction) into a
+// wave-private LDS tile, reads the B operands from it (swizzled 16-B slots:
+// site * 49 + category * 12 + chunk, conflict-free for the B reads), writes X3
+// back into the x1 tile and stores it with 16-B stores.  No block barriers:
+// LDS keeps one wave's DS instructions in order.
+__device__ __forceinline__ int slot(int c) {  // 16-B chunk of an 8-site tile -> LDS slot
+  const int site = c / 40, r = c - site * 40, cat = r / 10;
+  return site * 49 + cat * 12 + (r - cat * 10);
+}
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <bool PF, int MINW, int ABL = 0, bool BT16 = false>
+__global__ void __launch_bounds__(256, MINW)
+prot_b4t(const double *__restrict__ x1, const double *__restrict__ x2, double *__restrict__ x3,
+         const double *__restrict__ EV, const double *__restrict__ left, const double *__restrict__ right,
+         const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+         int64_t *scaler_sum) {
+  constexpr int S = 20, kSlots = 8 * 49;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int q = lane >> 4, b = (lane >> 2) & 3, j = lane & 3;
+  double AL[5][5], AR[5][5], AE[BT16 ? 1 : 5][5], E16[5], E4[5];
+#pragma unroll
+  for (int m = 0; m < 5; m++)
+#pragma unroll
+    for (int s = 0; s < 5; s++) {
+      AL[m][s] = left[b * S * S + (4 * m + j) * S + 4 * s + q];
+      AR[m][s] = right[b * S * S + (4 * m + j) * S + 4 * s + q];
+      if constexpr (!BT16) AE[m][s] = EV[(4 * s + q) * S + 4 * m + j];
+    }
+  // 16x16x4 A operand: lane 16k + i holds A[i][k] = EV^T[l = i][k = 4s + k] (rows 0..15);
+  // 4x4x4_4b rows 16..19: lane 16k + 4b' + i holds EV^T[16 + i][4s + k]
+#pragma unroll
+  for (int s = 0; s < 5; s++) {
+    E16[s] = EV[(4 * s + q) * S + (lane & 15)];
+    E4[s] = EV[(4 * s + q) * S + 16 + j];
+  }
+  __shared__ f64x2 tiles[4][2][kSlots];
+  f64x2 *T1 = tiles[wv][0], *T2 = tiles[wv][1];
+  const double *T1d = reinterpret_cast<const double *>(T1);
+  const double *T2d = reinterpret_cast<const double *>(T2);
+  double *T1w = reinterpret_cast<double *>(T1);
+  const double mlim = Num<double>::minlik();
+  const unsigned long long pat = 0x1111111111111111ull;
+  long long acc = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wv;
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 8;
+  // B-operand slot offsets (doubles) of this lane for sub-tile t, k-step s
+  int boff[2][5];
+#pragma unroll
+  for (int t = 0; t < 2; t++)
+#pragma unroll
+    for (int s = 0; s < 5; s++) boff[t][s] = slot((4 * t + j) * 40 + b * 10 + 2 * s + (q >> 1)) * 2 + (q & 1);
+  int ioff[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) ioff[i] = slot(i * 64 + lane);
+  f64x2 g1[5], g2[5];
+  auto fetch = [&](int64_t base) {
+    const f64x2 *s1 = reinterpret_cast<const f64x2 *>(x1 + base * 80);
+    const f64x2 *s2 = reinterpret_cast<const f64x2 *>(x2 + base * 80);
+    const int64_t lim = (n - base) * 40;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const int ch = i * 64 + lane;
+      const int cc = ch < lim ? ch : 0;  // clamped, unconditional
+      if constexpr (ABL == 2) {
+        g1[i] = f64x2{1.0 + lane, 0.5}; g2[i] = f64x2{0.25, 2.0 + i};
+      } else {
+        g1[i] = __builtin_nontemporal_load(s1 + cc);
+        g2[i] = __builtin_nontemporal_load(s2 + cc);
+      }
+    }
+  };
+  int64_t base = wave * 8;
+  if (PF && base < n) fetch(base);
+  for (; base < n; base += stride) {
+    if (!PF) fetch(base);
+    int W[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const int64_t st = base + 4 * t + j;
+      W[t] = wgt_at(wgt, st < n ? st : n - 1, ws);
+    }
+#pragma unroll
+    for (int i = 0; i < 5; i++) { T1[ioff[i]] = g1[i]; T2[ioff[i]] = g2[i]; }
+    if (PF && base + stride < n) fetch(base + stride);
+    wave_sync_lds();
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      double A1[5], A2[5];
+#pragma unroll
+      for (int s = 0; s < 5; s++) { A1[s] = T1d[boff[t][s]]; A2[s] = T2d[boff[t][s]]; }
+      double p[5];
+#pragma unroll
+      for (int m = 0; m < 5; m++) {
+        double uL = 0.0, uR = 0.0;
+#pragma unroll
+        for (int s = 0; s < 5; s++) {
+          if constexpr (ABL == 1) { uL += AL[m][s] * A1[s]; uR += AR[m][s] * A2[s]; }
+          else { uL = mfma4(AL[m][s], A1[s], uL); uR = mfma4(AR[m][s], A2[s], uR); }
+        }
+        p[m] = uL * uR;
+      }
+      double o[5];
+      bool small = true;
+      if constexpr (BT16 && ABL != 1) {
+        f64x4 X0 = {0.0, 0.0, 0.0, 0.0};
+        double X1 = 0.0;
+#pragma unroll
+        for (int s = 0; s < 5; s++) {
+          X0 = __builtin_amdgcn_mfma_f64_16x16x4f64(E16[s], p[s], X0, 0, 0, 0);
+          X1 = mfma4(E4[s], p[s], X1);
+        }
+        o[0] = X0[0]; o[1] = X0[1]; o[2] = X0[2]; o[3] = X0[3]; o[4] = X1;
+      } else {
+#pragma unroll
+        for (int m = 0; m < 5; m++) {
+          double x = 0.0;
+#pragma unroll
+          for (int s = 0; s < 5; s++) {
+            if constexpr (ABL == 1) x += E16[s] * p[s];
+            else x = mfma4(AE[m][s], p[s], x);
+          }
+          o[m] = x;
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 5; m++) small = small && (__builtin_fabs(o[m]) < mlim);
+      const int64_t site = base + 4 * t + j;
+      const bool valid = site < n;
+      const unsigned long long mk = __ballot(small && valid);
+      const bool sc = ((mk >> j) & pat) == pat;
+#pragma unroll
+      for (int m = 0; m < 5; m++) T1w[boff[t][m]] = sc ? o[m] * Num<double>::two32() : o[m];
+      if (lane < 4 && valid) {
+        if (scaler) scaler[site] = (uint8_t)sc;
+        if (sc) acc += W[t];
+      }
+    }
+    wave_sync_lds();
+    {
+      f64x2 *d = reinterpret_cast<f64x2 *>(x3 + base * 80);
+      const int64_t lim = (n - base) * 40;
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        const int ch = i * 64 + lane;
+        const f64x2 v = T1[ioff[i]];
+        if constexpr (ABL == 2) { if (v.x == -1.25) d[lane] = v; }
+        else if (ch < lim) __builtin_nontemporal_store(v, d + ch);
+      }
+    }
+    wave_sync_lds();
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
+__global__ void fill(double *p, int64_t n, uint64_t seed, double s4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 31;
+    double v = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    if (s4 != 1.0 && ((i / 80) % 4) == 0) v *= s4;
+    p[i] = v;
+  }
+}
+
+typedef double f64x2v __attribute__((ext_vector_type(2)));
+__global__ void __launch_bounds__(256) stream3(const f64x2v *__restrict__ a, const f64x2v *__restrict__ b,
+                                               f64x2v *__restrict__ c, int64_t nrec) {
+  constexpr int V = 4;
+  const int64_t stride = (int64_t)gridDim.x * 256 * V;
+  for (int64_t i = (int64_t)blockIdx.x * 256 * V + threadIdx.x; i < nrec; i += stride) {
+    f64x2v x[V], y[V];
+#pragma unroll
+    for (int v = 0; v < V; v++) {
+      x[v] = __builtin_nontemporal_load(a + i + 256 * v);
+      y[v] = __builtin_nontemporal_load(b + i + 256 * v);
+    }
+#pragma unroll
+    for (int v = 0; v < V; v++) __builtin_nontemporal_store(x[v] + y[v], c + i + 256 * v);
+  }
+}
+
+struct Set { double *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
+
+int main(int argc, char **argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : (1 << 18);
+  const int R = 4, reps = argc > 2 ? atoi(argv[2]) : 30, rounds = 5;
+  hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
+  const int CUs = prop.multiProcessorCount;
+  std::vector<Set> sets(R);
+  double *EV, *L, *Rm; unsigned long long *ws;
+  CK(hipMalloc(&EV, 400 * 8)); CK(hipMalloc(&L, 1600 * 8)); CK(hipMalloc(&Rm, 1600 * 8));
+  CK(hipMalloc(&ws, kWsWords * 8)); CK(hipMemset(ws, 0, kWsWords * 8));
+  fill<<<8, 64>>>(EV, 400, 7, 1.0); fill<<<32, 64>>>(L, 1600, 8, 1.0); fill<<<32, 64>>>(Rm, 1600, 9, 1.0);
+  for (auto &s : sets) {
+    CK(hipMalloc(&s.x1, n * 640)); CK(hipMalloc(&s.x2, n * 640)); CK(hipMalloc(&s.x3, n * 640));
+    CK(hipMalloc(&s.wgt, n * 4)); CK(hipMalloc(&s.sc, n)); CK(hipMalloc(&s.sum, 8));
+    fill<<<2048, 256>>>(s.x1, n * 80, 10, 1e-14); fill<<<2048, 256>>>(s.x2, n * 80, 20, 1.0);
+    std::vector<int> wv(n);
+    for (int64_t i = 0; i < n; i++) wv[i] = 1 + (int)(i % 3);
+    CK(hipMemcpy(s.wgt, wv.data(), n * 4, hipMemcpyHostToDevice));
+  }
+  CK(hipDeviceSynchronize());
+  auto occ = [&](const void *k) { int b = 0; CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, 256, 0)); return b; };
+  struct V { std::string name; std::function<void(const Set &)> run; std::vector<float> us; };
+  std::vector<V> vs;
+  vs.push_back({"stream 2R+1W (same bytes)", [&](const Set &s) {
+    stream3<<<CUs * 4, 256>>>((const f64x2v *)s.x1, (const f64x2v *)s.x2, (f64x2v *)s.x3, n * 40); }, {}});
+#define ADD(NAME, K, SPB, MUL)                                                                     \
+  {                                                                                                \
+    auto k = K;                                                                                    \
+    const int o = occ((const void *)k);                                                            \
+    const int64_t grid = std::min<int64_t>((n + SPB - 1) / SPB, (int64_t)o * CUs * MUL);           \
+    vs.push_back({std::string(NAME) + " occ " + std::to_string(o) + " grid " + std::to_string(grid), \
+                  [=](const Set &s) {                                                              \
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
+                         s.wgt, s.sc, n, ws, s.sum, nullptr); }, {}});                             \
+  }
+#define ADD2(NAME, K, SPB, MUL)                                                                    \
+  {                                                                                                \
+    auto k = K;                                                                                    \
+    const int o = occ((const void *)k);                                                            \
+    const int64_t grid = std::min<int64_t>((n + SPB - 1) / SPB, (int64_t)o * CUs * MUL);           \
+    vs.push_back({std::string(NAME) + " occ " + std::to_string(o) + " grid " + std::to_string(grid), \
+                  [=](const Set &s) {                                                              \
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
+                         s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
+  }
+  ADD("csrc mfma (product)", (&plf_prot_mfma_kernel<true>), 64, 1)
+  ADD2("blk4 T=2 pf plain ld+st", (&prot_blk4<2, 1, true, 0>), 32, 1)
+  ADD2("b4t minw2", (&prot_b4t<false, 2>), 32, 1)
+  ADD2("b4t minw2 bt16", (&prot_b4t<false, 2, 0, true>), 32, 1)
+  ADD2("b4t pf minw2 bt16", (&prot_b4t<true, 2, 0, true>), 32, 1)
+  ADD2("b4t pf minw1 bt16", (&prot_b4t<true, 1, 0, true>), 32, 1)
+  ADD2("b4t minw2 bt16 ablate: no MFMA", (&prot_b4t<false, 2, 1, true>), 32, 1)
+  ADD2("b4t minw2 bt16 ablate: no HBM", (&prot_b4t<false, 2, 2, true>), 32, 1)
+
+  // bit-exact check of every variant against the product MFMA kernel (set 0)
+  {
+    const size_t bytes = n * 640;
+    std::vector<char> ref(bytes), got(bytes), rsc(n), gsc(n);
+    int64_t rsum = 0, gsum = 0;
+    vs[1].run(sets[0]);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(ref.data(), sets[0].x3, bytes, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(rsc.data(), sets[0].sc, n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(&rsum, sets[0].sum, 8, hipMemcpyDeviceToHost));
+    for (size_t i = 2; i < vs.size(); i++) {
+      CK(hipMemset(sets[0].x3, 0xFF, bytes)); CK(hipMemset(sets[0].sc, 7, n)); CK(hipMemset(sets[0].sum, 0, 8));
+      vs[i].run(sets[0]);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(got.data(), sets[0].x3, bytes, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(gsc.data(), sets[0].sc, n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(&gsum, sets[0].sum, 8, hipMemcpyDeviceToHost));
+      size_t bad = 0;
+      for (size_t e = 0; e < bytes / 8; e++) bad += memcmp(ref.data() + 8 * e, got.data() + 8 * e, 8) != 0;
+      if (vs[i].name.find("ablate") != std::string::npos) continue;
+      const bool ok = bad == 0 && !memcmp(rsc.data(), gsc.data(), n) && rsum == gsum;
+      printf("check %-44s %s (%zu values differ; sum %lld vs %lld)\n", vs[i].name.c_str(), ok ? "bit-exact" : "MISMATCH",
+             bad, (long long)gsum, (long long)rsum);
+    }
+  }
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; r++)
+    for (auto &v : vs) {
+      for (int i = 0; i < 3; i++) v.run(sets[i % R]);
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < reps; i++) v.run(sets[i % R]);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      v.us.push_back(ms * 1000.f / reps);
+    }
+  CK(hipGetLastError());
+  printf("n=%lld protein sites, %d reps x %d rounds interleaved, %d buffer sets\n", (long long)n, reps, rounds, R);
+  for (auto &v : vs) {
+    std::sort(v.us.begin(), v.us.end());
+    const double t = v.us[v.us.size() / 2] * 1e-6;
+    printf("%-48s median %8.2f us  %5.1f%% of 8 TB/s  %6.3f G sites/s\n", v.name.c_str(), v.us[v.us.size() / 2],
+           100.0 * 1925.0 * n / t / 8e12, n / t * 1e-9);
+  }
+  return 0;
+}
