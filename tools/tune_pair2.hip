@@ -267,6 +267,103 @@ pair_q(const double *__restrict__ x1, const double *__restrict__ x2, double *__r
   ticket_publish(tot, ws, scaler_sum);
 }
 
+
+// Rolling prefetch ("ring"): the trip's 2U 8-site blocks are loaded one trip
+// ahead, block by block -- block i of the next trip is issued right after
+// block i of this trip is computed -- so every wave keeps ~2U blocks of loads
+// in flight at all times without a second register set.  Loop trips issue
+// their next loads unconditionally (exact vmcnt waits); the last trip of a
+// wave runs as an epilogue without loads.  Full trips only (tuning harness).
+template <int U, int MINW>
+__global__ void __launch_bounds__(256, MINW)
+pair_ring(const double *__restrict__ x1, const double *__restrict__ x2, double *__restrict__ x3,
+          const double *__restrict__ EV, const double *__restrict__ left, const double *__restrict__ right,
+          const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+          int64_t *scaler_sum) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 1, c = (lane >> 1) & 3, g = lane >> 3, sh = lane & 56;
+  double PL[2][4], PR[2][4], E[4][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      PL[kk][l] = left[c * 16 + (2 * h + kk) * 4 + l];
+      PR[kk][l] = right[c * 16 + (2 * h + kk) * 4 + l];
+    }
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int t = 0; t < 2; t++) E[k][t] = EV[4 * k + 2 * h + t];
+  const double m = Num<double>::minlik();
+  long long acc = 0;
+  constexpr int B = 2 * U;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * 4 * 16 * U;
+  const int64_t first = wave * 16 * U;
+  if (first >= n) { block_ticket_sum(0, ws, scaler_sum); return; }
+  const int64_t trips = (n - first + stride - 1) / stride;  // >= 1
+  f64x2 a[B], b[B];
+  int w[B];
+  auto load = [&](int i, int64_t base) {
+    const int64_t site0 = base + i * 8;
+    a[i] = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(x1 + site0 * 16) + lane);
+    b[i] = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
+    w[i] = wgt_at(wgt, site0 + g, ws);
+  };
+  auto compute = [&](int i, int64_t base) {
+    const int64_t site0 = base + i * 8;
+    const double a0 = dpp_f64<kQuadEven>(a[i].x), a1 = dpp_f64<kQuadEven>(a[i].y);
+    const double a2 = dpp_f64<kQuadOdd>(a[i].x), a3 = dpp_f64<kQuadOdd>(a[i].y);
+    const double b0 = dpp_f64<kQuadEven>(b[i].x), b1 = dpp_f64<kQuadEven>(b[i].y);
+    const double b2 = dpp_f64<kQuadOdd>(b[i].x), b3 = dpp_f64<kQuadOdd>(b[i].y);
+    double pm[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+      double v = a0 * PL[kk][0];
+      v += a1 * PL[kk][1]; v += a2 * PL[kk][2]; v += a3 * PL[kk][3];
+      double y = b0 * PR[kk][0];
+      y += b1 * PR[kk][1]; y += b2 * PR[kk][2]; y += b3 * PR[kk][3];
+      pm[kk] = v * y;
+    }
+    const double p0 = dpp_f64<kQuadEven>(pm[0]), p1 = dpp_f64<kQuadEven>(pm[1]);
+    const double p2 = dpp_f64<kQuadOdd>(pm[0]), p3 = dpp_f64<kQuadOdd>(pm[1]);
+    double o[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      double x = 0.0;
+      x += p0 * E[0][t]; x += p1 * E[1][t]; x += p2 * E[2][t]; x += p3 * E[3][t];
+      o[t] = x;
+    }
+    const bool small = (__builtin_fabs(o[0]) < m) && (__builtin_fabs(o[1]) < m);
+    const unsigned long long mask = __ballot(small);
+    const bool sc = ((mask >> sh) & 0xFFull) == 0xFFull;
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const double s2 = o[t] * Num<double>::two32();
+      o[t] = sc ? s2 : o[t];
+    }
+    f64x2 ov = {o[0], o[1]};
+    __builtin_nontemporal_store(ov, reinterpret_cast<f64x2 *>(x3 + site0 * 16) + lane);
+    if ((lane & 7) == 0) {
+      if (scaler) scaler[site0 + g] = (uint8_t)sc;
+      if (sc) acc += w[i];
+    }
+  };
+  int64_t base = first;
+#pragma unroll
+  for (int i = 0; i < B; i++) load(i, base);
+  for (int64_t t = 1; t < trips; t++, base += stride) {
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+      compute(i, base);
+      load(i, base + stride);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < B; i++) compute(i, base);
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
 __global__ void fill(double *p, int64_t n, uint64_t seed, double scale4) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
@@ -294,6 +391,13 @@ __global__ void __launch_bounds__(256) stream3(const f64x2v *__restrict__ a, con
 #pragma unroll
     for (int v = 0; v < V; v++) __builtin_nontemporal_store(x[v] + y[v], c + i + 256 * v);
   }
+}
+
+__global__ void __launch_bounds__(256) stream1(const f64x2v *__restrict__ a, const f64x2v *__restrict__ b,
+                                               f64x2v *__restrict__ c, int64_t nrec) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nrec; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(a + i) + __builtin_nontemporal_load(b + i), c + i);
 }
 
 struct Set { double *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
@@ -325,12 +429,14 @@ int main(int argc, char **argv) {
   std::vector<V> vs;
   vs.push_back({"stream 2R+1W V=4 grid 4/CU", 384.0 * n, [&](const Set &s) {
     stream3<<<CUs * 4, 256>>>((const f64x2v *)s.x1, (const f64x2v *)s.x2, (f64x2v *)s.x3, n * 8); }, {}});
+  vs.push_back({"stream 2R+1W V=1 grid 2/CU", 384.0 * n, [&](const Set &s) {
+    stream1<<<CUs * 2, 256>>>((const f64x2v *)s.x1, (const f64x2v *)s.x2, (f64x2v *)s.x3, n * 8); }, {}});
   std::vector<std::string> checkme;
 #define ADD(NAME, K, MUL)                                                                          \
   {                                                                                                \
     auto k = K;                                                                                    \
     const int o = occ((const void *)k);                                                            \
-    const int64_t grid = std::min<int64_t>((n + 127) / 128, (int64_t)o * CUs * MUL);               \
+    const int64_t grid = std::min<int64_t>((n + 127) / 128, (int64_t)(o * CUs * MUL));               \
     vs.push_back({std::string(NAME) + " occ " + std::to_string(o) + " grid " + std::to_string(grid), 389.0 * n, \
                   [=](const Set &s) {                                                              \
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
@@ -345,24 +451,29 @@ int main(int argc, char **argv) {
                          s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
   }
   ADD("csrc pair U=2", (&plf_dna_f64_pair_kernel<2, true, 1, true>), 1)
-  ADD("lds U=1 pipe grid/2", (&pair_lds<1, true, 1>), 0.5)
-  ADDB("queue blk256 U=2 x4/CU", (&pair_q<256, 2>), 256, 4)
-  ADDB("queue blk256 U=1 x4/CU", (&pair_q<256, 1>), 256, 4)
-  ADDB("queue blk512 U=2 x2/CU", (&pair_q<512, 2>), 512, 2)
-  ADDB("queue blk1024 U=2 x1/CU", (&pair_q<1024, 2>), 1024, 1)
-  ADDB("queue blk1024 U=1 x1/CU", (&pair_q<1024, 1>), 1024, 1)
+  ADD("csrc pair U=2 x0.5", (&plf_dna_f64_pair_kernel<2, true, 1, true>), 0.5)
+  ADD("csrc pair U=2 x0.75", (&plf_dna_f64_pair_kernel<2, true, 1, true>), 0.75)
+  ADD("csrc pair U=1 x1", (&plf_dna_f64_pair_kernel<1, true, 1, true>), 1)
+  ADD("csrc pair U=1 x0.5", (&plf_dna_f64_pair_kernel<1, true, 1, true>), 0.5)
+  ADD("csrc pair U=1 x0.25", (&plf_dna_f64_pair_kernel<1, true, 1, true>), 0.25)
+  ADD("csrc pair U=1 x0.375", (&plf_dna_f64_pair_kernel<1, true, 1, true>), 0.375)
+  ADD("csrc pair U=1 x0.75", (&plf_dna_f64_pair_kernel<1, true, 1, true>), 0.75)
+  ADD("lds U=1 pipe x0.5", (&pair_lds<1, true, 1>), 0.5)
+  ADD("lds U=1 pipe x0.375", (&pair_lds<1, true, 1>), 0.375)
+  ADD("ring U=1 x0.5", (&pair_ring<1, 1>), 0.5)
+  ADD("ring U=1 x0.25", (&pair_ring<1, 1>), 0.25)
 
   // bit-exact check of every variant against the csrc kernel on set 0
   {
     const size_t bytes = n * 128;
     std::vector<char> ref(bytes), got(bytes), rsc(n), gsc(n);
     int64_t rsum = 0, gsum = 0;
-    vs[1].run(sets[0]);
+    vs[2].run(sets[0]);
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(ref.data(), sets[0].x3, bytes, hipMemcpyDeviceToHost));
     CK(hipMemcpy(rsc.data(), sets[0].sc, n, hipMemcpyDeviceToHost));
     CK(hipMemcpy(&rsum, sets[0].sum, 8, hipMemcpyDeviceToHost));
-    for (size_t i = 2; i < vs.size(); i++) {
+    for (size_t i = 3; i < vs.size(); i++) {
       CK(hipMemset(sets[0].x3, 0xFF, bytes)); CK(hipMemset(sets[0].sc, 7, n)); CK(hipMemset(sets[0].sum, 0, 8));
       vs[i].run(sets[0]);
       CK(hipDeviceSynchronize());
