@@ -73,6 +73,13 @@ def combine_ranks(wall_ms, dev_ms, got_sum, expect_sum, device, world):
     return float(t[0]), float(t[1]), int(tot[0]) == int(tot[1])
 
 
+def traffic_key(a):
+    """The configuration a committed PMC traffic record belongs to."""
+    mode = "exact" if a.exact else "fma"
+    fuse = 0 if a.no_fuse else a.fuse
+    return f"{a.workload}:{a.dtype}:{mode}:{'tips' if a.tips else 'dense'}:fuse{fuse}:sites{a.sites}"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -101,6 +108,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=4.0,
                     help="wall seconds per CPU-baseline variant (bounded sample)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_pmc_traffic.json"))
+    ap.add_argument("--print-traffic-key", action="store_true",
+                    help="print the configuration key of PMC traffic records and exit")
     return ap.parse_args()
 
 
@@ -435,6 +444,9 @@ WORKLOADS = {"node": NodeWorkload, "tree64": Tree64Workload, "nodes64": Nodes64W
 
 def main():
     a = parse()
+    if a.print_traffic_key:
+        print(traffic_key(a))
+        return
     os.environ["PLFX_FUSE"] = "0" if a.no_fuse else str(a.fuse)  # read by plfx_ctx_create
     import torch
     import torch.distributed as dist
@@ -522,11 +534,16 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None
-        ttp = Path(a.traffic_json).with_name(Path(a.traffic_json).name.replace("pmc_traffic", "tree_pmc_traffic"))
-        if a.workload == "tree64" and ttp.exists():  # per step (all of the step's launches)
+        # multi-kernel / other workloads: per-step traffic from tools/pmc_step.py,
+        # matched on the configuration key and the algorithmic bytes per step
+        wtp = {"tree64": "tree_pmc_traffic", "nodes64": "nodes64_pmc_traffic",
+               "protein": "protein_pmc_traffic"}.get(a.workload)
+        ttp = Path(a.traffic_json).with_name(Path(a.traffic_json).name.replace("pmc_traffic", wtp)) if wtp else None
+        if ttp is not None and ttp.exists():
             try:
                 tj = json.loads(ttp.read_text())
-                if abs(tj.get("algorithmic_bytes_per_step", 0) - wl.bytes_per_step) < 1:
+                if (abs(tj.get("algorithmic_bytes_per_step", 0) - wl.bytes_per_step) < 1
+                        and tj.get("key", traffic_key(a)) == traffic_key(a)):
                     traffic = tj.get("hbm_bytes_per_step")
             except (ValueError, OSError):
                 traffic = None

@@ -40,3 +40,18 @@ step tree_write 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/tree_write -o run --ou
 ALG=$(python3 -c "import json; d=json.loads(open('$OUT/tree_bench.log').read().strip().splitlines()[-1]); print(d['roofline']['bytes_per_step'])")
 python3 $R/tools/pmc_step.py $OUT/tree_fetch/run_counter_collection.csv $OUT/tree_write/run_counter_collection.csv $OUT/tree_pmc_traffic.json --steps 22 --alg-bytes $ALG > /dev/null && echo tree traffic ok
 
+# protein (configs[4], FMA on the f64 matrix cores) and nodes64 (configs[3]'s
+# per-GPU shard): bench line, kernel trace, the two PMC passes, per-step traffic
+for W in protein nodes64; do
+  case $W in protein) K=100; P=20 ;; nodes64) K=20; P=6 ;; esac
+  WB="$R/bench.py --workload $W --no-cpu-baseline"
+  step ${W}_bench 300 python $WB --steps $K --warmup 5
+  tail -1 $OUT/${W}_bench.log
+  step ${W}_trace 300 rocprofv3 --kernel-trace --stats -T -d $OUT/${W}_trace -o run --output-format csv -- python3 $WB --steps $K --warmup 5
+  step ${W}_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/${W}_fetch -o run --output-format csv -- python3 $WB --steps $P --warmup 2 --launch bound
+  step ${W}_write 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/${W}_write -o run --output-format csv -- python3 $WB --steps $P --warmup 2 --launch bound
+  ALG=$(python3 -c "import json; d=json.loads(open('$OUT/${W}_bench.log').read().strip().splitlines()[-1]); print(d['roofline']['bytes_per_step'])")
+  KEY=$(python3 $R/bench.py --workload $W --print-traffic-key)
+  EXCL=""; [ $W = nodes64 ] && EXCL="--exclude root_lnl"  # the 64 lnL launches run after the timed steps
+  python3 $R/tools/pmc_step.py $OUT/${W}_fetch/run_counter_collection.csv $OUT/${W}_write/run_counter_collection.csv $OUT/${W}_pmc_traffic.json --steps $((P + 2)) --alg-bytes $ALG --key $KEY $EXCL > /dev/null && echo "$W traffic ok"
+done

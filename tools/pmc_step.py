@@ -21,10 +21,12 @@ import statistics as st
 PLF_KERNELS = ("plf_dna", "root_lnl", "plf_prot", "pmatrix")
 
 
-def groups(path, name):
+def groups(path, name, exclude=()):
     g = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != name or not r["Kernel_Name"].startswith(PLF_KERNELS):
+            continue
+        if r["Kernel_Name"].startswith(tuple(exclude)):
             continue
         g[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
     return g
@@ -37,8 +39,11 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--steps", type=int, required=True)
     ap.add_argument("--alg-bytes", type=float, required=True)
+    ap.add_argument("--exclude", action="append", default=[],
+                    help="kernel-name prefix launched outside the timed steps (nodes64: root_lnl)")
+    ap.add_argument("--key", default=None, help="bench.py --print-traffic-key of the profiled command")
     a = ap.parse_args()
-    fg, wg = groups(a.fetch, "FETCH_SIZE"), groups(a.write, "WRITE_SIZE")
+    fg, wg = groups(a.fetch, "FETCH_SIZE", a.exclude), groups(a.write, "WRITE_SIZE", a.exclude)
     rows, tot = [], 0.0
     for key in sorted(set(fg) & set(wg)):
         f = sum(fg[key]) * 1024 * 2 / a.steps
@@ -50,6 +55,8 @@ def main():
     rec = {"groups": rows, "hbm_bytes_per_step": tot, "algorithmic_bytes_per_step": a.alg_bytes,
            "traffic_over_algorithmic": tot / a.alg_bytes,
            "correction": "FETCH_SIZE x1024 x2, WRITE_SIZE x1024 (MI355X_MICROARCH.md, HBM section)"}
+    if a.key:
+        rec["key"] = a.key
     json.dump(rec, open(a.out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
