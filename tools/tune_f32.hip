@@ -149,14 +149,11 @@ int main(int argc, char **argv) {
                          s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
   }
   ADD("csrc cat U=4", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 1)
-  ADD("csrc cat U=2", (&plf_dna_kernel<float, 2, true, true, 1>), 128, 1)
-  ADD("csrc cat U=8", (&plf_dna_kernel<float, 8, true, true, 1>), 512, 1)
-  ADD("pf U=2", (&cat_pf<2, 1>), 128, 1)
-  ADD("pf U=4", (&cat_pf<4, 1>), 256, 1)
-  ADD("pf U=1", (&cat_pf<1, 1>), 64, 1)
-  ADD("pf U=2 grid/2", (&cat_pf<2, 1>), 128, 0.5)
-  ADD("pf U=4 grid/2", (&cat_pf<4, 1>), 256, 0.5)
-  ADD("csrc cat U=4 grid/2", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 0.5)
+  ADD("csrc cat U=3", (&plf_dna_kernel<float, 3, true, true, 1>), 192, 1)
+  ADD("csrc cat U=4 minw4", (&plf_dna_kernel<float, 4, true, true, 4>), 256, 1)
+  ADD("csrc cat U=3 minw4", (&plf_dna_kernel<float, 3, true, true, 4>), 192, 1)
+  ADD("csrc cat U=2 x1.25", (&plf_dna_kernel<float, 2, true, true, 1>), 128, 1.25)
+  ADD("csrc cat U=4 x1.333", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 1.3334)
   {
     const size_t bytes = n * 64;
     std::vector<char> ref(bytes), got(bytes), rsc(n), gsc(n);
