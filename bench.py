@@ -16,7 +16,9 @@ the timed region one RCCL all-reduce combines the per-rank scaler totals.
 
 Prints ONE JSON line on rank 0 (driver contract), with
   roofline:      algorithmic bytes per launch / average launch duration
-                 (HIP events on the launch stream) against 8 TB/s; `traffic`
+                 (HIP events on the launch stream) against 8 TB/s, at SURVEY
+                 8(d)'s 385 B/site (x1, x2 read, x3 and the scaler byte
+                 written; `achieved_incl_wgt` adds the 4-B weight read); `traffic`
                  = HBM bytes per launch from the committed rocprofv3 PMC pass
                  (profiles/), or null;
   cpu_baseline:  the oracle's OpenMP f64 port on this host's cores over a
@@ -39,10 +41,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SEED = 20250117
 
 
+WGT_BYTES = 4  # the kernels also read the int32 site weight for the weighted scaler sum
+
+
 def bytes_per_site(dtype_bytes):
-    # read x1, x2 (16 values each), write x3 (16 values), write 1 scaler byte,
-    # read 4-byte wgt (the kernel computes the weighted scaler sum)
-    return 3 * 16 * dtype_bytes + 1 + 4
+    # SURVEY 8(d) headline: read x1, x2 (16 values each), write x3 (16 values),
+    # write 1 scaler byte -- 385 B in f64.  The 4-byte weight the kernel also
+    # reads is reported beside it (roofline.achieved_incl_wgt), not in it.
+    return 3 * 16 * dtype_bytes + 1
 
 
 def coll_device(device):
@@ -208,6 +214,7 @@ class NodeWorkload:
         self.sites_per_step = n
         self.bytes_per_step = bytes_per_site(esz) * n
         self.bytes_per_site = bytes_per_site(esz)
+        self.wgt_bytes_per_step = WGT_BYTES * n
         self.config = {
             "workload": f"DNA 4-state x 4 Gamma cats, 1 inner node per GPU per step, {n} sites, "
                         f"{a.dtype} (BASELINE configs[1])",
@@ -342,6 +349,7 @@ class Nodes64Workload:
         self.sites_per_step = self.nn * n
         self.bytes_per_site = bytes_per_site(esz)
         self.bytes_per_step = self.nn * self.bytes_per_site * n
+        self.wgt_bytes_per_step = WGT_BYTES * self.nn * n
         self.config = {
             "workload": f"DNA 4-state, 512 independent inner nodes sharded 64 per GPU, {n} sites, "
                         f"{a.dtype} (BASELINE configs[3]); lnL all-reduce after the timed region",
@@ -398,8 +406,9 @@ class ProteinWorkload:
                                   s=torch.zeros(1, dtype=torch.int64, device=dev)))
         self.sites_per_step = n
         # --tips: the left child is a tip (one code byte per site, plfx.h section 8)
-        self.bytes_per_site = (1 if a.tips else V * esz) + 2 * V * esz + 1 + 4
+        self.bytes_per_site = (1 if a.tips else V * esz) + 2 * V * esz + 1  # 1921 B f64
         self.bytes_per_step = self.bytes_per_site * n
+        self.wgt_bytes_per_step = WGT_BYTES * n
         mode = ('FMA (within 1e-12 of exact)' if esz == 8 else 'FMA') if self.fma else 'exact'
         self.config = {
             "workload": f"Protein 20-state x 4 Gamma cats, 1 inner node per GPU per step, {n} sites, "
@@ -542,7 +551,8 @@ def main():
         if ttp is not None and ttp.exists():
             try:
                 tj = json.loads(ttp.read_text())
-                if (abs(tj.get("algorithmic_bytes_per_step", 0) - wl.bytes_per_step) < 1
+                if (abs(tj.get("algorithmic_bytes_per_step", 0) - wl.bytes_per_step
+                        - getattr(wl, "wgt_bytes_per_step", 0)) < 1
                         and tj.get("key", traffic_key(a)) == traffic_key(a)):
                     traffic = tj.get("hbm_bytes_per_step")
             except (ValueError, OSError):
@@ -576,6 +586,10 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "bytes_per_site": wl.bytes_per_site,
+                **({"achieved_incl_wgt": (wl.bytes_per_step + wl.wgt_bytes_per_step)
+                                         / (per_step_ms * 1e-3) / 1e9,
+                    "bytes_per_site_incl_wgt": wl.bytes_per_site + WGT_BYTES}
+                   if hasattr(wl, "wgt_bytes_per_step") else {}),
                 "bytes_per_step": wl.bytes_per_step,
                 "kernel_avg_us": per_step_ms * 1e3,
             },
