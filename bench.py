@@ -551,8 +551,7 @@ def main():
         if ttp is not None and ttp.exists():
             try:
                 tj = json.loads(ttp.read_text())
-                if (abs(tj.get("algorithmic_bytes_per_step", 0) - wl.bytes_per_step
-                        - getattr(wl, "wgt_bytes_per_step", 0)) < 1
+                if (abs(tj.get("algorithmic_bytes_per_step", 0) - wl.bytes_per_step) < 1
                         and tj.get("key", traffic_key(a)) == traffic_key(a)):
                     traffic = tj.get("hbm_bytes_per_step")
             except (ValueError, OSError):

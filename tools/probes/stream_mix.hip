@@ -43,9 +43,10 @@ __global__ void __launch_bounds__(256) mix(Ptrs p, int64_t nrec) {
 }
 
 template <int R, int W, int U>
-void run(Ptrs p, int64_t nrec, int CUs) {
+void run(Ptrs p, int64_t nrec, int CUs, int per_cu = 0) {
   int occ = 0;
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mix<R, W, U>, 256, 0));
+  if (per_cu > 0 && per_cu < occ) occ = per_cu;  // fewer blocks (bytes in flight) per CU
   const int grid = occ * CUs;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -82,5 +83,11 @@ int main() {
   run<4, 3, 1>(p, nrec, C); run<4, 3, 2>(p, nrec, C);
   run<8, 7, 1>(p, nrec, C); run<8, 7, 2>(p, nrec, C);
   run<8, 1, 1>(p, nrec, C); run<1, 8, 2>(p, nrec, C); run<0 + 1, 4, 2>(p, nrec, C);
+  // bytes in flight: the same mixes at 1..4 blocks per CU
+  for (int pc : {1, 2, 3, 4}) {
+    run<2, 1, 1>(p, nrec, C, pc); run<2, 1, 4>(p, nrec, C, pc);
+    run<4, 3, 1>(p, nrec, C, pc); run<4, 3, 2>(p, nrec, C, pc);
+    run<8, 7, 1>(p, nrec, C, pc); run<8, 7, 2>(p, nrec, C, pc);
+  }
   return 0;
 }
