@@ -393,6 +393,38 @@ int plfx_instance_run(plfx_ctx *ctx, const void *in_left, const void *in_right, 
                          (const double *)right, nullptr, out_scaler, nullptr, stream);
 }
 
+int plfx_instance_run_host(plfx_ctx *ctx, const void *in_left, const void *in_right,
+                           void *out_clv, uint8_t *out_scaler, uint32_t alignment_sites,
+                           uint32_t window_size, int layout, int dtype) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  if (layout != PLFX_LAYOUT_COMBINED && layout != PLFX_LAYOUT_SEPARATE)
+    return fail(ctx, PLFX_ERR_INVALID, "bad layout %d", layout);
+  if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
+  if (!in_left || !in_right || (alignment_sites > 0 && !out_clv))
+    return fail(ctx, PLFX_ERR_INVALID, "null instance buffer");
+  const size_t es = dtype == PLFX_F32 ? 4 : 8, n = alignment_sites;
+  const size_t lbytes = (80 + 16 * n) * es;                                        // active prefix of in_left
+  const size_t rbytes = ((layout == PLFX_LAYOUT_COMBINED ? 80 : 64) + 16 * n) * es;  // and of in_right
+  const size_t obytes = 16 * n * es;
+  const size_t o_l = 0, o_r = round_up(lbytes, 256), o_o = o_r + round_up(rbytes, 256);
+  const size_t o_s = o_o + round_up(obytes, 256);
+  int rc = ensure_dbuf(ctx, o_s + round_up(std::max<size_t>(n, 1), 256));
+  if (rc != PLFX_OK) return rc;
+  char *d = static_cast<char *>(ctx->d_buf);
+  hipStream_t s = ctx->stream;
+  PLFX_HIP(ctx, hipMemcpyAsync(d + o_l, in_left, lbytes, hipMemcpyHostToDevice, s));
+  PLFX_HIP(ctx, hipMemcpyAsync(d + o_r, in_right, rbytes, hipMemcpyHostToDevice, s));
+  rc = plfx_instance_run(ctx, d + o_l, d + o_r, d + o_o, out_scaler ? (uint8_t *)(d + o_s) : nullptr,
+                         alignment_sites, window_size, layout, dtype, s);
+  if (rc != PLFX_OK) return rc;
+  if (n > 0) {
+    PLFX_HIP(ctx, hipMemcpyAsync(out_clv, d + o_o, obytes, hipMemcpyDeviceToHost, s));
+    if (out_scaler) PLFX_HIP(ctx, hipMemcpyAsync(out_scaler, d + o_s, n, hipMemcpyDeviceToHost, s));
+  }
+  PLFX_HIP(ctx, hipStreamSynchronize(s));
+  return PLFX_OK;
+}
+
 int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *nodes, int count,
                        const void *EV, int64_t n, const int32_t *wgt, void *stream) {
   if (!ctx) return PLFX_ERR_INVALID;

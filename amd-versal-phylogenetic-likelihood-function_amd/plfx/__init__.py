@@ -40,7 +40,7 @@ EXPORTS = (
     "plfx_ctx_create", "plfx_ctx_destroy", "plfx_last_error", "plfx_get_version",
     "plfx_ctx_stream", "plfx_ctx_device", "plfx_ctx_synchronize",
     "plfx_plf_f32", "plfx_plf_f64", "plfx_plf_dev_f32", "plfx_plf_dev_f64",
-    "plfx_instance_run", "plfx_scaler_sum",
+    "plfx_instance_run", "plfx_instance_run_host", "plfx_scaler_sum",
     "plfx_tb_alignments_per_instance", "plfx_tb_alignments_padding",
     "plfx_tb_instance_site_offset", "plfx_tb_elements_per_instance",
     "plfx_tb_instance_elements_left", "plfx_tb_instance_elements_right",
@@ -109,6 +109,7 @@ def load():
         getattr(L, f"plfx_plf_{s}").argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, C.POINTER(i32)]
         getattr(L, f"plfx_plf_dev_{s}").argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
     L.plfx_instance_run.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, C.c_uint32, i32, i32, vp]
+    L.plfx_instance_run_host.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, C.c_uint32, i32, i32]
     L.plfx_scaler_sum.argtypes = [vp, vp, vp, i64, vp, vp]
     tbp = C.POINTER(_TB)
     for name in ("alignments_per_instance", "instance_site_offset",
@@ -291,6 +292,29 @@ class Context:
                                               p(out_scaler), n, int(window_size), int(layout),
                                               F32 if dt == torch.float32 else F64,
                                               _stream_handle(stream)))
+
+    def instance_run_host(self, in_left, in_right, out_clv, out_scaler, alignment_sites,
+                          window_size, layout):
+        """instance_run on numpy host buffers, synchronous (bo.write -> run ->
+        bo.read, host_mem.cpp:293-318)."""
+        import numpy as np
+
+        dt = in_left.dtype
+        if dt not in (np.float32, np.float64) or in_right.dtype != dt or out_clv.dtype != dt:
+            raise PlfxError(ERR_INVALID, "instance buffers must share a float dtype")
+        hdr_r = 80 if layout == LAYOUT_COMBINED else 64
+        n = int(alignment_sites)
+        if in_left.size < 80 + 16 * n or in_right.size < hdr_r + 16 * n or out_clv.size < 16 * n:
+            raise PlfxError(ERR_INVALID, "instance buffers too small for alignment_sites")
+        if out_scaler is not None and (out_scaler.dtype != np.uint8 or out_scaler.size < n):
+            raise PlfxError(ERR_INVALID, "out_scaler must be uint8 with >= alignment_sites bytes")
+        for a in (in_left, in_right, out_clv, out_scaler):
+            if a is not None and not a.flags.c_contiguous:
+                raise PlfxError(ERR_INVALID, "instance buffers must be C-contiguous")
+        p = lambda a: None if a is None else C.c_void_p(a.ctypes.data)  # noqa: E731
+        self._check(self._L.plfx_instance_run_host(self.h, p(in_left), p(in_right), p(out_clv),
+                                                   p(out_scaler), n, int(window_size), int(layout),
+                                                   F32 if dt == np.float32 else F64))
 
     def plf_dev_gen(self, x1, x2, x3, EV, left, right, states, wgt=None, scaler=None,
                     scaler_sum=None, n=None, fma=False, stream=None):

@@ -139,6 +139,16 @@ int plfx_instance_run(plfx_ctx *ctx, const void *in_left, const void *in_right,
                       void *out_clv, uint8_t *out_scaler, uint32_t alignment_sites,
                       uint32_t window_size, int layout, int dtype, void *stream);
 
+/* The same contract on HOST buffers, synchronous -- one accelerator instance
+ * run as host_mem.cpp:293-318 drives it: write the active prefix of the two
+ * input bos (bo.write(..., active bytes), :297-298), run the movers and the
+ * graph (:305), read back alignment_sites CLVs and scaler bytes (:313-314).
+ * The copies go through the context's device staging and stream; out_scaler
+ * may be NULL.  Host buffers may be pageable or page-locked. */
+int plfx_instance_run_host(plfx_ctx *ctx, const void *in_left, const void *in_right,
+                           void *out_clv, uint8_t *out_scaler, uint32_t alignment_sites,
+                           uint32_t window_size, int layout, int dtype);
+
 /* ---- (4) scaler reduction (host_mem.cpp:384-388) on the device ---------- */
 /* out_sum (device int64) = sum_j scaler[j] * (wgt ? wgt[j] : 1). */
 int plfx_scaler_sum(plfx_ctx *ctx, const uint8_t *scaler, const int32_t *wgt,

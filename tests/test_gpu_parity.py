@@ -275,6 +275,35 @@ def test_instance_run_contract(ctx, oracle, dtype, layout, P, W, aie):
     assert int((scal.astype(np.int64) * d["wgt"]).sum()) == einc
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("layout,P,W", [(0, 3, 1024), (1, 4, 16288), (1, 1, 8192)])
+def test_instance_run_host_buffers(ctx, oracle, dtype, layout, P, W):
+    """The instance contract on host buffers (bo.write -> run -> bo.read):
+    the reference's packed bos in, n_k CLVs and scaler bytes out, bit-exact,
+    nothing written past n_k."""
+    import plfx
+
+    n = 4099
+    d = oracle.gen_hostmem(n, dtype, 23)
+    tb = plfx.Testbench(n, P, W, layout, 1)
+    e3, esc, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+    out = np.empty(16 * n, dtype)
+    scal = np.empty(n, np.uint8)
+    for k in range(P):
+        nk = tb.alignments_per_instance(k)
+        off = tb.instance_site_offset(k)
+        L, R = tb.pack_instance(k, d["EV"], d["left"], d["right"], d["x1"], d["x2"])
+        o = np.full(tb.instance_elements_out(), -3.0, dtype)
+        sb = np.full(nk + 64, 0xAB, np.uint8)
+        ctx.instance_run_host(L, R, o, sb, nk, W, layout)
+        assert np.all(o[16 * nk:] == -3.0) and np.all(sb[nk:] == 0xAB)
+        out[16 * off:16 * (off + nk)] = o[:16 * nk]
+        scal[off:off + nk] = sb[:nk]
+    assert np.array_equal(bits(out), bits(e3))
+    assert np.array_equal(scal, esc)
+    assert int((scal.astype(np.int64) * d["wgt"]).sum()) == einc
+
+
 def test_rejects_bad_arguments(ctx):
     import plfx
     import torch
