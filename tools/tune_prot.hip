@@ -126,7 +126,7 @@ int main(int argc, char **argv) {
     auto k = &plf_prot_kernel<double, false, true>;
     const int64_t grid = std::min<int64_t>((n + 63) / 64, occ((const void *)k) * CUs);
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, sets[0].x1, sets[0].x2, ref, EV, L, Rm,
-                       sets[0].wgt, refsc, n, ws, refsum);
+                       sets[0].wgt, refsc, n, ws, refsum, nullptr);
     CK(hipDeviceSynchronize());
   }
   std::vector<uint64_t> h_ref(n * 80), h_got(n * 80);
@@ -149,7 +149,18 @@ int main(int argc, char **argv) {
     if (!only || strstr(nm, only) || strstr(nm, "product"))                                        \
       vs.push_back({nm, [=](const Set &s) {                                                        \
         hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,  \
-                           s.wgt, s.sc, n, ws, s.sum); }, {}, true});                              \
+                           s.wgt, s.sc, n, ws, s.sum, nullptr); }, {}, true});                           \
+  }
+#define ADD_K11(NAME, KERNEL, SITES_PER_BLOCK)                                                         \
+  {                                                                                                \
+    auto k = KERNEL;                                                                               \
+    const int o = occ((const void *)k);                                                            \
+    const int64_t grid = std::min<int64_t>((n + SITES_PER_BLOCK - 1) / SITES_PER_BLOCK, (int64_t)o * CUs); \
+    char nm[200]; snprintf(nm, sizeof nm, "%s occ=%d/CU grid=%lld", NAME, o, (long long)grid);      \
+    if (!only || strstr(nm, only) || strstr(nm, "product"))                                        \
+      vs.push_back({nm, [=](const Set &s) {                                                        \
+        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,  \
+                           s.wgt, s.sc, n, ws, s.sum); }, {}, true});                           \
   }
   ADD_K("product exact", (&plf_prot_kernel<double, false, true>), 64)
   ADD_K("product fma-mfma", (&plf_prot_mfma_kernel<true>), 64)
@@ -157,10 +168,10 @@ int main(int argc, char **argv) {
   ADD_K("mfma ablate: no matrix cores", (&plf_prot_mfma_kernel<true, 2, true, 1>), 64)
   ADD_K("mfma ablate: no HBM traffic", (&plf_prot_mfma_kernel<true, 2, true, 2>), 64)
   ADD_K("mfma 16x16x4 only (padded rows)", (&plf_prot_mfma_kernel<true, 2, true, 0, false>), 64)
-  ADD_K("mfma ring (2 tiles in flight)", (&plf_prot_mfma_ring_kernel<true, 2>), 64)
-  ADD_K("mfma probe: ring traffic only", (&probe_tiles<0>), 64)
-  ADD_K("mfma probe: ring traffic + LDS + barriers", (&probe_tiles<1>), 64)
-  ADD_K("mfma ring minw=1", (&plf_prot_mfma_ring_kernel<true, 1>), 64)
+  ADD_K11("mfma ring (2 tiles in flight)", (&plf_prot_mfma_ring_kernel<true, 2>), 64)
+  ADD_K11("mfma probe: ring traffic only", (&probe_tiles<0>), 64)
+  ADD_K11("mfma probe: ring traffic + LDS + barriers", (&probe_tiles<1>), 64)
+  ADD_K11("mfma ring minw=1", (&plf_prot_mfma_ring_kernel<true, 1>), 64)
 
   // FMA-mode reference for the mfma variants
   std::vector<uint64_t> h_fref(n * 80);
@@ -168,7 +179,7 @@ int main(int argc, char **argv) {
     auto k = &plf_prot_mfma_kernel<true>;
     const int64_t grid = std::min<int64_t>((n + 63) / 64, occ((const void *)k) * CUs);
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, sets[0].x1, sets[0].x2, ref, EV, L, Rm,
-                       sets[0].wgt, refsc, n, ws, refsum);
+                       sets[0].wgt, refsc, n, ws, refsum, nullptr);
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(h_fref.data(), ref, n * 640, hipMemcpyDeviceToHost));
   }
