@@ -1116,6 +1116,141 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
   if constexpr (kSum) block_ticket_sum7(acc, ws + (size_t)blockIdx.y * 7 * kWsWords, d.ss);
 }
 
+// Fused six-level subtree ("deep", f64 lane-pair mapping): the 63 ops of a
+// complete binary subtree over 64 dense leaves in one pass -- 64 leaf reads +
+// 63 writes per site (2.02 CLV transfers per node; three-level passes move
+// 2.14, and a 64-taxon tree as nine of them reads the eight level-3 CLVs
+// back).  Node numbering is heap order by level: level 1 = 0..31 (node i over
+// leaves 2i, 2i+1), level 2 = 32..47, level 3 = 48..55, level 4 = 56..59,
+// level 5 = 60, 61, root 62; node 32+i's children are nodes 2i, 2i+1 and so
+// on up.  A trip evaluates eight three-level groups (group q: leaves
+// 8q..8q+7, nodes 4q..4q+3, 32+2q, 33+2q, 48+q) and folds the upper three
+// levels in as a binary carry (at most one pending value per level), so the
+// code is one group body plus three node bodies.  The 63 nodes' matrices sit
+// in LDS (63 KB, one copy per 512-thread block) and every lane reads its 16 per
+// node just in time; each node's weighted scaler sum collects in an LDS
+// counter (a wave reduction + atomic per node and 8-site block, only where a
+// site scaled) and is published by the per-region ticket at the end.  Results
+// are bit-identical to 63 separate updates.  (Measured, tools/gpu_deep.sh,
+// profiles/r01_deep.log: 256/512/768-thread blocks, U = 1/2, next-group
+// prefetch; coded leaves expanded in registers ran 20-40 % slower than the
+// three-level passes' tip tables, so the scheduler keeps tips there.)
+struct DeepDesc {
+  const void *g[64];
+  void *x[63];
+  const void *mat[126];  // left, right of node i at 2i, 2i+1
+  uint8_t *sc[63];
+  int64_t *ss[63];
+};
+
+template <bool kSum, bool NTL, int U, int kThreads>
+__global__ void __launch_bounds__(kThreads, 1)
+plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
+                        const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
+  constexpr int kWaves = kThreads / 64;
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 1, c = (lane >> 1) & 3, g = lane >> 3, sh = lane & 56;
+  __shared__ double mats[63][128];
+  __shared__ unsigned long long nacc[63];
+  for (int e = threadIdx.x; e < 63 * 128; e += kThreads) {
+    const int node = e >> 7, k = e & 127;
+    mats[node][k] = static_cast<const double *>(d.mat[2 * node + (k >> 6)])[k & 63];
+  }
+  if (threadIdx.x < 63) nacc[threadIdx.x] = 0;
+  __syncthreads();
+  double E[4][2];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int t = 0; t < 2; t++) E[k][t] = EV[4 * k + 2 * h + t];
+  const double m = Num<double>::minlik();
+  const int64_t wave = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWaves * 8 * U;
+  for (int64_t base = wave * 8 * U; base < n; base += stride) {
+    int z = 0;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keep the matrix reads inside the loop
+    const double *mz = &mats[0][0] + z;
+    bool valid[U];
+    int64_t sq[U];
+    int w[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+      valid[j] = base + 8 * j + g < n;
+      sq[j] = valid[j] ? base + 8 * j + g : n - 1;  // past n: any valid record (unused)
+      w[j] = kSum ? wgt_at(wgt, sq[j], ws) : 0;
+    }
+    // node `node` of this trip on inputs a, b: output stored, scaler byte and sum
+    auto node_eval = [&](int node, const f64x2 (&a)[U], const f64x2 (&b)[U], f64x2 (&o)[U]) {
+      PairMats M;
+      pair_mats_lds(mz + 128 * node, c, h, M);
+      f64x2 *dst = static_cast<f64x2 *>(d.x[node]);
+      uint8_t *scp = d.sc[node];
+#pragma unroll
+      for (int j = 0; j < U; j++) {
+        bool sc;
+        o[j] = pair_node<false, false>(a[j], b[j], nullptr, nullptr, M, E, valid[j], sh, m, sc);
+        if (valid[j]) {
+          __builtin_nontemporal_store(o[j], dst + (base + 8 * j) * 8 + lane);
+          if ((lane & 7) == 0 && scp) scp[base + 8 * j + g] = (uint8_t)sc;
+        }
+        if (kSum) {
+          const bool mine = (lane & 7) == 0 && valid[j] && sc;
+          if (__ballot(mine)) {  // rare: some site of the block scaled
+            long long v = mine ? (long long)w[j] : 0ll;
+            v += __shfl_xor(v, 8);
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (lane == 0) atomicAdd(&nacc[node], (unsigned long long)v);
+          }
+        }
+      }
+    };
+    f64x2 s3[U], s4[U], s5[U];  // pending level-3/4/5 values of the carry
+#pragma unroll 1
+    for (int q = 0; q < 8; q++) {
+      f64x2 v[8][U];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const f64x2 *gp = static_cast<const f64x2 *>(d.g[8 * q + i]);
+#pragma unroll
+        for (int j = 0; j < U; j++) v[i][j] = ld16<NTL>(gp + sq[j] * 8 + (lane & 7));
+      }
+      f64x2 a1[4][U], a2[2][U], r[U];
+#pragma unroll
+      for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i]);
+#pragma unroll
+      for (int i = 0; i < 2; i++) node_eval(32 + 2 * q + i, a1[2 * i], a1[2 * i + 1], a2[i]);
+      node_eval(48 + q, a2[0], a2[1], r);
+      if (!(q & 1)) {
+#pragma unroll
+        for (int j = 0; j < U; j++) s3[j] = r[j];
+        continue;
+      }
+      f64x2 r4[U];
+      node_eval(56 + (q >> 1), s3, r, r4);
+      if (!(q & 2)) {
+#pragma unroll
+        for (int j = 0; j < U; j++) s4[j] = r4[j];
+        continue;
+      }
+      f64x2 r5[U];
+      node_eval(60 + (q >> 2), s4, r4, r5);
+      if (!(q & 4)) {
+#pragma unroll
+        for (int j = 0; j < U; j++) s5[j] = r5[j];
+        continue;
+      }
+      f64x2 r6[U];
+      node_eval(62, s5, r5, r6);
+    }
+  }
+  if constexpr (kSum) {
+    __syncthreads();
+    if (threadIdx.x < 63)
+      ticket_publish((long long)nacc[threadIdx.x], ws + (size_t)threadIdx.x * kWsWords, d.ss[threadIdx.x]);
+  }
+}
+
 // Fused three-level subtree in the lane = category mapping (f32; any T): the
 // same seven-node pass as plf_dna_f64_septet_kernel, lane = (site q, category
 // c), 16 sites per wave and block of U.  A lane needs 32 matrix values per

@@ -15,6 +15,8 @@
 // blocks over the batch's nodes (blockIdx.y = node).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstdint>
 
@@ -36,6 +38,7 @@ static_assert(sizeof(TripleDescH) == sizeof(dev::TripleDesc), "triple descriptor
 static_assert(kMaxTriples == dev::kMaxTriples && 3 * kMaxTriples <= kMaxBatch, "triple batch size");
 static_assert(sizeof(SeptetDescH) == sizeof(dev::SeptetDesc), "septet descriptor mismatch");
 static_assert(kMaxSeptets == dev::kMaxSeptets, "septet batch size");
+static_assert(sizeof(DeepDescH) == sizeof(dev::DeepDesc), "deep descriptor mismatch");
 
 // Tuned on MI355X (tools/tune_plf.hip, profiles/r01_tune.log):
 // f64 lane-pair kernel, 2 x 16-site steps per trip, non-temporal CLV loads
@@ -271,7 +274,44 @@ hipError_t launch_septets32_t(const dev::SeptetBatch &b, int count, const float 
   return hipGetLastError();
 }
 
+// fused six-level subtrees: 512-thread blocks (one LDS copy of the 63 nodes'
+// matrices per 8 waves), 2 x 8-site blocks per trip, grid = co-resident blocks
+// (tools/gpu_deep.sh, profiles/r01_deep.log)
+template <bool kSum>
+hipError_t launch_deep_t(const dev::DeepDesc &d, const double *EV, const int32_t *wgt, int64_t n,
+                         unsigned long long *ws, int max_blocks, hipStream_t s) {
+  constexpr int kThreads = 512, U = 2;
+  static int resident = 0;
+  auto kernel = &dev::plf_dna_f64_deep_kernel<kSum, kNtl64, U, kThreads>;
+  if (!resident) {
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    (void)hipGetDevice(&dev);
+    (void)hipGetDeviceProperties(&prop, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kernel, kThreads, 0) !=
+            hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    resident = per_cu * prop.multiProcessorCount;
+  }
+  const int64_t per_block = (int64_t)(kThreads / 64) * 8 * U;
+  int64_t gx = (n + per_block - 1) / per_block;
+  gx = std::max<int64_t>(1, std::min<int64_t>(gx, max_blocks > 0 ? max_blocks : resident));
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kThreads), 0, s, d, EV, wgt, n, ws);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_plf_dna_deep(const DeepDescH *t, const void *EV, const int32_t *wgt, int64_t n,
+                               unsigned long long *ws, int max_blocks, hipStream_t s) {
+  dev::DeepDesc d;
+  __builtin_memcpy(&d, t, sizeof(d));
+  bool any_sum = false;
+  for (int q = 0; q < kDeepNodes; q++) any_sum |= t->ss[q] != nullptr;
+  return any_sum ? launch_deep_t<true>(d, (const double *)EV, wgt, n, ws, max_blocks, s)
+                 : launch_deep_t<false>(d, (const double *)EV, wgt, n, ws, max_blocks, s);
+}
 
 hipError_t launch_plf_dna_septets(int dtype, const SeptetDescH *t, int count, const void *EV,
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,

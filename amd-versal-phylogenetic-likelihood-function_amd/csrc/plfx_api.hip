@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <new>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/plfx.h"
@@ -25,7 +26,8 @@ struct plfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
-  int fuse = 2;  // traverse: 2 three-level subtrees + level pairs, 1 level pairs, 0 none (PLFX_FUSE)
+  int fuse = 3;  // traverse: 3 six-level subtrees (f64) before 2's, 2 three-level subtrees +
+                 // level pairs, 1 level pairs, 0 none (PLFX_FUSE)
   unsigned long long *ws = nullptr; // ticket reduction words (kMaxBatch x kWsWords u64), zero at rest
   double *lnl_partials = nullptr;   // kLnlMaxGrid doubles
   unsigned long long *lnl_ticket = nullptr;
@@ -261,7 +263,7 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
     if (v > 0) ctx->max_blocks = v;
   }
   if (const char *env = std::getenv("PLFX_FUSE")) ctx->fuse = std::atoi(env);
-  const size_t ws_regions = std::max(plfx::kMaxBatch, 7 * plfx::kMaxSeptets);
+  const size_t ws_regions = std::max({plfx::kMaxBatch, 7 * plfx::kMaxSeptets, plfx::kDeepNodes});
   const size_t ws_bytes = ws_regions * plfx::kWsWords * sizeof(unsigned long long);
   if (hipMalloc(reinterpret_cast<void **>(&ctx->ws), ws_bytes) != hipSuccess ||
       hipMemsetAsync(ctx->ws, 0, ws_bytes, ctx->stream) != hipSuccess ||
@@ -557,6 +559,40 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
     return x >= 0 && y >= 0 && x != y && !used[x] && !used[y] && !used[p] && level[x] == L &&
            level[y] == L && level[p] == L + 1;
   };
+  // Fused six-level subtrees (DNA f64, plf_dna.hpp DeepDesc): a complete
+  // binary subtree of 63 ops on consecutive levels L..L+5, every op's own slot
+  // free by L (pdep <= L), 64 dense leaves.  Collected per level in heap
+  // order (children left to right before parents): the ops of level k are
+  // lv[k], and lv[k][i]'s children were written by lv[k-1][2i], lv[k-1][2i+1].
+  // Tried before the three-level subtrees.
+  struct Deep {
+    std::vector<int> ops;  // the 63 ops in DeepDesc node order
+    int L;
+  };
+  std::vector<Deep> deeps;
+  std::function<bool(int, int, int, std::vector<int> *)> complete =
+      [&](int r, int D, int L, std::vector<int> *lv) {
+        if (r < 0 || used[r] || level[r] != L + D - 1 || pdep[r] > L) return false;
+        if (D > 1 && (w1[r] < 0 || w2[r] < 0 || w1[r] == w2[r] ||
+                      !complete(w1[r], D - 1, L, lv) || !complete(w2[r], D - 1, L, lv)))
+          return false;
+        lv[D - 1].push_back(r);
+        return true;
+      };
+  if (ctx->fuse >= 3 && states == 4 && dtype == PLFX_F64) {
+    for (int r = 0; r < nops; r++) {
+      if (level[r] < 5 || used[r]) continue;
+      std::vector<int> lv[6];
+      if (!complete(r, 6, level[r] - 5, lv)) continue;
+      bool dense = true;  // coded leaves stay with the three-level passes' tip tables
+      for (int j : lv[0]) dense = dense && !is_tip(ops[j].child1) && !is_tip(ops[j].child2);
+      if (!dense) continue;
+      Deep t{{}, level[r] - 5};
+      for (auto &v : lv) t.ops.insert(t.ops.end(), v.begin(), v.end());
+      for (int j : t.ops) used[j] = 1;
+      deeps.push_back(std::move(t));
+    }
+  }
   if (ctx->fuse >= 2 && states == 4) {
     for (int r = 0; r < nops; r++) {
       Septet t{};
@@ -597,6 +633,33 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
       batch[k].clear();
       tb[k].clear();
       sb[k].clear();
+    }
+    for (const Deep &t : deeps) {
+      if (t.L != lv) continue;
+      plfx::DeepDescH d{};
+      for (int q = 0; q < plfx::kDeepNodes; q++) {
+        const int j = t.ops[q];
+        const plfx_trav_op &o = ops[j];
+        int kq;
+        const int rc = check_node(ctx, node_of(j, &kq), kq, n, j);
+        if (rc != PLFX_OK) return rc;
+        if (q < 32) {  // level 1: the (dense) leaves, child1 then child2
+          d.g[2 * q] = clv[o.child1];
+          d.g[2 * q + 1] = clv[o.child2];
+        }
+        d.x[q] = clv[o.parent];
+        d.mat[2 * q] = pm + (size_t)(2 * o.pmat) * mat * es;
+        d.mat[2 * q + 1] = pm + (size_t)(2 * o.pmat + 1) * mat * es;
+        d.sc[q] = scalers ? scalers[j] : nullptr;
+        d.ss[q] = scaler_sums ? scaler_sums + j : nullptr;
+      }
+      if (n == 0) {
+        for (int64_t *ss : d.ss)
+          if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
+        continue;
+      }
+      hipError_t e = plfx::launch_plf_dna_deep(&d, EV, wgt, n, ctx->ws, ctx->max_blocks, s);
+      if (e != hipSuccess) return hip_fail(ctx, e, "fused six-level launch");
     }
     for (const Septet &t : septets) {
       if (level[t.a[0]] != lv) continue;

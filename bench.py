@@ -98,9 +98,10 @@ def parse():
                     help="protein: fused multiply-add mode (the default; f64 runs on the matrix cores)")
     ap.add_argument("--exact", action="store_true",
                     help="protein: plf()'s separate multiply/add (bit-identical to the double loop)")
-    ap.add_argument("--fuse", type=int, choices=[0, 1, 2], default=2,
-                    help="tree64 schedule (PLFX_FUSE): 2 fused three-level subtrees and "
-                         "level pairs, 1 level pairs only, 0 one launch per level")
+    ap.add_argument("--fuse", type=int, choices=[0, 1, 2, 3], default=3,
+                    help="tree64 schedule (PLFX_FUSE): 3 fused six-level subtrees (f64) "
+                         "before 2's, 2 fused three-level subtrees and level pairs, "
+                         "1 level pairs only, 0 one launch per level")
     ap.add_argument("--no-fuse", action="store_true", help="same as --fuse 0")
     ap.add_argument("--tips", action="store_true",
                     help="tree64: tips as uint8 state codes (plfx.h section 8) instead of dense CLVs")
@@ -276,7 +277,10 @@ class Tree64Workload:
         leaf = tip_b if a.tips else clv_b
         fuse = 0 if a.no_fuse else a.fuse
         self.bytes_per_site = 3 * clv_b + 4
-        if fuse == 2:  # levels 0-2 as 8 seven-node subtrees, levels 3-5 as one
+        if fuse == 3 and esz == 8 and not a.tips:  # the whole tree as one six-level subtree
+            self.bytes_per_step = ((64 * leaf + 63 * clv_b + 4) + (clv_b + 4)) * n
+            sched = "fused six-level subtree: one 63-node pass"
+        elif fuse >= 2:  # levels 0-2 as 8 seven-node subtrees, levels 3-5 as one
             self.bytes_per_step = (8 * (8 * leaf + 7 * clv_b + 4) + (15 * clv_b + 4)
                                    + (clv_b + 4)) * n
             sched = "fused three-level subtrees: 9 seven-node passes in 2 launches"

@@ -235,6 +235,61 @@ def test_fused_level_pairs_match_unfused(ctx, oracle, tipmode, dtype, monkeypatc
             assert np.array_equal(r[2][j], escal[j]), j
 
 
+@pytest.mark.parametrize("tipmode", ["dense", "mixed", "coded", "left", "tipvec"])
+def test_fused_six_level_subtrees(oracle, tipmode, monkeypatch):
+    """PLFX_FUSE=3 (f64, the default): complete six-level subtrees over dense
+    leaves run as one 63-node pass (plf_dna_f64_deep_kernel).  A 128-taxon
+    balanced tree (two such passes, then the root) with a tail that reuses tips
+    and inner slots, n not a multiple of the trip; with dense tips the deep
+    passes run, with mixed / coded / left-coded tips (or a caller tipvec table)
+    the scheduler keeps the three-level passes: CLVs, scaler bytes and sums
+    bit-identical to the oracle in every case."""
+    import plfx
+    import torch
+
+    n = 1001
+    rng = np.random.default_rng(31)
+    ntax = 128
+    ops = [list(r) for r in oracle.balanced_tree_ops(ntax)]  # root = slot 2*ntax-2
+    nb = len(ops)
+    root = 2 * ntax - 2
+    ops += [[root + 1, root, 0, nb], [root + 2, root + 1, 5, nb + 1], [root + 3, root + 2, root + 1, nb + 2]]
+    ops = np.array(ops, np.int32)
+    nslots, nops = root + 4, ops.shape[0]
+    codes = [oracle.random_tip_codes(rng, n, 0.2) for _ in range(ntax)]
+    is_coded = [{"dense": False, "mixed": t % 4 != 3, "coded": True, "left": t % 2 == 0,
+                 "tipvec": t % 3 != 0}[tipmode] for t in range(ntax)]
+    tv = rng.random(64) if tipmode == "tipvec" else None
+    dense = [rng.random(16 * n) for _ in range(ntax)]
+    pm = rng.random(nops * 128) * 0.3
+    EV = rng.random(16) * 0.3
+    wgt = rng.integers(1, 5, n).astype(np.int32)
+    host = [oracle.expand_tips(codes[t], np.float64, tipvec=tv) if is_coded[t] else dense[t].copy()
+            for t in range(ntax)]
+    host += [np.zeros(16 * n) for _ in range(nslots - ntax)]
+    esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
+    assert esums.sum() > 0
+
+    monkeypatch.setenv("PLFX_FUSE", "3")
+    c = plfx.Context(0)
+    try:
+        clv = [None if is_coded[t] else dev(dense[t]) for t in range(ntax)]
+        clv += [torch.zeros(16 * n, dtype=torch.float64, device="cuda") for _ in range(nslots - ntax)]
+        tips = [dev(codes[t]) if is_coded[t] else None for t in range(ntax)] + [None] * (nslots - ntax)
+        sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
+        scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+        c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips,
+                   tipvec=None if tv is None else dev(tv))
+        torch.cuda.synchronize()
+    finally:
+        c.close()
+    for s_ in range(ntax, nslots):
+        assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
+    assert np.array_equal(sums.cpu().numpy(), esums)
+    for j in range(nops):
+        assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+
+
 def _tree_driver_expected(oracle, taxa, n, seed, alpha=0.5):
     """Re-derive plfx_tree's inputs (std::mt19937 + uniform_real_distribution,
     restated by the oracle) and its GTR+G4 lnL by an independent numpy pruning
