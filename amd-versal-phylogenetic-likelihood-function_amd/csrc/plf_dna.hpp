@@ -1251,6 +1251,122 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
   }
 }
 
+// The same six-level pass in the lane = category mapping (f32; any T): lane =
+// (site q, category c), 16 sites per wave and block of U; a lane reads its
+// category's 32 matrix values per node from the LDS copy (31.5 KB f32).
+template <typename T, bool kSum, bool NT, int U, int kThreads>
+__global__ void __launch_bounds__(kThreads, 1)
+plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
+                        const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
+  constexpr int kWaves = kThreads / 64;
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 3, qs = lane >> 2, nib = lane & 60;
+  __shared__ T mats[63 * 128];  // node i: left [c][16] | right [c][16]
+  __shared__ unsigned long long nacc[63];
+  for (int e = threadIdx.x; e < 63 * 128; e += kThreads) {
+    const int node = e >> 7, k = e & 127;
+    mats[e] = static_cast<const T *>(d.mat[2 * node + (k >> 6)])[k & 63];
+  }
+  if (threadIdx.x < 63) nacc[threadIdx.x] = 0;
+  __syncthreads();
+  T E[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) E[i] = EV[i];
+  const T m = Num<T>::minlik();
+  const int64_t wave = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWaves * 16 * U;
+  for (int64_t base = wave * 16 * U; base < n; base += stride) {
+    int z = 0;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keep the matrix reads inside the loop
+    const T *mz = mats + z;
+    bool valid[U];
+    int64_t sq[U];
+    int w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      valid[u] = base + u * 16 + qs < n;
+      sq[u] = valid[u] ? base + u * 16 + qs : n - 1;  // past n: any valid record (unused)
+      w[u] = kSum ? wgt_at(wgt, sq[u], ws) : 0;
+    }
+    auto node_eval = [&](int node, const T (&a)[U][4], const T (&b)[U][4], T (&o)[U][4]) {
+      T PL[16], PR[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        PL[j] = mz[128 * node + c * 16 + j];
+        PR[j] = mz[128 * node + 64 + c * 16 + j];
+      }
+      T *dst = static_cast<T *>(d.x[node]);
+      uint8_t *scp = d.sc[node];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        bool sc;
+        cat_node<T, false, false>(a[u], b[u], nullptr, nullptr, PL, PR, E, valid[u], nib, m, o[u], sc);
+        if (valid[u]) {
+          Num<T>::store4_nt(dst + sq[u] * 16 + c * 4, o[u]);
+          if (c == 0 && scp) scp[sq[u]] = (uint8_t)sc;
+        }
+        if (kSum) {
+          const bool mine = c == 0 && valid[u] && sc;
+          if (__ballot(mine)) {  // rare: some site of the block scaled
+            long long v = mine ? (long long)w[u] : 0ll;
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (lane == 0) atomicAdd(&nacc[node], (unsigned long long)v);
+          }
+        }
+      }
+    };
+    T s3[U][4], s4[U][4], s5[U][4];  // pending level-3/4/5 values of the carry
+#pragma unroll 1
+    for (int q = 0; q < 8; q++) {
+      T v[8][U][4];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const T *gp = static_cast<const T *>(d.g[8 * q + i]);
+#pragma unroll
+        for (int u = 0; u < U; u++) Num<T>::template load4<NT>(gp + sq[u] * 16 + c * 4, v[i][u]);
+      }
+      T a1[4][U][4], a2[2][U][4], r[U][4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i]);
+#pragma unroll
+      for (int i = 0; i < 2; i++) node_eval(32 + 2 * q + i, a1[2 * i], a1[2 * i + 1], a2[i]);
+      node_eval(48 + q, a2[0], a2[1], r);
+      auto keep = [&](T (&dst)[U][4], const T (&src)[U][4]) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+          for (int l = 0; l < 4; l++) dst[u][l] = src[u][l];
+      };
+      if (!(q & 1)) {
+        keep(s3, r);
+        continue;
+      }
+      T r4[U][4];
+      node_eval(56 + (q >> 1), s3, r, r4);
+      if (!(q & 2)) {
+        keep(s4, r4);
+        continue;
+      }
+      T r5[U][4];
+      node_eval(60 + (q >> 2), s4, r4, r5);
+      if (!(q & 4)) {
+        keep(s5, r5);
+        continue;
+      }
+      T r6[U][4];
+      node_eval(62, s5, r5, r6);
+    }
+  }
+  if constexpr (kSum) {
+    __syncthreads();
+    if (threadIdx.x < 63)
+      ticket_publish((long long)nacc[threadIdx.x], ws + (size_t)threadIdx.x * kWsWords, d.ss[threadIdx.x]);
+  }
+}
+
 // Fused three-level subtree in the lane = category mapping (f32; any T): the
 // same seven-node pass as plf_dna_f64_septet_kernel, lane = (site q, category
 // c), 16 sites per wave and block of U.  A lane needs 32 matrix values per

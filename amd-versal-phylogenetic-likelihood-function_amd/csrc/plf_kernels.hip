@@ -56,6 +56,7 @@ constexpr int kTripleU32 = 2;
 // LDS, next trip's loads in flight (tools/tune_septet.hip, r01_tune_septet.log)
 constexpr int kSeptetU = 2;
 constexpr int kSeptetU32 = 2;  // f32 (lane = category): 2 x 16-site blocks per trip
+constexpr int kDeepU32 = 2;    // f32 six-level pass: 2 x 16-site blocks per trip
 
 // Co-resident 256-thread blocks of `kernel` on the current device (cached per
 // kernel instantiation by the caller).
@@ -277,12 +278,16 @@ hipError_t launch_septets32_t(const dev::SeptetBatch &b, int count, const float 
 // fused six-level subtrees: 512-thread blocks (one LDS copy of the 63 nodes'
 // matrices per 8 waves), 2 x 8-site blocks per trip, grid = co-resident blocks
 // (tools/gpu_deep.sh, profiles/r01_deep.log)
-template <bool kSum>
-hipError_t launch_deep_t(const dev::DeepDesc &d, const double *EV, const int32_t *wgt, int64_t n,
+template <typename T, bool kSum, int U, int kThreads>
+hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt, int64_t n,
                          unsigned long long *ws, int max_blocks, hipStream_t s) {
-  constexpr int kThreads = 512, U = 2;
   static int resident = 0;
-  auto kernel = &dev::plf_dna_f64_deep_kernel<kSum, kNtl64, U, kThreads>;
+  // f64: lane pairs, 8 sites per wave instruction; f32: lane = category, 16
+  auto kernel = [] {
+    if constexpr (sizeof(T) == 8) return &dev::plf_dna_f64_deep_kernel<kSum, kNtl64, U, kThreads>;
+    else return &dev::plf_dna_cat_deep_kernel<T, kSum, kNt, U, kThreads>;
+  }();
+  constexpr int kSitesPerWave = sizeof(T) == 8 ? 8 : 16;
   if (!resident) {
     int dev = 0, per_cu = 0;
     hipDeviceProp_t prop;
@@ -294,7 +299,7 @@ hipError_t launch_deep_t(const dev::DeepDesc &d, const double *EV, const int32_t
       per_cu = 1;
     resident = per_cu * prop.multiProcessorCount;
   }
-  const int64_t per_block = (int64_t)(kThreads / 64) * 8 * U;
+  const int64_t per_block = (int64_t)(kThreads / 64) * kSitesPerWave * U;
   int64_t gx = (n + per_block - 1) / per_block;
   gx = std::max<int64_t>(1, std::min<int64_t>(gx, max_blocks > 0 ? max_blocks : resident));
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kThreads), 0, s, d, EV, wgt, n, ws);
@@ -303,14 +308,19 @@ hipError_t launch_deep_t(const dev::DeepDesc &d, const double *EV, const int32_t
 
 }  // namespace
 
-hipError_t launch_plf_dna_deep(const DeepDescH *t, const void *EV, const int32_t *wgt, int64_t n,
-                               unsigned long long *ws, int max_blocks, hipStream_t s) {
+hipError_t launch_plf_dna_deep(int dtype, const DeepDescH *t, const void *EV, const int32_t *wgt,
+                               int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s) {
   dev::DeepDesc d;
   __builtin_memcpy(&d, t, sizeof(d));
   bool any_sum = false;
   for (int q = 0; q < kDeepNodes; q++) any_sum |= t->ss[q] != nullptr;
-  return any_sum ? launch_deep_t<true>(d, (const double *)EV, wgt, n, ws, max_blocks, s)
-                 : launch_deep_t<false>(d, (const double *)EV, wgt, n, ws, max_blocks, s);
+  const double *E64 = (const double *)EV;
+  const float *E32 = (const float *)EV;
+  if (dtype == 1)
+    return any_sum ? launch_deep_t<double, true, 2, 512>(d, E64, wgt, n, ws, max_blocks, s)
+                   : launch_deep_t<double, false, 2, 512>(d, E64, wgt, n, ws, max_blocks, s);
+  return any_sum ? launch_deep_t<float, true, kDeepU32, 512>(d, E32, wgt, n, ws, max_blocks, s)
+                 : launch_deep_t<float, false, kDeepU32, 512>(d, E32, wgt, n, ws, max_blocks, s);
 }
 
 hipError_t launch_plf_dna_septets(int dtype, const SeptetDescH *t, int count, const void *EV,

@@ -90,8 +90,8 @@ hipError_t launch_plf_dna_septets(int dtype, const SeptetDescH *t, int count, co
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,
                                   int max_blocks, hipStream_t s, int tips, const void *tipvec);
 
-// Fused six-level subtree (plf_dna.hpp DeepDesc), f64, 64 dense leaves, one per
-// launch, ws >= 63 regions.
+// Fused six-level subtree (plf_dna.hpp DeepDesc), dtype 0 f32 / 1 f64, 64 dense
+// leaves, one per launch, ws >= 63 regions.
 struct DeepDescH {
   const void *g[64];
   void *x[63];
@@ -100,7 +100,7 @@ struct DeepDescH {
   int64_t *ss[63];
 };
 constexpr int kDeepNodes = 63;
-hipError_t launch_plf_dna_deep(const DeepDescH *t, const void *EV, const int32_t *wgt, int64_t n,
-                               unsigned long long *ws, int max_blocks, hipStream_t s);
+hipError_t launch_plf_dna_deep(int dtype, const DeepDescH *t, const void *EV, const int32_t *wgt,
+                               int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s);
 
 }  // namespace plfx

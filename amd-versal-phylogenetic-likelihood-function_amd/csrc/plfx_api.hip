@@ -26,7 +26,7 @@ struct plfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
-  int fuse = 3;  // traverse: 3 six-level subtrees (f64) before 2's, 2 three-level subtrees +
+  int fuse = 3;  // traverse: 3 six-level subtrees before 2's, 2 three-level subtrees +
                  // level pairs, 1 level pairs, 0 none (PLFX_FUSE)
   unsigned long long *ws = nullptr; // ticket reduction words (kMaxBatch x kWsWords u64), zero at rest
   double *lnl_partials = nullptr;   // kLnlMaxGrid doubles
@@ -559,7 +559,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
     return x >= 0 && y >= 0 && x != y && !used[x] && !used[y] && !used[p] && level[x] == L &&
            level[y] == L && level[p] == L + 1;
   };
-  // Fused six-level subtrees (DNA f64, plf_dna.hpp DeepDesc): a complete
+  // Fused six-level subtrees (DNA, plf_dna.hpp DeepDesc): a complete
   // binary subtree of 63 ops on consecutive levels L..L+5, every op's own slot
   // free by L (pdep <= L), 64 dense leaves.  Collected per level in heap
   // order (children left to right before parents): the ops of level k are
@@ -579,7 +579,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         lv[D - 1].push_back(r);
         return true;
       };
-  if (ctx->fuse >= 3 && states == 4 && dtype == PLFX_F64) {
+  if (ctx->fuse >= 3 && states == 4) {
     for (int r = 0; r < nops; r++) {
       if (level[r] < 5 || used[r]) continue;
       std::vector<int> lv[6];
@@ -658,7 +658,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
           if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
         continue;
       }
-      hipError_t e = plfx::launch_plf_dna_deep(&d, EV, wgt, n, ctx->ws, ctx->max_blocks, s);
+      hipError_t e = plfx::launch_plf_dna_deep(dtype, &d, EV, wgt, n, ctx->ws, ctx->max_blocks, s);
       if (e != hipSuccess) return hip_fail(ctx, e, "fused six-level launch");
     }
     for (const Septet &t : septets) {

@@ -99,7 +99,7 @@ def parse():
     ap.add_argument("--exact", action="store_true",
                     help="protein: plf()'s separate multiply/add (bit-identical to the double loop)")
     ap.add_argument("--fuse", type=int, choices=[0, 1, 2, 3], default=3,
-                    help="tree64 schedule (PLFX_FUSE): 3 fused six-level subtrees (f64) "
+                    help="tree64 schedule (PLFX_FUSE): 3 fused six-level subtrees (dense leaves) "
                          "before 2's, 2 fused three-level subtrees and level pairs, "
                          "1 level pairs only, 0 one launch per level")
     ap.add_argument("--no-fuse", action="store_true", help="same as --fuse 0")
@@ -277,7 +277,7 @@ class Tree64Workload:
         leaf = tip_b if a.tips else clv_b
         fuse = 0 if a.no_fuse else a.fuse
         self.bytes_per_site = 3 * clv_b + 4
-        if fuse == 3 and esz == 8 and not a.tips:  # the whole tree as one six-level subtree
+        if fuse == 3 and not a.tips:  # the whole tree as one six-level subtree
             self.bytes_per_step = ((64 * leaf + 63 * clv_b + 4) + (clv_b + 4)) * n
             sched = "fused six-level subtree: one 63-node pass"
         elif fuse >= 2:  # levels 0-2 as 8 seven-node subtrees, levels 3-5 as one

@@ -235,10 +235,12 @@ def test_fused_level_pairs_match_unfused(ctx, oracle, tipmode, dtype, monkeypatc
             assert np.array_equal(r[2][j], escal[j]), j
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("tipmode", ["dense", "mixed", "coded", "left", "tipvec"])
-def test_fused_six_level_subtrees(oracle, tipmode, monkeypatch):
-    """PLFX_FUSE=3 (f64, the default): complete six-level subtrees over dense
-    leaves run as one 63-node pass (plf_dna_f64_deep_kernel).  A 128-taxon
+def test_fused_six_level_subtrees(oracle, tipmode, dtype, monkeypatch):
+    """PLFX_FUSE=3 (the default): complete six-level subtrees over dense
+    leaves run as one 63-node pass (plf_dna_f64_deep_kernel, f32:
+    plf_dna_cat_deep_kernel).  A 128-taxon
     balanced tree (two such passes, then the root) with a tail that reuses tips
     and inner slots, n not a multiple of the trip; with dense tips the deep
     passes run, with mixed / coded / left-coded tips (or a caller tipvec table)
@@ -259,14 +261,14 @@ def test_fused_six_level_subtrees(oracle, tipmode, monkeypatch):
     codes = [oracle.random_tip_codes(rng, n, 0.2) for _ in range(ntax)]
     is_coded = [{"dense": False, "mixed": t % 4 != 3, "coded": True, "left": t % 2 == 0,
                  "tipvec": t % 3 != 0}[tipmode] for t in range(ntax)]
-    tv = rng.random(64) if tipmode == "tipvec" else None
-    dense = [rng.random(16 * n) for _ in range(ntax)]
-    pm = rng.random(nops * 128) * 0.3
-    EV = rng.random(16) * 0.3
+    tv = rng.random(64).astype(dtype) if tipmode == "tipvec" else None
+    dense = [rng.random(16 * n).astype(dtype) for _ in range(ntax)]
+    pm = (rng.random(nops * 128) * 0.3).astype(dtype)
+    EV = (rng.random(16) * 0.3).astype(dtype)
     wgt = rng.integers(1, 5, n).astype(np.int32)
-    host = [oracle.expand_tips(codes[t], np.float64, tipvec=tv) if is_coded[t] else dense[t].copy()
+    host = [oracle.expand_tips(codes[t], dtype, tipvec=tv) if is_coded[t] else dense[t].copy()
             for t in range(ntax)]
-    host += [np.zeros(16 * n) for _ in range(nslots - ntax)]
+    host += [np.zeros(16 * n, dtype) for _ in range(nslots - ntax)]
     esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
     assert esums.sum() > 0
 
@@ -274,7 +276,8 @@ def test_fused_six_level_subtrees(oracle, tipmode, monkeypatch):
     c = plfx.Context(0)
     try:
         clv = [None if is_coded[t] else dev(dense[t]) for t in range(ntax)]
-        clv += [torch.zeros(16 * n, dtype=torch.float64, device="cuda") for _ in range(nslots - ntax)]
+        tt = torch.float64 if dtype == np.float64 else torch.float32
+        clv += [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nslots - ntax)]
         tips = [dev(codes[t]) if is_coded[t] else None for t in range(ntax)] + [None] * (nslots - ntax)
         sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
         scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
