@@ -233,8 +233,9 @@ int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const
  * not read) and may not be an op's parent (codes and tipvec as above for the
  * states).  Each level is
  * issued as up to three batched launches (tip/tip, tip/inner, inner/inner),
- * three-level subtrees and level pairs fused where possible
- * (bit-identical results; env PLFX_FUSE=1 pairs only, 0 none).  states 4 or 20; flags as
+ * six-level subtrees over dense leaves, three-level subtrees and level pairs
+ * fused where possible (bit-identical results; env PLFX_FUSE=2 no six-level
+ * passes, 1 pairs only, 0 none).  states 4 or 20; flags as
  * plfx_plf_dev_gen (PLFX_FMA: protein nodes on the f64 matrix cores; DNA is
  * always exact).  plfx_traverse == flags PLFX_EXACT, no tips, no tipvec. */
 int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const plfx_trav_op *ops,
