@@ -1116,9 +1116,9 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
   if constexpr (kSum) block_ticket_sum7(acc, ws + (size_t)blockIdx.y * 7 * kWsWords, d.ss);
 }
 
-// Fused six-level subtree ("deep", f64 lane-pair mapping): the 63 ops of a
-// complete binary subtree over 64 dense leaves in one pass -- 64 leaf reads +
-// 63 writes per site (2.02 CLV transfers per node; three-level passes move
+// Fused six-level subtree ("deep", f64 lane-pair mapping; built for depth D =
+// 4, 5, 6 -- the numbers below are D = 6): the 63 ops of a complete binary
+// subtree over 64 dense leaves in one pass -- 64 leaf reads + 63 writes per site (2.02 CLV transfers per node; three-level passes move
 // 2.14, and a 64-taxon tree as nine of them reads the eight level-3 CLVs
 // back).  Node numbering is heap order by level: level 1 = 0..31 (node i over
 // leaves 2i, 2i+1), level 2 = 32..47, level 3 = 48..55, level 4 = 56..59,
@@ -1135,6 +1135,15 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
 // profiles/r01_deep.log: 256/512/768-thread blocks, U = 1/2, next-group
 // prefetch; coded leaves expanded in registers ran 20-40 % slower than the
 // three-level passes' tip tables, so the scheduler keeps tips there.)
+// Heap-order level offsets of a complete subtree of depth D (level 1 first):
+// node numbers off(l) .. off(l) + 2^(D-1-l) - 1 hold level l+1.
+template <int D>
+__device__ constexpr int deep_off(int l) {
+  int o = 0;
+  for (int i = 0; i < l; i++) o += 1 << (D - 1 - i);
+  return o;
+}
+
 struct DeepDesc {
   const void *g[64];
   void *x[63];
@@ -1143,20 +1152,21 @@ struct DeepDesc {
   int64_t *ss[63];
 };
 
-template <bool kSum, bool NTL, int U, int kThreads>
+template <int D, bool kSum, bool NTL, int U, int kThreads>
 __global__ void __launch_bounds__(kThreads, 1)
 plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
                         const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
-  constexpr int kWaves = kThreads / 64;
+  static_assert(D >= 4 && D <= 6, "depth 4..6");
+  constexpr int kWaves = kThreads / 64, kNodes = (1 << D) - 1, kGroups = 1 << (D - 3);
   const int lane = threadIdx.x & 63;
   const int h = lane & 1, c = (lane >> 1) & 3, g = lane >> 3, sh = lane & 56;
-  __shared__ double mats[63][128];
-  __shared__ unsigned long long nacc[63];
-  for (int e = threadIdx.x; e < 63 * 128; e += kThreads) {
+  __shared__ double mats[kNodes][128];
+  __shared__ unsigned long long nacc[kNodes];
+  for (int e = threadIdx.x; e < kNodes * 128; e += kThreads) {
     const int node = e >> 7, k = e & 127;
     mats[node][k] = static_cast<const double *>(d.mat[2 * node + (k >> 6)])[k & 63];
   }
-  if (threadIdx.x < 63) nacc[threadIdx.x] = 0;
+  if (threadIdx.x < kNodes) nacc[threadIdx.x] = 0;
   __syncthreads();
   double E[4][2];
 #pragma unroll
@@ -1207,7 +1217,7 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
     };
     f64x2 s3[U], s4[U], s5[U];  // pending level-3/4/5 values of the carry
 #pragma unroll 1
-    for (int q = 0; q < 8; q++) {
+    for (int q = 0; q < kGroups; q++) {
       f64x2 v[8][U];
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -1219,34 +1229,27 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
 #pragma unroll
       for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i]);
 #pragma unroll
-      for (int i = 0; i < 2; i++) node_eval(32 + 2 * q + i, a1[2 * i], a1[2 * i + 1], a2[i]);
-      node_eval(48 + q, a2[0], a2[1], r);
-      if (!(q & 1)) {
+      for (int i = 0; i < 2; i++) node_eval(deep_off<D>(1) + 2 * q + i, a1[2 * i], a1[2 * i + 1], a2[i]);
+      node_eval(deep_off<D>(2) + q, a2[0], a2[1], r);
+      // levels 4..D: a binary carry over the groups, one pending value per level
 #pragma unroll
-        for (int j = 0; j < U; j++) s3[j] = r[j];
-        continue;
-      }
-      f64x2 r4[U];
-      node_eval(56 + (q >> 1), s3, r, r4);
-      if (!(q & 2)) {
+      for (int l = 3; l < D; l++) {
+        f64x2 (&pend)[U] = l == 3 ? s3 : (l == 4 ? s4 : s5);
+        if (!((q >> (l - 3)) & 1)) {
 #pragma unroll
-        for (int j = 0; j < U; j++) s4[j] = r4[j];
-        continue;
-      }
-      f64x2 r5[U];
-      node_eval(60 + (q >> 2), s4, r4, r5);
-      if (!(q & 4)) {
+          for (int j = 0; j < U; j++) pend[j] = r[j];
+          break;
+        }
+        f64x2 up[U];
+        node_eval(deep_off<D>(l) + (q >> (l - 2)), pend, r, up);
 #pragma unroll
-        for (int j = 0; j < U; j++) s5[j] = r5[j];
-        continue;
+        for (int j = 0; j < U; j++) r[j] = up[j];
       }
-      f64x2 r6[U];
-      node_eval(62, s5, r5, r6);
     }
   }
   if constexpr (kSum) {
     __syncthreads();
-    if (threadIdx.x < 63)
+    if (threadIdx.x < kNodes)
       ticket_publish((long long)nacc[threadIdx.x], ws + (size_t)threadIdx.x * kWsWords, d.ss[threadIdx.x]);
   }
 }
@@ -1254,20 +1257,21 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
 // The same six-level pass in the lane = category mapping (f32; any T): lane =
 // (site q, category c), 16 sites per wave and block of U; a lane reads its
 // category's 32 matrix values per node from the LDS copy (31.5 KB f32).
-template <typename T, bool kSum, bool NT, int U, int kThreads>
+template <int D, typename T, bool kSum, bool NT, int U, int kThreads>
 __global__ void __launch_bounds__(kThreads, 1)
 plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
                         const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
-  constexpr int kWaves = kThreads / 64;
+  static_assert(D >= 4 && D <= 6, "depth 4..6");
+  constexpr int kWaves = kThreads / 64, kNodes = (1 << D) - 1, kGroups = 1 << (D - 3);
   const int lane = threadIdx.x & 63;
   const int c = lane & 3, qs = lane >> 2, nib = lane & 60;
-  __shared__ T mats[63 * 128];  // node i: left [c][16] | right [c][16]
-  __shared__ unsigned long long nacc[63];
-  for (int e = threadIdx.x; e < 63 * 128; e += kThreads) {
+  __shared__ T mats[kNodes * 128];  // node i: left [c][16] | right [c][16]
+  __shared__ unsigned long long nacc[kNodes];
+  for (int e = threadIdx.x; e < kNodes * 128; e += kThreads) {
     const int node = e >> 7, k = e & 127;
     mats[e] = static_cast<const T *>(d.mat[2 * node + (k >> 6)])[k & 63];
   }
-  if (threadIdx.x < 63) nacc[threadIdx.x] = 0;
+  if (threadIdx.x < kNodes) nacc[threadIdx.x] = 0;
   __syncthreads();
   T E[16];
 #pragma unroll
@@ -1320,7 +1324,7 @@ plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
     };
     T s3[U][4], s4[U][4], s5[U][4];  // pending level-3/4/5 values of the carry
 #pragma unroll 1
-    for (int q = 0; q < 8; q++) {
+    for (int q = 0; q < kGroups; q++) {
       T v[8][U][4];
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -1332,37 +1336,31 @@ plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
 #pragma unroll
       for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i]);
 #pragma unroll
-      for (int i = 0; i < 2; i++) node_eval(32 + 2 * q + i, a1[2 * i], a1[2 * i + 1], a2[i]);
-      node_eval(48 + q, a2[0], a2[1], r);
+      for (int i = 0; i < 2; i++) node_eval(deep_off<D>(1) + 2 * q + i, a1[2 * i], a1[2 * i + 1], a2[i]);
+      node_eval(deep_off<D>(2) + q, a2[0], a2[1], r);
       auto keep = [&](T (&dst)[U][4], const T (&src)[U][4]) {
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
           for (int l = 0; l < 4; l++) dst[u][l] = src[u][l];
       };
-      if (!(q & 1)) {
-        keep(s3, r);
-        continue;
+      // levels 4..D: a binary carry over the groups, one pending value per level
+#pragma unroll
+      for (int l = 3; l < D; l++) {
+        T (&pend)[U][4] = l == 3 ? s3 : (l == 4 ? s4 : s5);
+        if (!((q >> (l - 3)) & 1)) {
+          keep(pend, r);
+          break;
+        }
+        T up[U][4];
+        node_eval(deep_off<D>(l) + (q >> (l - 2)), pend, r, up);
+        keep(r, up);
       }
-      T r4[U][4];
-      node_eval(56 + (q >> 1), s3, r, r4);
-      if (!(q & 2)) {
-        keep(s4, r4);
-        continue;
-      }
-      T r5[U][4];
-      node_eval(60 + (q >> 2), s4, r4, r5);
-      if (!(q & 4)) {
-        keep(s5, r5);
-        continue;
-      }
-      T r6[U][4];
-      node_eval(62, s5, r5, r6);
     }
   }
   if constexpr (kSum) {
     __syncthreads();
-    if (threadIdx.x < 63)
+    if (threadIdx.x < kNodes)
       ticket_publish((long long)nacc[threadIdx.x], ws + (size_t)threadIdx.x * kWsWords, d.ss[threadIdx.x]);
   }
 }

@@ -278,14 +278,14 @@ hipError_t launch_septets32_t(const dev::SeptetBatch &b, int count, const float 
 // fused six-level subtrees: 512-thread blocks (one LDS copy of the 63 nodes'
 // matrices per 8 waves), 2 x 8-site blocks per trip, grid = co-resident blocks
 // (tools/gpu_deep.sh, profiles/r01_deep.log)
-template <typename T, bool kSum, int U, int kThreads>
+template <int D, typename T, bool kSum, int U, int kThreads>
 hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt, int64_t n,
                          unsigned long long *ws, int max_blocks, hipStream_t s) {
   static int resident = 0;
   // f64: lane pairs, 8 sites per wave instruction; f32: lane = category, 16
   auto kernel = [] {
-    if constexpr (sizeof(T) == 8) return &dev::plf_dna_f64_deep_kernel<kSum, kNtl64, U, kThreads>;
-    else return &dev::plf_dna_cat_deep_kernel<T, kSum, kNt, U, kThreads>;
+    if constexpr (sizeof(T) == 8) return &dev::plf_dna_f64_deep_kernel<D, kSum, kNtl64, U, kThreads>;
+    else return &dev::plf_dna_cat_deep_kernel<D, T, kSum, kNt, U, kThreads>;
   }();
   constexpr int kSitesPerWave = sizeof(T) == 8 ? 8 : 16;
   if (!resident) {
@@ -308,19 +308,32 @@ hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt
 
 }  // namespace
 
-hipError_t launch_plf_dna_deep(int dtype, const DeepDescH *t, const void *EV, const int32_t *wgt,
-                               int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s) {
-  dev::DeepDesc d;
-  __builtin_memcpy(&d, t, sizeof(d));
-  bool any_sum = false;
-  for (int q = 0; q < kDeepNodes; q++) any_sum |= t->ss[q] != nullptr;
+template <int D>
+hipError_t launch_deep_d(int dtype, bool any_sum, const dev::DeepDesc &d, const void *EV,
+                         const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                         hipStream_t s) {
   const double *E64 = (const double *)EV;
   const float *E32 = (const float *)EV;
   if (dtype == 1)
-    return any_sum ? launch_deep_t<double, true, 2, 512>(d, E64, wgt, n, ws, max_blocks, s)
-                   : launch_deep_t<double, false, 2, 512>(d, E64, wgt, n, ws, max_blocks, s);
-  return any_sum ? launch_deep_t<float, true, kDeepU32, 512>(d, E32, wgt, n, ws, max_blocks, s)
-                 : launch_deep_t<float, false, kDeepU32, 512>(d, E32, wgt, n, ws, max_blocks, s);
+    return any_sum ? launch_deep_t<D, double, true, 2, 512>(d, E64, wgt, n, ws, max_blocks, s)
+                   : launch_deep_t<D, double, false, 2, 512>(d, E64, wgt, n, ws, max_blocks, s);
+  return any_sum ? launch_deep_t<D, float, true, kDeepU32, 512>(d, E32, wgt, n, ws, max_blocks, s)
+                 : launch_deep_t<D, float, false, kDeepU32, 512>(d, E32, wgt, n, ws, max_blocks, s);
+}
+
+hipError_t launch_plf_dna_deep(int dtype, int depth, const DeepDescH *t, const void *EV,
+                               const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                               hipStream_t s) {
+  if (depth < 4 || depth > 6) return hipErrorInvalidValue;
+  dev::DeepDesc d;
+  __builtin_memcpy(&d, t, sizeof(d));
+  bool any_sum = false;
+  for (int q = 0; q < (1 << depth) - 1; q++) any_sum |= t->ss[q] != nullptr;
+  switch (depth) {
+    case 4: return launch_deep_d<4>(dtype, any_sum, d, EV, wgt, n, ws, max_blocks, s);
+    case 5: return launch_deep_d<5>(dtype, any_sum, d, EV, wgt, n, ws, max_blocks, s);
+    default: return launch_deep_d<6>(dtype, any_sum, d, EV, wgt, n, ws, max_blocks, s);
+  }
 }
 
 hipError_t launch_plf_dna_septets(int dtype, const SeptetDescH *t, int count, const void *EV,

@@ -90,8 +90,9 @@ hipError_t launch_plf_dna_septets(int dtype, const SeptetDescH *t, int count, co
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,
                                   int max_blocks, hipStream_t s, int tips, const void *tipvec);
 
-// Fused six-level subtree (plf_dna.hpp DeepDesc), dtype 0 f32 / 1 f64, 64 dense
-// leaves, one per launch, ws >= 63 regions.
+// Fused complete subtree of depth 4..6 (plf_dna.hpp DeepDesc: 2^depth dense
+// leaves, 2^depth - 1 nodes in heap order by level), dtype 0 f32 / 1 f64, one
+// per launch, ws >= 2^depth - 1 regions.
 struct DeepDescH {
   const void *g[64];
   void *x[63];
@@ -100,7 +101,8 @@ struct DeepDescH {
   int64_t *ss[63];
 };
 constexpr int kDeepNodes = 63;
-hipError_t launch_plf_dna_deep(int dtype, const DeepDescH *t, const void *EV, const int32_t *wgt,
-                               int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s);
+hipError_t launch_plf_dna_deep(int dtype, int depth, const DeepDescH *t, const void *EV,
+                               const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                               hipStream_t s);
 
 }  // namespace plfx

@@ -559,15 +559,15 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
     return x >= 0 && y >= 0 && x != y && !used[x] && !used[y] && !used[p] && level[x] == L &&
            level[y] == L && level[p] == L + 1;
   };
-  // Fused six-level subtrees (DNA, plf_dna.hpp DeepDesc): a complete
-  // binary subtree of 63 ops on consecutive levels L..L+5, every op's own slot
-  // free by L (pdep <= L), 64 dense leaves.  Collected per level in heap
+  // Fused deep subtrees (DNA, plf_dna.hpp DeepDesc): a complete binary
+  // subtree of depth D = 6, 5 or 4 (2^D - 1 ops on consecutive levels
+  // L..L+D-1), every op's own slot free by L (pdep <= L), dense leaves.  Collected per level in heap
   // order (children left to right before parents): the ops of level k are
   // lv[k], and lv[k][i]'s children were written by lv[k-1][2i], lv[k-1][2i+1].
   // Tried before the three-level subtrees.
   struct Deep {
-    std::vector<int> ops;  // the 63 ops in DeepDesc node order
-    int L;
+    std::vector<int> ops;  // the 2^D - 1 ops in DeepDesc node order
+    int L, D;
   };
   std::vector<Deep> deeps;
   std::function<bool(int, int, int, std::vector<int> *)> complete =
@@ -580,17 +580,19 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         return true;
       };
   if (ctx->fuse >= 3 && states == 4) {
-    for (int r = 0; r < nops; r++) {
-      if (level[r] < 5 || used[r]) continue;
-      std::vector<int> lv[6];
-      if (!complete(r, 6, level[r] - 5, lv)) continue;
-      bool dense = true;  // coded leaves stay with the three-level passes' tip tables
-      for (int j : lv[0]) dense = dense && !is_tip(ops[j].child1) && !is_tip(ops[j].child2);
-      if (!dense) continue;
-      Deep t{{}, level[r] - 5};
-      for (auto &v : lv) t.ops.insert(t.ops.end(), v.begin(), v.end());
-      for (int j : t.ops) used[j] = 1;
-      deeps.push_back(std::move(t));
+    for (int D = 6; D >= 4; D--) {  // deepest first
+      for (int r = 0; r < nops; r++) {
+        if (level[r] < D - 1 || used[r]) continue;
+        std::vector<int> lv[6];
+        if (!complete(r, D, level[r] - (D - 1), lv)) continue;
+        bool dense = true;  // coded leaves stay with the three-level passes' tip tables
+        for (int j : lv[0]) dense = dense && !is_tip(ops[j].child1) && !is_tip(ops[j].child2);
+        if (!dense) continue;
+        Deep t{{}, level[r] - (D - 1), D};
+        for (int k = 0; k < D; k++) t.ops.insert(t.ops.end(), lv[k].begin(), lv[k].end());
+        for (int j : t.ops) used[j] = 1;
+        deeps.push_back(std::move(t));
+      }
     }
   }
   if (ctx->fuse >= 2 && states == 4) {
@@ -637,13 +639,14 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
     for (const Deep &t : deeps) {
       if (t.L != lv) continue;
       plfx::DeepDescH d{};
-      for (int q = 0; q < plfx::kDeepNodes; q++) {
+      const int nodes = (1 << t.D) - 1, leaf_ops = 1 << (t.D - 1);
+      for (int q = 0; q < nodes; q++) {
         const int j = t.ops[q];
         const plfx_trav_op &o = ops[j];
         int kq;
         const int rc = check_node(ctx, node_of(j, &kq), kq, n, j);
         if (rc != PLFX_OK) return rc;
-        if (q < 32) {  // level 1: the (dense) leaves, child1 then child2
+        if (q < leaf_ops) {  // level 1: the (dense) leaves, child1 then child2
           d.g[2 * q] = clv[o.child1];
           d.g[2 * q + 1] = clv[o.child2];
         }
@@ -658,8 +661,8 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
           if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
         continue;
       }
-      hipError_t e = plfx::launch_plf_dna_deep(dtype, &d, EV, wgt, n, ctx->ws, ctx->max_blocks, s);
-      if (e != hipSuccess) return hip_fail(ctx, e, "fused six-level launch");
+      hipError_t e = plfx::launch_plf_dna_deep(dtype, t.D, &d, EV, wgt, n, ctx->ws, ctx->max_blocks, s);
+      if (e != hipSuccess) return hip_fail(ctx, e, "fused deep-subtree launch");
     }
     for (const Septet &t : septets) {
       if (level[t.a[0]] != lv) continue;

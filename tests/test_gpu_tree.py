@@ -293,6 +293,74 @@ def test_fused_six_level_subtrees(oracle, tipmode, dtype, monkeypatch):
         assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
 
 
+def _balanced_ops(tips, slot, pmat):
+    """Level-order ops of a balanced subtree over `tips` (a power of two)."""
+    ops, level = [], list(tips)
+    while len(level) > 1:
+        nxt = []
+        for i in range(0, len(level), 2):
+            ops.append([slot, level[i], level[i + 1], pmat])
+            nxt.append(slot)
+            slot, pmat = slot + 1, pmat + 1
+        level = nxt
+    return ops, level[0], slot, pmat
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("tipmode", ["dense", "half"])
+def test_fused_depth4_depth5_subtrees(oracle, tipmode, dtype, monkeypatch):
+    """The deep pass at depth 5 and 4 (31 and 15 ops): a 53-taxon tree made
+    of a balanced 16-taxon subtree, a balanced 32-taxon subtree and a
+    caterpillar over the rest.  Dense tips: both subtrees run as one deep pass
+    each; "half": the first 16 tips of the 32-taxon subtree are coded, so it
+    falls back to a depth-4 deep pass over its dense half plus three-level
+    passes.  CLVs, scaler bytes and sums bit-identical to the oracle."""
+    import plfx
+    import torch
+
+    n = 777
+    rng = np.random.default_rng(45)
+    ntax = 53
+    ops_a, ra, slot, pmat = _balanced_ops(range(0, 16), ntax, 0)
+    ops_b, rb, slot, pmat = _balanced_ops(range(16, 48), slot, pmat)
+    ops = ops_a + ops_b + [[slot, ra, rb, pmat]]
+    slot, pmat = slot + 1, pmat + 1
+    for t in range(48, ntax):
+        ops.append([slot, slot - 1, t, pmat])
+        slot, pmat = slot + 1, pmat + 1
+    ops = np.array(ops, np.int32)
+    nslots, nops = slot, ops.shape[0]
+    codes = [oracle.random_tip_codes(rng, n, 0.2) for _ in range(ntax)]
+    is_coded = [tipmode == "half" and 16 <= t < 32 for t in range(ntax)]
+    dense = [rng.random(16 * n).astype(dtype) for _ in range(ntax)]
+    pm = (rng.random(nops * 128) * 0.3).astype(dtype)
+    EV = (rng.random(16) * 0.3).astype(dtype)
+    wgt = rng.integers(1, 5, n).astype(np.int32)
+    host = [oracle.expand_tips(codes[t], dtype) if is_coded[t] else dense[t].copy() for t in range(ntax)]
+    host += [np.zeros(16 * n, dtype) for _ in range(nslots - ntax)]
+    esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
+    assert esums.sum() > 0
+
+    monkeypatch.setenv("PLFX_FUSE", "3")
+    c = plfx.Context(0)
+    try:
+        tt = torch.float64 if dtype == np.float64 else torch.float32
+        clv = [None if is_coded[t] else dev(dense[t]) for t in range(ntax)]
+        clv += [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nslots - ntax)]
+        tips = [dev(codes[t]) if is_coded[t] else None for t in range(ntax)] + [None] * (nslots - ntax)
+        sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
+        scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+        c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips)
+        torch.cuda.synchronize()
+    finally:
+        c.close()
+    for s_ in range(ntax, nslots):
+        assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
+    assert np.array_equal(sums.cpu().numpy(), esums)
+    for j in range(nops):
+        assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+
+
 def _tree_driver_expected(oracle, taxa, n, seed, alpha=0.5):
     """Re-derive plfx_tree's inputs (std::mt19937 + uniform_real_distribution,
     restated by the oracle) and its GTR+G4 lnL by an independent numpy pruning
