@@ -587,6 +587,12 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         if (!complete(r, D, level[r] - (D - 1), lv)) continue;
         bool dense = true;  // coded leaves stay with the three-level passes' tip tables
         for (int j : lv[0]) dense = dense && !is_tip(ops[j].child1) && !is_tip(ops[j].child2);
+        // nor may a deep pass take the top of a subtree whose lower levels are
+        // still unfused (over coded leaves: the septets below it would become
+        // level pairs and move more bytes in all)
+        for (int j : lv[0])
+          for (int wr : {w1[j], w2[j]})
+            if (wr >= 0 && !used[wr] && level[wr] == level[r] - D) dense = false;
         if (!dense) continue;
         Deep t{{}, level[r] - (D - 1), D};
         for (int k = 0; k < D; k++) t.ops.insert(t.ops.end(), lv[k].begin(), lv[k].end());
