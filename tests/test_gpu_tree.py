@@ -293,6 +293,44 @@ def test_fused_six_level_subtrees(oracle, tipmode, dtype, monkeypatch):
         assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("n", [1, 7, 17, 33])
+def test_six_level_pass_tiny_alignments(oracle, n, dtype, monkeypatch):
+    """The 63-node pass on alignments shorter than one trip (one wave
+    active, partial 8/16-site blocks): a 64-taxon balanced dense tree equals
+    the oracle bit for bit, sums included."""
+    import plfx
+    import torch
+
+    rng = np.random.default_rng(100 + n)
+    ntax = 64
+    ops = np.array(oracle.balanced_tree_ops(ntax), np.int32)
+    nslots, nops = 2 * ntax - 1, ops.shape[0]
+    dense = [rng.random(16 * n).astype(dtype) for _ in range(ntax)]
+    dense[0][::3] *= 1e-30 if dtype == np.float64 else 1e-20  # some sites scale
+    pm = (rng.random(nops * 128) * 0.3).astype(dtype)
+    EV = (rng.random(16) * 0.3).astype(dtype)
+    wgt = rng.integers(1, 5, n).astype(np.int32)
+    host = [d.copy() for d in dense] + [np.zeros(16 * n, dtype) for _ in range(nslots - ntax)]
+    esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
+    monkeypatch.setenv("PLFX_FUSE", "3")
+    c = plfx.Context(0)
+    try:
+        tt = torch.float64 if dtype == np.float64 else torch.float32
+        clv = [dev(d) for d in dense] + [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nslots - ntax)]
+        sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
+        scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+        c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums)
+        torch.cuda.synchronize()
+    finally:
+        c.close()
+    for s_ in range(ntax, nslots):
+        assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
+    assert np.array_equal(sums.cpu().numpy(), esums)
+    for j in range(nops):
+        assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+
+
 def _balanced_ops(tips, slot, pmat):
     """Level-order ops of a balanced subtree over `tips` (a power of two)."""
     ops, level = [], list(tips)
