@@ -30,7 +30,7 @@ step prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/prof_fetch -o run --ou
 step prof_write 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/prof_write -o run --output-format csv -- python3 $R/bench.py --steps 40 --warmup 4 --no-cpu-baseline --launch bound
 find $OUT/prof_trace $OUT/prof_fetch $OUT/prof_write -name "*.csv" | head -20
 python3 $R/tools/pmc_traffic.py $OUT/prof_fetch/run_counter_collection.csv $OUT/prof_write/run_counter_collection.csv $OUT/pmc_traffic.json > /dev/null && echo traffic ok
-# tree64 (configs[2], fused three-level subtrees): kernel trace and the two PMC passes
+# tree64 (configs[2], one fused six-level pass): kernel trace and the two PMC passes
 TREE="$R/bench.py --workload tree64 --no-cpu-baseline"
 step tree_bench 300 python $TREE --steps 50 --warmup 5
 tail -1 $OUT/tree_bench.log
