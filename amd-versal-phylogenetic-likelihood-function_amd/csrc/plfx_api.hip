@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
+#include <deque>
 #include <new>
 #include <string>
 #include <functional>
@@ -22,15 +23,27 @@
 
 constexpr int kHostChunksMax = 16;
 
+// Scaler-sum / lnL reduction workspace of one stream (plf_dna.hpp
+// block_ticket_sum, plf_lnl.hpp): zero at rest, restored to zero by the last
+// arriving block of every launch.  One per stream, so sum-producing launches
+// on different streams of one context may overlap (plfx.h, "Streams and the
+// scaler-sum workspace").
+struct StreamWs {
+  hipStream_t stream = nullptr;
+  unsigned long long *ws = nullptr;  // kWsRegions x kWsWords u64
+  double *lnl_partials = nullptr;    // kLnlMaxGrid doubles
+  unsigned long long *lnl_ticket = nullptr;
+  void *block = nullptr;             // the one allocation holding all three
+};
+
 struct plfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
   int fuse = 3;  // traverse: 3 six-level subtrees before 2's, 2 three-level subtrees +
                  // level pairs, 1 level pairs, 0 none (PLFX_FUSE)
-  unsigned long long *ws = nullptr; // ticket reduction words (kMaxBatch x kWsWords u64), zero at rest
-  double *lnl_partials = nullptr;   // kLnlMaxGrid doubles
-  unsigned long long *lnl_ticket = nullptr;
+  std::deque<StreamWs> wss;         // per-stream workspaces (stable addresses)
+  int sched[PLFX_SCHED_COUNTS] = {};  // schedule of the last traverse
   // grow-only staging for the synchronous host entry points
   void *d_buf = nullptr;
   size_t d_cap = 0;
@@ -41,6 +54,32 @@ struct plfx_ctx {
 };
 
 namespace {
+
+// Every entry point runs with the context's device current and gives the
+// caller's current device back (hipSetDevice is per host thread).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+    else prev = -1;  // nothing to restore
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard &) = delete;
+  DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
+#define PLFX_BIND(ctx)                 \
+  if (!(ctx)) return PLFX_ERR_INVALID; \
+  DeviceGuard plfx_guard_((ctx)->device)
+
+constexpr size_t kWsRegions = std::max({(size_t)plfx::kMaxBatch, (size_t)7 * plfx::kMaxSeptets,
+                                        (size_t)plfx::kDeepNodes});
+constexpr size_t kWsBytes = kWsRegions * plfx::kWsWords * sizeof(unsigned long long);
+constexpr size_t kLnlPartialBytes = plfx::kLnlMaxGrid * sizeof(double);
+constexpr size_t kLnlTicketBytes = plfx::kWsWords * sizeof(unsigned long long);
 
 int fail(plfx_ctx *ctx, int code, const char *fmt, ...) {
   if (ctx) {
@@ -70,6 +109,55 @@ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // to run on the context's own stream.
 hipStream_t pick(plfx_ctx *, void *stream) { return reinterpret_cast<hipStream_t>(stream); }
 
+// The workspace of stream s, created (zeroed in order on s) on its first use.
+// Not inside a stream capture: the allocation would not be part of the graph.
+StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
+  for (StreamWs &w : ctx->wss)
+    if (w.stream == s) return &w;
+  *rc = PLFX_OK;
+  if ((int)ctx->wss.size() >= PLFX_MAX_STREAMS) {
+    *rc = fail(ctx, PLFX_ERR_INVALID, "more than %d streams used with one context", PLFX_MAX_STREAMS);
+    return nullptr;
+  }
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (s && hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
+    *rc = fail(ctx, PLFX_ERR_INVALID,
+               "first call on a stream inside a graph capture: issue one call on the stream "
+               "before capturing (its reduction workspace is allocated then)");
+    return nullptr;
+  }
+  StreamWs w;
+  w.stream = s;
+  const size_t bytes = kWsBytes + kLnlPartialBytes + kLnlTicketBytes;
+  hipError_t e = hipMalloc(&w.block, bytes);
+  if (e != hipSuccess) {
+    *rc = fail(ctx, PLFX_ERR_NOMEM, "workspace hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    return nullptr;
+  }
+  char *b = static_cast<char *>(w.block);
+  w.ws = reinterpret_cast<unsigned long long *>(b);
+  w.lnl_partials = reinterpret_cast<double *>(b + kWsBytes);
+  w.lnl_ticket = reinterpret_cast<unsigned long long *>(b + kWsBytes + kLnlPartialBytes);
+  e = hipMemsetAsync(w.block, 0, bytes, s);
+  if (e == hipSuccess && !s) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    (void)hipFree(w.block);
+    *rc = hip_fail(ctx, e, "workspace memset");
+    return nullptr;
+  }
+  ctx->wss.push_back(w);
+  return &ctx->wss.back();
+}
+
+// the workspace of stream s as `out`; returns from the caller on failure
+#define PLFX_WS(ctx, s, out)                      \
+  StreamWs *out = nullptr;                        \
+  do {                                            \
+    int wrc_ = PLFX_OK;                           \
+    out = ws_for((ctx), (s), &wrc_);              \
+    if (!out) return wrc_;                        \
+  } while (0)
+
 int check_dev_args(plfx_ctx *ctx, const void *x1, const void *x2, const void *x3, const void *EV,
                    int64_t n, const void *left, const void *right) {
   if (!ctx) return PLFX_ERR_INVALID;
@@ -94,7 +182,8 @@ int plf_dev(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int64_t
     if (scaler_sum) PLFX_HIP(ctx, hipMemsetAsync(scaler_sum, 0, sizeof(int64_t), s));
     return PLFX_OK;
   }
-  plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, ctx->ws, n};
+  PLFX_WS(ctx, s, w);
+  plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, w->ws, n};
   hipError_t e = sizeof(T) == 4 ? plfx::launch_plf_dna_f32(a, ctx->max_blocks, s)
                                 : plfx::launch_plf_dna_f64(a, ctx->max_blocks, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "plf_dna launch");
@@ -130,6 +219,11 @@ int plf_host(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int n,
   if (n < 0) return fail(ctx, PLFX_ERR_INVALID, "n < 0 (%d)", n);
   if (n > 0 && (!x1 || !x2 || !x3 || !EV || !left || !right))
     return fail(ctx, PLFX_ERR_INVALID, "null argument");
+  if (wgt && n >= 512) {  // the reduction's bound (plfx.h): sum |wgt| < 2^40
+    int64_t tot = 0;
+    for (int i = 0; i < n; i++) tot += wgt[i] < 0 ? -(int64_t)wgt[i] : (int64_t)wgt[i];
+    if (tot >= (int64_t(1) << 40)) return fail(ctx, PLFX_ERR_INVALID, "sum |wgt| >= 2^40");
+  }
   constexpr int64_t kMinChunk = 1 << 17;  // sites; smaller chunks pay per-copy overheads
   const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(kHostChunksMax, n / kMinChunk));
   const int64_t chunk = ((int64_t)n + nch - 1) / nch;
@@ -201,9 +295,11 @@ int check_node(plfx_ctx *ctx, const plfx_node &d, int tips, int64_t n, int i) {
 
 // Nodes of one kind (tips = number of tip children, tip child first) in
 // launches of kMaxBatch.  A tip child is a uint8 code array (no alignment rule).
+// *launches counts the kernel launches issued (may be NULL).
 int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, const void *EV,
                int64_t n, const int32_t *wgt, hipStream_t s, int tips,
-               const void *tipvec = nullptr, int states = 4, int flags = PLFX_EXACT) {
+               const void *tipvec = nullptr, int states = 4, int flags = PLFX_EXACT,
+               int *launches = nullptr) {
   if (count < 0 || n < 0 || (count > 0 && (!nodes || !EV)))
     return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
   for (int i = 0; i < count; i++) {
@@ -212,23 +308,26 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
     if (rc != PLFX_OK) return rc;
     if (n == 0 && d.scaler_sum) PLFX_HIP(ctx, hipMemsetAsync(d.scaler_sum, 0, sizeof(int64_t), s));
   }
-  if (n == 0) return PLFX_OK;
+  if (n == 0 || count == 0) return PLFX_OK;
+  PLFX_WS(ctx, s, w);
   if (states == 20) {  // protein: one full-GPU launch per node (plf_prot.hpp)
     for (int i = 0; i < count; i++) {
       const plfx_node &d = nodes[i];
-      plfx::DnaArgs a{d.x1, d.x2, d.x3, EV, d.left, d.right, wgt, d.scaler, d.scaler_sum, ctx->ws, n};
+      plfx::DnaArgs a{d.x1, d.x2, d.x3, EV, d.left, d.right, wgt, d.scaler, d.scaler_sum, w->ws, n};
       hipError_t e = plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s,
                                            tips, tipvec);
       if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot launch");
+      if (launches) ++*launches;
     }
     return PLFX_OK;
   }
   for (int i = 0; i < count; i += plfx::kMaxBatch) {
     const int c = std::min(plfx::kMaxBatch, count - i);
     hipError_t e = plfx::launch_plf_dna_batch(dtype, reinterpret_cast<const plfx::NodeDescH *>(nodes + i),
-                                              c, EV, wgt, n, ctx->ws, ctx->max_blocks, s, tips,
+                                              c, EV, wgt, n, w->ws, ctx->max_blocks, s, tips,
                                               tipvec);
     if (e != hipSuccess) return hip_fail(ctx, e, "plf batch launch");
+    if (launches) ++*launches;
   }
   return PLFX_OK;
 }
@@ -251,8 +350,8 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
   plfx_ctx *ctx = new (std::nothrow) plfx_ctx();
   if (!ctx) return PLFX_ERR_NOMEM;
   ctx->device = device;
-  if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+  DeviceGuard guard(device);  // the caller's current device is restored on return
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return PLFX_ERR_HIP;
   }
@@ -263,20 +362,12 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
     if (v > 0) ctx->max_blocks = v;
   }
   if (const char *env = std::getenv("PLFX_FUSE")) ctx->fuse = std::atoi(env);
-  const size_t ws_regions = std::max({plfx::kMaxBatch, 7 * plfx::kMaxSeptets, plfx::kDeepNodes});
-  const size_t ws_bytes = ws_regions * plfx::kWsWords * sizeof(unsigned long long);
-  if (hipMalloc(reinterpret_cast<void **>(&ctx->ws), ws_bytes) != hipSuccess ||
-      hipMemsetAsync(ctx->ws, 0, ws_bytes, ctx->stream) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void **>(&ctx->lnl_partials), plfx::kLnlMaxGrid * sizeof(double)) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void **>(&ctx->lnl_ticket), plfx::kWsWords * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemsetAsync(ctx->lnl_ticket, 0, plfx::kWsWords * sizeof(unsigned long long), ctx->stream) != hipSuccess ||
-      hipStreamSynchronize(ctx->stream) != hipSuccess) {
-    if (ctx->ws) (void)hipFree(ctx->ws);
-    if (ctx->lnl_partials) (void)hipFree(ctx->lnl_partials);
-    if (ctx->lnl_ticket) (void)hipFree(ctx->lnl_ticket);
+  int rc = PLFX_OK;
+  if (!ws_for(ctx, ctx->stream, &rc) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    for (StreamWs &w : ctx->wss) (void)hipFree(w.block);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
-    return PLFX_ERR_HIP;
+    return rc != PLFX_OK ? rc : PLFX_ERR_HIP;
   }
   *out = ctx;
   return PLFX_OK;
@@ -284,19 +375,21 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
 
 int plfx_ctx_destroy(plfx_ctx *ctx) {
   if (!ctx) return PLFX_OK;
-  (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->d_buf) (void)hipFree(ctx->d_buf);
-  if (ctx->d2h_stream) {
-    (void)hipStreamSynchronize(ctx->d2h_stream);
-    (void)hipStreamDestroy(ctx->d2h_stream);
+  {
+    DeviceGuard guard(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_buf) (void)hipFree(ctx->d_buf);
+    if (ctx->d2h_stream) {
+      (void)hipStreamSynchronize(ctx->d2h_stream);
+      (void)hipStreamDestroy(ctx->d2h_stream);
+    }
+    for (hipEvent_t e : ctx->chunk_done)
+      if (e) (void)hipEventDestroy(e);
+    // other streams' workspaces: their last launches must be done before the free
+    (void)hipDeviceSynchronize();
+    for (StreamWs &w : ctx->wss) (void)hipFree(w.block);
+    (void)hipStreamDestroy(ctx->stream);
   }
-  for (hipEvent_t e : ctx->chunk_done)
-    if (e) (void)hipEventDestroy(e);
-  if (ctx->ws) (void)hipFree(ctx->ws);
-  if (ctx->lnl_partials) (void)hipFree(ctx->lnl_partials);
-  if (ctx->lnl_ticket) (void)hipFree(ctx->lnl_ticket);
-  (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return PLFX_OK;
 }
@@ -308,31 +401,35 @@ void *plfx_ctx_stream(plfx_ctx *ctx) { return ctx ? reinterpret_cast<void *>(ctx
 int plfx_ctx_device(const plfx_ctx *ctx) { return ctx ? ctx->device : -1; }
 
 int plfx_ctx_synchronize(plfx_ctx *ctx) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
   PLFX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return PLFX_OK;
 }
 
 int plfx_plf_f32(plfx_ctx *ctx, const float *x1, const float *x2, float *x3, const float *EV, int n,
                  const float *left, const float *right, const int *wgt, int *scalerIncrement) {
+  PLFX_BIND(ctx);
   return plf_host<float>(ctx, x1, x2, x3, EV, n, left, right, wgt, scalerIncrement);
 }
 
 int plfx_plf_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *x3, const double *EV,
                  int n, const double *left, const double *right, const int *wgt,
                  int *scalerIncrement) {
+  PLFX_BIND(ctx);
   return plf_host<double>(ctx, x1, x2, x3, EV, n, left, right, wgt, scalerIncrement);
 }
 
 int plfx_plf_dev_f32(plfx_ctx *ctx, const float *x1, const float *x2, float *x3, const float *EV,
                      int64_t n, const float *left, const float *right, const int32_t *wgt,
                      uint8_t *scaler, int64_t *scaler_sum, void *stream) {
+  PLFX_BIND(ctx);
   return plf_dev<float>(ctx, x1, x2, x3, EV, n, left, right, wgt, scaler, scaler_sum, stream);
 }
 
 int plfx_plf_dev_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *x3,
                      const double *EV, int64_t n, const double *left, const double *right,
                      const int32_t *wgt, uint8_t *scaler, int64_t *scaler_sum, void *stream) {
+  PLFX_BIND(ctx);
   return plf_dev<double>(ctx, x1, x2, x3, EV, n, left, right, wgt, scaler, scaler_sum, stream);
 }
 
@@ -340,7 +437,7 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
                      const void *x2, void *x3, const void *EV, int64_t n, const void *left,
                      const void *right, const int32_t *wgt, uint8_t *scaler,
                      int64_t *scaler_sum, void *stream) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
   if (flags & ~PLFX_FMA) return fail(ctx, PLFX_ERR_INVALID, "bad flags %d", flags);
   if (states == 4) {
@@ -360,7 +457,8 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
     if (scaler_sum) PLFX_HIP(ctx, hipMemsetAsync(scaler_sum, 0, sizeof(int64_t), s));
     return PLFX_OK;
   }
-  plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, ctx->ws, n};
+  PLFX_WS(ctx, s, w);
+  plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, w->ws, n};
   hipError_t e = plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot launch");
   return PLFX_OK;
@@ -369,7 +467,7 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
 int plfx_instance_run(plfx_ctx *ctx, const void *in_left, const void *in_right, void *out_clv,
                       uint8_t *out_scaler, uint32_t alignment_sites, uint32_t window_size,
                       int layout, int dtype, void *stream) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
   if (layout != PLFX_LAYOUT_COMBINED && layout != PLFX_LAYOUT_SEPARATE)
     return fail(ctx, PLFX_ERR_INVALID, "bad layout %d", layout);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
@@ -398,7 +496,7 @@ int plfx_instance_run(plfx_ctx *ctx, const void *in_left, const void *in_right, 
 int plfx_instance_run_host(plfx_ctx *ctx, const void *in_left, const void *in_right,
                            void *out_clv, uint8_t *out_scaler, uint32_t alignment_sites,
                            uint32_t window_size, int layout, int dtype) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
   if (layout != PLFX_LAYOUT_COMBINED && layout != PLFX_LAYOUT_SEPARATE)
     return fail(ctx, PLFX_ERR_INVALID, "bad layout %d", layout);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
@@ -429,7 +527,7 @@ int plfx_instance_run_host(plfx_ctx *ctx, const void *in_left, const void *in_ri
 
 int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *nodes, int count,
                        const void *EV, int64_t n, const int32_t *wgt, void *stream) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
   if (states != 4 && states != 20)
     return fail(ctx, PLFX_ERR_UNSUPPORTED, "batched nodes: states=%d not built (4, 20)", states);
@@ -441,7 +539,7 @@ int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const
                           const void *EV, int64_t n, const void *left, const void *right,
                           const int32_t *wgt, uint8_t *scaler, int64_t *scaler_sum,
                           const void *tipvec, void *stream) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
   if (states != 4 && states != 20)
     return fail(ctx, PLFX_ERR_UNSUPPORTED, "states=%d not built (4, 20)", states);
@@ -480,7 +578,8 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
                        int npmats, const void *EV, int64_t n, const int32_t *wgt,
                        uint8_t *const *scalers, int64_t *scaler_sums, const void *tipvec,
                        void *stream) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
+  for (int &c : ctx->sched) c = 0;
   if (states != 4 && states != 20)
     return fail(ctx, PLFX_ERR_UNSUPPORTED, "traverse: states=%d not built (4, 20)", states);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
@@ -518,6 +617,11 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
     nlev = std::max(nlev, lv + 1);
   }
   hipStream_t s = pick(ctx, stream);
+  unsigned long long *ws = nullptr;
+  if (nops > 0 && n > 0) {
+    PLFX_WS(ctx, s, w);
+    ws = w->ws;
+  }
   const char *pm = static_cast<const char *>(pmats);
   // the node descriptor of op j, tip child first (dense/tip runs as tip/dense:
   // the product u1*u2 commutes exactly); *kind = number of tip children
@@ -633,6 +737,12 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
       triples.push_back({a, b, p, ka});
     }
   }
+  // the schedule, as plfx_traverse_schedule reports it
+  int sched[PLFX_SCHED_COUNTS] = {};
+  for (const Deep &t : deeps) sched[6 - t.D]++;
+  sched[3] = (int)septets.size();
+  sched[4] = (int)triples.size();
+  for (int j = 0; j < nops; j++) sched[5] += used[j] ? 0 : 1;
   std::vector<plfx_node> batch[3];  // by number of tip children
   std::vector<plfx::TripleDescH> tb[3];
   std::vector<plfx::SeptetDescH> sb[3];
@@ -667,8 +777,9 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
           if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
         continue;
       }
-      hipError_t e = plfx::launch_plf_dna_deep(dtype, t.D, &d, EV, wgt, n, ctx->ws, ctx->max_blocks, s);
+      hipError_t e = plfx::launch_plf_dna_deep(dtype, t.D, &d, EV, wgt, n, ws, ctx->max_blocks, s);
       if (e != hipSuccess) return hip_fail(ctx, e, "fused deep-subtree launch");
+      sched[6]++;
     }
     for (const Septet &t : septets) {
       if (level[t.a[0]] != lv) continue;
@@ -723,8 +834,9 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
           continue;
         }
         hipError_t e = plfx::launch_plf_dna_septets(dtype, sb[k].data() + i, c, EV, wgt, n,
-                                                    ctx->ws, ctx->max_blocks, s, k, tipvec);
+                                                    ws, ctx->max_blocks, s, k, tipvec);
         if (e != hipSuccess) return hip_fail(ctx, e, "fused three-level launch");
+        sched[6]++;
       }
       for (size_t i = 0; i < tb[k].size(); i += plfx::kMaxTriples) {
         const int c = (int)std::min<size_t>(plfx::kMaxTriples, tb[k].size() - i);
@@ -734,24 +846,33 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
               if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
           continue;
         }
-        hipError_t e = plfx::launch_plf_dna_triples(dtype, tb[k].data() + i, c, EV, wgt, n, ctx->ws,
+        hipError_t e = plfx::launch_plf_dna_triples(dtype, tb[k].data() + i, c, EV, wgt, n, ws,
                                                     ctx->max_blocks, s, k, tipvec);
         if (e != hipSuccess) return hip_fail(ctx, e, "fused level-pair launch");
+        sched[6]++;
       }
       if (batch[k].empty()) continue;
       int rc = batch_impl(ctx, dtype, batch[k].data(), (int)batch[k].size(), EV, n, wgt, s, k,
-                          tipvec, states, flags);
+                          tipvec, states, flags, &sched[6]);
       if (rc != PLFX_OK) return rc;
     }
   }
+  for (int i = 0; i < PLFX_SCHED_COUNTS; i++) ctx->sched[i] = sched[i];
   return PLFX_OK;
+}
+
+int plfx_traverse_schedule(const plfx_ctx *ctx, int *counts, int ncounts) {
+  if (!ctx || (ncounts > 0 && !counts)) return 0;
+  const int m = std::min(ncounts, PLFX_SCHED_COUNTS);
+  for (int i = 0; i < m; i++) counts[i] = ctx->sched[i];
+  return m < 0 ? 0 : m;
 }
 
 int plfx_root_lnl(plfx_ctx *ctx, int dtype, int states, const void *x, int64_t n,
                   const double *catw, const double *freq, const int32_t *wgt,
                   const int64_t *scaler_sums, int nsums, double *out_lnl, double *site_lnl,
                   void *stream) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
   if (states != 4 && states != 20) return fail(ctx, PLFX_ERR_UNSUPPORTED, "lnl: states=%d", states);
   if (!out_lnl || n < 0 || (n > 0 && !x) || nsums < 0 || (nsums > 0 && !scaler_sums))
@@ -761,22 +882,24 @@ int plfx_root_lnl(plfx_ctx *ctx, int dtype, int states, const void *x, int64_t n
     PLFX_HIP(ctx, hipMemsetAsync(out_lnl, 0, sizeof(double), s));
     if (nsums == 0) return PLFX_OK;
   }
+  PLFX_WS(ctx, s, w);
   hipError_t e = plfx::launch_root_lnl(dtype, states, x, n, catw, freq, wgt, scaler_sums, nsums,
-                                       ctx->lnl_partials, ctx->lnl_ticket, out_lnl, site_lnl, s);
+                                       w->lnl_partials, w->lnl_ticket, out_lnl, site_lnl, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "root_lnl launch");
   return PLFX_OK;
 }
 
 int plfx_scaler_sum(plfx_ctx *ctx, const uint8_t *scaler, const int32_t *wgt, int64_t n,
                     int64_t *out_sum, void *stream) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
   if (!out_sum || n < 0 || (n > 0 && !scaler)) return fail(ctx, PLFX_ERR_INVALID, "bad scaler_sum args");
   hipStream_t s = pick(ctx, stream);
   if (n == 0) {
     PLFX_HIP(ctx, hipMemsetAsync(out_sum, 0, sizeof(int64_t), s));
     return PLFX_OK;
   }
-  hipError_t e = plfx::launch_scaler_sum(scaler, wgt, n, out_sum, ctx->ws, ctx->max_blocks, s);
+  PLFX_WS(ctx, s, w);
+  hipError_t e = plfx::launch_scaler_sum(scaler, wgt, n, out_sum, w->ws, ctx->max_blocks, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "scaler_sum launch");
   return PLFX_OK;
 }
@@ -784,7 +907,7 @@ int plfx_scaler_sum(plfx_ctx *ctx, const uint8_t *scaler, const int32_t *wgt, in
 int plfx_pmatrix(plfx_ctx *ctx, int dtype, int states, int convention, const double *eigen,
                  const double *rates, int ncat, const double *blen, int64_t nbranch, void *pmats,
                  void *stream) {
-  if (!ctx) return PLFX_ERR_INVALID;
+  PLFX_BIND(ctx);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
   if (convention != PLFX_PMAT_STATE && convention != PLFX_PMAT_EIGEN)
     return fail(ctx, PLFX_ERR_INVALID, "bad convention %d", convention);

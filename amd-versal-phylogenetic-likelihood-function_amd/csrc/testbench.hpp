@@ -9,8 +9,48 @@
 #pragma once
 #include <cstdint>
 #include <cstring>
+#include <random>
 
 namespace plfx {
+
+// The reference's split of `total` items over `parts` instances
+// (include.h:181-189, offsets host_mem.cpp:229,290-291): n0 = ceil(total /
+// parts), part k starts at k*n0, the last part is short by n0*parts - total.
+// Used for sites over accelerator instances and for independent nodes over
+// ranks.  Returns false where the reference's arithmetic underflows (the
+// padding reaches a whole share, e.g. 10 items over 8 parts).
+inline bool shard(uint64_t total, uint32_t parts, uint32_t k, uint64_t *offset, uint64_t *count) {
+  if (parts == 0 || k >= parts) return false;
+  const uint64_t n0 = (total + parts - 1) / parts;
+  const uint64_t pad = n0 * parts - total;
+  if (parts > 1 && total > 0 && pad >= n0) return false;
+  *offset = (uint64_t)k * n0;
+  *count = total == 0 ? 0 : n0 - (k == parts - 1 ? pad : 0);
+  return true;
+}
+
+// host_mem.cpp:179-209 input protocol with a fixed seed (the reference seeds
+// from std::random_device): std::mt19937 +
+// std::uniform_real_distribution<double>(0, 1); EV[16]; left/right P
+// interleaved; then the CLVs interleaved element by element, the left CLV x1e-12
+// on the first 16 of every 64 elements (every 4th site scales); wgt = 1.
+template <typename T>
+void gen_hostmem(uint32_t seed, uint64_t n, T *ev, T *left, T *right, T *x1, T *x2, int32_t *wgt) {
+  std::mt19937 gen(seed);
+  std::uniform_real_distribution<> dis(0.0, 1.0);
+  for (int j = 0; j < 16; j++) ev[j] = (T)dis(gen);
+  for (int j = 0; j < 64; j++) {
+    left[j] = (T)dis(gen);
+    right[j] = (T)dis(gen);
+  }
+  for (uint64_t j = 0; j < 16 * n; j++) {
+    const double scale = (j % 64 < 16) ? 1.0e-12 : 1.0;
+    x1[j] = (T)(dis(gen) * scale);
+    x2[j] = (T)dis(gen);
+  }
+  if (wgt)
+    for (uint64_t j = 0; j < n; j++) wgt[j] = 1;
+}
 
 enum Layout : int { COMBINED = 0, SEPARATE = 1 };  // include.h:20
 enum Aie : int { STREAM = 0, WINDOW = 1 };         // include.h:21

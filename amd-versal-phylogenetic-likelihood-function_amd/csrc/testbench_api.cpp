@@ -70,4 +70,23 @@ int plfx_pack_instance(const plfx_testbench *t, int k, int dtype, const void *EV
   return PLFX_OK;
 }
 
+int plfx_shard(uint64_t total, uint32_t parts, uint32_t k, uint64_t *offset, uint64_t *count) {
+  if (!offset || !count) return PLFX_ERR_INVALID;
+  return plfx::shard(total, parts, k, offset, count) ? PLFX_OK : PLFX_ERR_INVALID;
+}
+
+int plfx_gen_hostmem(int dtype, uint32_t seed, uint64_t n, void *EV, void *left, void *right,
+                     void *x1, void *x2, int32_t *wgt) {
+  if (!EV || !left || !right || (n > 0 && (!x1 || !x2))) return PLFX_ERR_INVALID;
+  if (dtype == PLFX_F32)
+    plfx::gen_hostmem<float>(seed, n, (float *)EV, (float *)left, (float *)right, (float *)x1,
+                             (float *)x2, wgt);
+  else if (dtype == PLFX_F64)
+    plfx::gen_hostmem<double>(seed, n, (double *)EV, (double *)left, (double *)right,
+                              (double *)x1, (double *)x2, wgt);
+  else
+    return PLFX_ERR_INVALID;
+  return PLFX_OK;
+}
+
 }  // extern "C"

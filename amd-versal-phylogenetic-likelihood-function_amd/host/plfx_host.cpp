@@ -2,13 +2,17 @@
 // reference's app/src/host_mem.cpp (XRT) with the accelerator replaced by HIP.
 //
 //   usage: plfx_host <alignment sites> <plf calls> <parallel instances>
-//                    [--dtype f32|f64] [--layout comb|sep] [--aie window|stream]
-//                    [--window BYTES] [--seed S] [--dump PREFIX] [--quiet]
+//                    [--target hw|sw_emu] [--dtype f32|f64] [--layout comb|sep]
+//                    [--aie window|stream] [--window BYTES] [--seed S]
+//                    [--dump PREFIX] [--no-check] [--quiet]
 //
 // Mirrors host_mem.cpp:
 //   * argv shape <sites> <calls> <instances> (host_mem.cpp:13-38); the xclbin
 //     and BDF arguments are gone, layout/AIE type/window are explicit flags
 //     instead of being parsed out of the xclbin file name;
+//     --target picks the run mode as the Makefile's TARGET does
+//     (Makefile:199-220): hw = the GPU, sw_emu = the accelerator instance
+//     emulated on the CPU (plfx_swemu_instance_run, no GPU touched);
 //   * size table (host_mem.cpp:45-101) from testbench sizing (include.h:150-266);
 //   * host_mem input protocol (host_mem.cpp:179-209) with a fixed seed (Q8);
 //   * per-instance packing [EV|P_L|CLV_L], [EV|P_R|CLV_R] / [P_R|CLV_R]
@@ -17,16 +21,22 @@
 //     fused kernel -> D2H CLV || D2H scaler, with the begin/t1/t2/end regions
 //     of timing.h:25-52 taken by HIP events (host_mem.cpp:283-325);
 //   * host scaler reduction sum scaler[j]*wgt[j] (host_mem.cpp:384-388);
-//   * timing table in the layout of timing.h:107-151 (no CPU "Reference" row:
-//     the CPU check lives in the tests, which read --dump output).
+//   * the correctness check of host_mem.cpp:403-442: this program's own CPU
+//     plf() (below, plf.cpp:19-65 restated) run plf_calls times and timed,
+//     every CLV value and every scalerIncrement compared exactly, "Test result:
+//     Passed" / "Failed with N errors" (a scalerIncrement mismatch counts as
+//     an error here; the reference only prints it);
+//   * the timing table of timing.h:107-151 per instance and for all instances
+//     together (the reference prints instance 0 only), with the
+//     Reference row and the speed-ups excluding / including the transfers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <random>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -51,6 +61,8 @@ struct Opts {
   uint64_t sites = 0;
   uint32_t calls = 1, instances = 1;
   bool f64 = true;
+  bool sw_emu = false;
+  bool check = true;
   int layout = plfx::SEPARATE;
   int aie = plfx::WINDOW;
   uint32_t window = 8192;
@@ -61,8 +73,9 @@ struct Opts {
 
 Opts parse(int argc, char **argv) {
   if (argc < 4)
-    die("usage: plfx_host <alignment sites> <plf calls> <parallel instances> [--dtype f32|f64] "
-        "[--layout comb|sep] [--aie window|stream] [--window BYTES] [--seed S] [--dump PREFIX]");
+    die("usage: plfx_host <alignment sites> <plf calls> <parallel instances> [--target hw|sw_emu] "
+        "[--dtype f32|f64] [--layout comb|sep] [--aie window|stream] [--window BYTES] [--seed S] "
+        "[--dump PREFIX] [--no-check] [--quiet]");
   Opts o;
   try {
     o.sites = std::stoull(argv[1]);
@@ -82,6 +95,11 @@ Opts parse(int argc, char **argv) {
       if (v == "f32") o.f64 = false;
       else if (v == "f64") o.f64 = true;
       else die("bad dtype " + v);
+    } else if (a == "--target") {
+      std::string v = next();
+      if (v == "hw") o.sw_emu = false;
+      else if (v == "sw_emu") o.sw_emu = true;
+      else die("bad target " + v);
     } else if (a == "--layout") {
       std::string v = next();
       if (v == "comb") o.layout = plfx::COMBINED;
@@ -98,6 +116,8 @@ Opts parse(int argc, char **argv) {
       o.seed = (uint32_t)std::stoul(next());
     } else if (a == "--dump") {
       o.dump = next();
+    } else if (a == "--no-check") {
+      o.check = false;
     } else if (a == "--quiet") {
       o.quiet = true;
     } else {
@@ -105,12 +125,49 @@ Opts parse(int argc, char **argv) {
     }
   }
   if (o.instances == 0 || o.calls == 0) die("calls and instances must be > 0");
-  if (o.aie == plfx::WINDOW && (o.window < 16 || o.window % 16)) die("window must be a multiple of 16 bytes");
+  if (o.aie == plfx::WINDOW && (o.window < 32 || o.window % 32)) die("window must be a multiple of 32 bytes");
+  if (o.sw_emu && o.aie == plfx::STREAM && o.layout != plfx::COMBINED)
+    die("stream movers exist in the COMBINED layout only");
   return o;
 }
 
-struct Region {  // timing.h:25-52, device-event based
-  std::vector<double> hm, msm, mh, total;
+// The host program's own CPU plf() -- the reference host links plf.cpp for
+// its "Reference" row and correctness check (host_mem.cpp:416-420); this is
+// that loop (plf.cpp:19-65) restated, in T.  Built with -ffp-contract=off.
+template <typename T>
+void cpu_plf(const T *x1, const T *x2, T *x3, const T *EV, uint64_t n, const T *left, const T *right,
+             const int *wgt, long long &scalerIncrement) {
+  long long add = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    const T *a = x1 + 16 * i, *b = x2 + 16 * i;
+    T *o = x3 + 16 * i;
+    for (int j = 0; j < 16; j++) o[j] = T(0);
+    for (int c = 0; c < 4; c++) {
+      for (int k = 0; k < 4; k++) {
+        T ul = T(0), ur = T(0);
+        for (int l = 0; l < 4; l++) {
+          ul += a[c * 4 + l] * left[c * 16 + k * 4 + l];
+          ur += b[c * 4 + l] * right[c * 16 + k * 4 + l];
+        }
+        const T p = ul * ur;
+        for (int l = 0; l < 4; l++) o[c * 4 + l] += p * EV[k * 4 + l];
+      }
+    }
+    bool scale = true;
+    for (int j = 0; j < 16 && scale; j++) scale = std::fabs((double)o[j]) < 1.0 / 4294967296.0;
+    if (scale) {
+      for (int j = 0; j < 16; j++) o[j] = (T)(o[j] * 4294967296.0);
+      add += wgt[i];
+    }
+  }
+  scalerIncrement = add;
+}
+
+struct Regions {  // timing.h:25-52: begin/t1/t2/end of one call of one instance, ms
+  double begin, t1, t2, end;
+  double hm() const { return t1 - begin; }
+  double msm() const { return t2 - t1; }
+  double mh() const { return end - t2; }
 };
 
 template <typename T>
@@ -126,9 +183,11 @@ int run(const Opts &o) {
   // instance's share (e.g. 10 sites over 8 instances); reject it instead.
   if (tb.alignments_padding() >= n0 && o.instances > 1) die("too many instances for this many sites");
   const size_t es = sizeof(T);
+  const char *target = o.sw_emu ? "sw_emu" : "hw";
 
   if (!o.quiet) {
     std::printf("==================================================================================\n");
+    std::printf("| target:                  | %53s |\n", target);
     std::printf("| alignment sites:        | %54llu |\n", (unsigned long long)o.sites);
     std::printf("| plf calls:              | %54u |\n", o.calls);
     std::printf("| parallel plfs:          | %54u |\n", o.instances);
@@ -146,113 +205,206 @@ int run(const Opts &o) {
     std::printf("==================================================================================\n");
   }
 
-  plfx_ctx *ctx = nullptr;
-  int rc = plfx_ctx_create(0, &ctx);
-  if (rc != PLFX_OK) die("plfx_ctx_create failed: " + std::to_string(rc));
-
   // host_mem.cpp:179-209 input protocol, fixed seed
-  std::mt19937 gen(o.seed);
-  std::uniform_real_distribution<> dis(0.0f, 1.0f);
   T ev[16], bl[64], br[64];
   const uint64_t elems = o.sites * 16;
   std::vector<T> xl(elems), xr(elems);
-  for (int j = 0; j < 16; j++) ev[j] = (T)dis(gen);
-  for (int j = 0; j < 64; j++) {
-    bl[j] = (T)dis(gen);
-    br[j] = (T)dis(gen);
-  }
-  for (uint64_t j = 0; j < elems; j++) {
-    const double scale = (j % 64 < 16) ? 1.0e-12 : 1.0;
-    xl[j] = (T)(dis(gen) * scale);
-    xr[j] = (T)dis(gen);
-  }
   std::vector<int> wgt(o.sites, 1);
+  plfx::gen_hostmem<T>(o.seed, o.sites, ev, bl, br, xl.data(), xr.data(), wgt.data());
 
-  // per-instance pinned host buffers, device buffers, streams and events
   const uint32_t P = o.instances;
-  std::vector<T *> hL(P), hR(P), dL(P), dR(P), dO(P);
-  std::vector<uint8_t *> dS(P);
-  std::vector<hipStream_t> st(P);
-  std::vector<hipEvent_t> eb(P * o.calls), e1(P * o.calls), e2(P * o.calls), ee(P * o.calls);
-  for (uint32_t k = 0; k < P; k++) {
-    HIPCHK(hipHostMalloc((void **)&hL[k], tb.instance_elements_left() * es));
-    HIPCHK(hipHostMalloc((void **)&hR[k], tb.instance_elements_right() * es));
-    HIPCHK(hipMalloc((void **)&dL[k], tb.instance_elements_left() * es));
-    HIPCHK(hipMalloc((void **)&dR[k], tb.instance_elements_right() * es));
-    HIPCHK(hipMalloc((void **)&dO[k], std::max<uint64_t>(tb.instance_elements_out(), 16) * es));
-    HIPCHK(hipMalloc((void **)&dS[k], std::max<uint64_t>(n0, 1)));
-    HIPCHK(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
-    tb.pack<T>(k, ev, bl, br, xl.data(), xr.data(), hL[k], hR[k]);
-  }
-  for (auto *v : {&eb, &e1, &e2, &ee})
-    for (auto &e : *v) HIPCHK(hipEventCreate(&e));
-
   std::vector<std::vector<T>> result(o.calls, std::vector<T>(elems));
   std::vector<std::vector<uint8_t>> scaler(o.calls, std::vector<uint8_t>(o.sites));
   std::vector<long long> inc(o.calls, 0);
+  std::vector<Regions> reg((size_t)o.calls * P);  // [call][instance]
   const int dt = o.f64 ? PLFX_F64 : PLFX_F32;
+  double wall_ms = 0;
 
-  auto t0 = std::chrono::steady_clock::now();
-  for (uint32_t i = 0; i < o.calls; i++) {
-    for (uint32_t k = 0; k < P; k++) {
-      const uint64_t nk = tb.alignments_per_instance(k);
-      const uint64_t off = tb.instance_site_offset(k);
-      const size_t ev_i = (size_t)i * P + k;
-      HIPCHK(hipEventRecord(eb[ev_i], st[k]));
-      HIPCHK(hipMemcpyAsync(dL[k], hL[k], tb.instance_active_elements_left(k) * es, hipMemcpyHostToDevice, st[k]));
-      HIPCHK(hipMemcpyAsync(dR[k], hR[k], tb.instance_active_elements_right(k) * es, hipMemcpyHostToDevice, st[k]));
-      HIPCHK(hipEventRecord(e1[ev_i], st[k]));
-      rc = plfx_instance_run(ctx, dL[k], dR[k], dO[k], dS[k], (uint32_t)nk,
-                             o.aie == plfx::WINDOW ? o.window : 0, o.layout, dt, st[k]);
-      if (rc != PLFX_OK) die(std::string("plfx_instance_run: ") + plfx_last_error(ctx));
-      HIPCHK(hipEventRecord(e2[ev_i], st[k]));
-      HIPCHK(hipMemcpyAsync(result[i].data() + off * 16, dO[k], nk * 16 * es, hipMemcpyDeviceToHost, st[k]));
-      HIPCHK(hipMemcpyAsync(scaler[i].data() + off, dS[k], nk, hipMemcpyDeviceToHost, st[k]));
-      HIPCHK(hipEventRecord(ee[ev_i], st[k]));
+  if (o.sw_emu) {
+    // the instance dataflow on the CPU; no device memory, so no transfer regions
+    std::vector<std::vector<T>> hL(P, std::vector<T>(tb.instance_elements_left())),
+        hR(P, std::vector<T>(tb.instance_elements_right()));
+    for (uint32_t k = 0; k < P; k++) tb.pack<T>(k, ev, bl, br, xl.data(), xr.data(), hL[k].data(), hR[k].data());
+    auto t0 = std::chrono::steady_clock::now();
+    auto ms_since = [&](std::chrono::steady_clock::time_point a) {
+      return std::chrono::duration<double, std::milli>(a - t0).count();
+    };
+    for (uint32_t i = 0; i < o.calls; i++) {
+      for (uint32_t k = 0; k < P; k++) {
+        const uint64_t nk = tb.alignments_per_instance(k), off = tb.instance_site_offset(k);
+        Regions &r = reg[(size_t)i * P + k];
+        r.begin = r.t1 = ms_since(std::chrono::steady_clock::now());
+        const int rc = plfx_swemu_instance_run(hL[k].data(), hR[k].data(), result[i].data() + off * 16,
+                                               scaler[i].data() + off, (uint32_t)nk,
+                                               o.aie == plfx::WINDOW ? o.window : 0, o.layout, o.aie, dt);
+        if (rc != PLFX_OK) die("plfx_swemu_instance_run failed: " + std::to_string(rc));
+        r.t2 = r.end = ms_since(std::chrono::steady_clock::now());
+      }
+      long long s = 0;  // host_mem.cpp:385-388
+      for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
+      inc[i] = s;
     }
-    for (uint32_t k = 0; k < P; k++) HIPCHK(hipStreamSynchronize(st[k]));
-    long long s = 0;  // host_mem.cpp:385-388
-    for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
-    inc[i] = s;
+    wall_ms = ms_since(std::chrono::steady_clock::now());
+  } else {
+    plfx_ctx *ctx = nullptr;
+    int rc = plfx_ctx_create(0, &ctx);
+    if (rc != PLFX_OK) die("plfx_ctx_create failed: " + std::to_string(rc));
+    // per-instance pinned host buffers, device buffers, streams and events
+    std::vector<T *> hL(P), hR(P), dL(P), dR(P), dO(P);
+    std::vector<uint8_t *> dS(P);
+    std::vector<hipStream_t> st(P);
+    std::vector<hipEvent_t> eb(P * o.calls), e1(P * o.calls), e2(P * o.calls), ee(P * o.calls);
+    hipEvent_t e0;
+    for (uint32_t k = 0; k < P; k++) {
+      HIPCHK(hipHostMalloc((void **)&hL[k], tb.instance_elements_left() * es));
+      HIPCHK(hipHostMalloc((void **)&hR[k], tb.instance_elements_right() * es));
+      HIPCHK(hipMalloc((void **)&dL[k], tb.instance_elements_left() * es));
+      HIPCHK(hipMalloc((void **)&dR[k], tb.instance_elements_right() * es));
+      HIPCHK(hipMalloc((void **)&dO[k], std::max<uint64_t>(tb.instance_elements_out(), 16) * es));
+      HIPCHK(hipMalloc((void **)&dS[k], std::max<uint64_t>(n0, 1)));
+      HIPCHK(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
+      tb.pack<T>(k, ev, bl, br, xl.data(), xr.data(), hL[k], hR[k]);
+    }
+    for (auto *v : {&eb, &e1, &e2, &ee})
+      for (auto &e : *v) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipDeviceSynchronize());
+    auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(hipEventRecord(e0, st[0]));
+    for (uint32_t i = 0; i < o.calls; i++) {
+      for (uint32_t k = 0; k < P; k++) {
+        const uint64_t nk = tb.alignments_per_instance(k);
+        const uint64_t off = tb.instance_site_offset(k);
+        const size_t ev_i = (size_t)i * P + k;
+        HIPCHK(hipEventRecord(eb[ev_i], st[k]));
+        HIPCHK(hipMemcpyAsync(dL[k], hL[k], tb.instance_active_elements_left(k) * es, hipMemcpyHostToDevice, st[k]));
+        HIPCHK(hipMemcpyAsync(dR[k], hR[k], tb.instance_active_elements_right(k) * es, hipMemcpyHostToDevice, st[k]));
+        HIPCHK(hipEventRecord(e1[ev_i], st[k]));
+        rc = plfx_instance_run(ctx, dL[k], dR[k], dO[k], dS[k], (uint32_t)nk,
+                               o.aie == plfx::WINDOW ? o.window : 0, o.layout, dt, st[k]);
+        if (rc != PLFX_OK) die(std::string("plfx_instance_run: ") + plfx_last_error(ctx));
+        HIPCHK(hipEventRecord(e2[ev_i], st[k]));
+        HIPCHK(hipMemcpyAsync(result[i].data() + off * 16, dO[k], nk * 16 * es, hipMemcpyDeviceToHost, st[k]));
+        HIPCHK(hipMemcpyAsync(scaler[i].data() + off, dS[k], nk, hipMemcpyDeviceToHost, st[k]));
+        HIPCHK(hipEventRecord(ee[ev_i], st[k]));
+      }
+      for (uint32_t k = 0; k < P; k++) HIPCHK(hipStreamSynchronize(st[k]));
+      long long s = 0;  // host_mem.cpp:385-388
+      for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
+      inc[i] = s;
+    }
+    wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (size_t q = 0; q < reg.size(); q++) {
+      float a, b, c, d;
+      HIPCHK(hipEventElapsedTime(&a, e0, eb[q]));
+      HIPCHK(hipEventElapsedTime(&b, e0, e1[q]));
+      HIPCHK(hipEventElapsedTime(&c, e0, e2[q]));
+      HIPCHK(hipEventElapsedTime(&d, e0, ee[q]));
+      reg[q] = Regions{a, b, c, d};
+    }
+    for (uint32_t k = 0; k < P; k++) {
+      (void)hipHostFree(hL[k]); (void)hipHostFree(hR[k]);
+      (void)hipFree(dL[k]); (void)hipFree(dR[k]); (void)hipFree(dO[k]); (void)hipFree(dS[k]);
+      (void)hipStreamDestroy(st[k]);
+    }
+    for (auto *v : {&eb, &e1, &e2, &ee})
+      for (auto &e : *v) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(e0);
+    plfx_ctx_destroy(ctx);
   }
-  const double wall_ms =
-      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 
-  // timing regions of instance 0 (as the reference prints, host_mem.cpp:449),
-  // plus the slowest/fastest kernel over all instances and calls
-  double hm = 0, msm = 0, mh = 0, mx = 0, mn = 1e300;
-  for (uint32_t i = 0; i < o.calls; i++) {
-    for (uint32_t k = 0; k < P; k++) {
-      const size_t ev_i = (size_t)i * P + k;
-      float a, b, c;
-      HIPCHK(hipEventElapsedTime(&a, eb[ev_i], e1[ev_i]));
-      HIPCHK(hipEventElapsedTime(&b, e1[ev_i], e2[ev_i]));
-      HIPCHK(hipEventElapsedTime(&c, e2[ev_i], ee[ev_i]));
-      if (k == 0) { hm += a; msm += b; mh += c; }
-      mx = std::max(mx, (double)b);
-      mn = std::min(mn, (double)b);
+  // ---- correctness check and the CPU "Reference" region (host_mem.cpp:403-442)
+  double ref_ms = 0;
+  std::string verdict = "skipped (--no-check)";
+  unsigned errors = 0;
+  if (o.check) {
+    std::vector<T> cpu(elems);
+    std::vector<long long> cinc(o.calls);
+    for (uint32_t i = 0; i < o.calls; i++) {
+      auto a = std::chrono::steady_clock::now();
+      cpu_plf<T>(xl.data(), xr.data(), cpu.data(), ev, o.sites, bl, br, wgt.data(), cinc[i]);
+      ref_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+      for (uint64_t j = 0; j < elems && errors < 20; j++) {
+        if (std::memcmp(&cpu[j], &result[i][j], sizeof(T)) != 0) {  // bit patterns, stricter than !=
+          std::printf("ERROR: alignment data wrong for call %u at alignment %llu, probability %llu, "
+                      "cpu!=%s: %.17g!=%.17g\n", i, (unsigned long long)(j >> 4),
+                      (unsigned long long)(j % 16), target, (double)cpu[j], (double)result[i][j]);
+          errors++;
+        }
+      }
+      if (cinc[i] != inc[i]) {
+        std::printf("ERROR: scalerIncrement wrong for call %u, cpu!=gpu: %lld!=%lld\n", i, cinc[i], inc[i]);
+        errors++;
+      }
     }
+    verdict = errors == 0 ? "Passed"
+                          : (errors >= 20 ? "Failed with more than 20 errors"
+                                          : "Failed with " + std::to_string(errors) + " errors");
   }
+
+  // ---- timing table (timing.h:107-151), per instance and for all instances
+  const double bytes_inst = (double)(tb.instance_elements_left() + tb.instance_elements_right() +
+                                     tb.instance_elements_out()) * es;
   const double total_sites = (double)o.sites * o.calls;
-  const double bytes = (double)(tb.instance_elements_left() + tb.instance_elements_right() +
-                                tb.instance_elements_out()) * es * P * o.calls;
-  auto row = [&](const char *name, double ms, double nbytes, double nsites) {
-    std::printf("| %-38s | %10.4f | %16.1f | %24.3f |\n", name, ms, nbytes / 1e6 / (ms / 1e3),
-                nsites / (ms / 1e3) * 1e-6);
+  auto row = [&](const std::string &name, double ms, double nbytes, double nsites) {
+    std::printf("| %-38s | %10.4f | %16.1f | %24.3f |\n", name.c_str(), ms,
+                ms > 0 ? nbytes / 1e6 / (ms / 1e3) : 0.0, ms > 0 ? nsites / (ms / 1e3) * 1e-6 : 0.0);
   };
+  // all instances of a call together: first begin .. last end of each region
+  double agg_hm = 0, agg_msm = 0, agg_mh = 0;
+  for (uint32_t i = 0; i < o.calls; i++) {
+    Regions a{1e300, -1e300, -1e300, -1e300};
+    double b0 = 1e300;
+    for (uint32_t k = 0; k < P; k++) {
+      const Regions &r = reg[(size_t)i * P + k];
+      b0 = std::min(b0, r.begin);
+      a.t1 = std::max(a.t1, r.t1);
+      a.t2 = std::max(a.t2, r.t2);
+      a.end = std::max(a.end, r.end);
+    }
+    a.begin = b0;
+    agg_hm += a.hm();
+    agg_msm += a.msm();
+    agg_mh += a.mh();
+  }
   if (!o.quiet) {
     std::printf("=====================================================================================================\n");
-    std::printf("| Timing region                          | time (ms)  | bandwidth (MB/s) |         bandwidth (MA/s) |\n");
+    std::printf("| Timing region (%-6s)                 | time (ms)  | bandwidth (MB/s) |         bandwidth (MA/s) |\n", target);
     std::printf("=====================================================================================================\n");
-    row("Host to GPU memory (instance 0):", hm, bytes / P, total_sites / P);
-    row("GPU PLF kernel (instance 0):", msm, bytes / P, total_sites / P);
-    row("  - slowest call/instance:", mx, bytes / P / o.calls, total_sites / P / o.calls);
-    row("  - fastest call/instance:", mn, bytes / P / o.calls, total_sites / P / o.calls);
-    row("GPU memory to host (instance 0):", mh, bytes / P, total_sites / P);
-    row("Total wall time (all instances):", wall_ms, bytes, total_sites);
+    for (uint32_t k = 0; k < P; k++) {
+      const double nk_sites = (double)tb.alignments_per_instance(k) * o.calls;
+      double hm = 0, msm = 0, mh = 0, mx = 0, mn = 1e300;
+      for (uint32_t i = 0; i < o.calls; i++) {
+        const Regions &r = reg[(size_t)i * P + k];
+        hm += r.hm();
+        msm += r.msm();
+        mh += r.mh();
+        mx = std::max(mx, r.msm());
+        mn = std::min(mn, r.msm());
+      }
+      const std::string tag = "[instance " + std::to_string(k) + "] ";
+      row(tag + "Host to GPU memory:", hm, bytes_inst * o.calls, nk_sites);
+      row(tag + "GPU PLF kernel:", msm, bytes_inst * o.calls, nk_sites);
+      row("  - slowest call:", mx, bytes_inst, nk_sites / o.calls);
+      row("  - fastest call:", mn, bytes_inst, nk_sites / o.calls);
+      row(tag + "GPU memory to host:", mh, bytes_inst * o.calls, nk_sites);
+    }
+    std::printf("|----------------------------------------+------------+------------------+--------------------------|\n");
+    row("[all instances] Host to GPU memory:", agg_hm, bytes_inst * P * o.calls, total_sites);
+    row("[all instances] GPU PLF kernel:", agg_msm, bytes_inst * P * o.calls, total_sites);
+    row("[all instances] GPU memory to host:", agg_mh, bytes_inst * P * o.calls, total_sites);
+    row("Total execution time:", wall_ms, bytes_inst * P * o.calls, total_sites);
     std::printf("=====================================================================================================\n");
+    if (o.check) {
+      row("Reference (CPU plf, 1 thread):", ref_ms, bytes_inst * P * o.calls, total_sites);
+      std::printf("|----------------------------------------+------------+------------------+--------------------------|\n");
+      std::printf("| Speed up (excluding transfers):        | %56.3f |\n", agg_msm > 0 ? ref_ms / agg_msm : 0.0);
+      std::printf("| Speed up (including transfers):        | %56.3f |\n", wall_ms > 0 ? ref_ms / wall_ms : 0.0);
+      std::printf("=====================================================================================================\n");
+    }
     for (uint32_t i = 0; i < o.calls; i++) std::printf("scalerIncrement[call %u] = %lld\n", i, inc[i]);
   }
+  std::printf("Test result: %s\n", verdict.c_str());
   if (!o.dump.empty()) {
     for (uint32_t i = 0; i < o.calls; i++) {
       std::string base = o.dump + "_call" + std::to_string(i);
@@ -268,15 +420,7 @@ int run(const Opts &o) {
       std::fclose(f);
     }
   }
-  for (uint32_t k = 0; k < P; k++) {
-    (void)hipHostFree(hL[k]); (void)hipHostFree(hR[k]);
-    (void)hipFree(dL[k]); (void)hipFree(dR[k]); (void)hipFree(dO[k]); (void)hipFree(dS[k]);
-    (void)hipStreamDestroy(st[k]);
-  }
-  for (auto *v : {&eb, &e1, &e2, &ee})
-    for (auto &e : *v) (void)hipEventDestroy(e);
-  plfx_ctx_destroy(ctx);
-  return 0;
+  return errors == 0 ? 0 : 1;
 }
 
 }  // namespace

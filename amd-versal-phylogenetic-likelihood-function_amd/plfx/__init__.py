@@ -51,7 +51,10 @@ EXPORTS = (
     "plfx_plf_tips_dev", "plfx_plf_tips_dev_gen", "plfx_traverse_tips",
     "plfx_model_eigen", "plfx_gamma_rates", "plfx_model_ev", "plfx_model_root_weights",
     "plfx_pmatrix", "plfx_model_tip_vectors",
+    "plfx_shard", "plfx_gen_hostmem", "plfx_swemu_instance_run", "plfx_traverse_schedule",
 )
+MAX_STREAMS = 64   # PLFX_MAX_STREAMS
+SCHED_KEYS = ("deep6", "deep5", "deep4", "septets", "triples", "unfused", "launches")
 PMAT_STATE, PMAT_EIGEN = 0, 1
 EXACT, FMA = 0, 1
 PROT_CODES = 24  # protein tip codes: rows of the tip-vector table (plfx.h section 8)
@@ -142,6 +145,11 @@ def load():
     L.plfx_traverse_tips.argtypes = [vp, i32, i32, i32, C.POINTER(TravOp), i32, C.POINTER(vp),
                                      C.POINTER(vp), i32, vp, i32, vp, i64, vp, C.POINTER(vp), vp, vp,
                                      vp]
+    u64p = C.POINTER(C.c_uint64)
+    L.plfx_shard.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, u64p, u64p]
+    L.plfx_gen_hostmem.argtypes = [i32, C.c_uint32, C.c_uint64, vp, vp, vp, vp, vp, vp]
+    L.plfx_swemu_instance_run.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, i32, i32, i32]
+    L.plfx_traverse_schedule.argtypes = [vp, C.POINTER(i32), i32]
     _lib = L
     return L
 
@@ -239,16 +247,11 @@ class Context:
             raise PlfxError(ERR_INVALID, "CLV tensors shorter than 16*n")
         if EV.numel() < 16 or left.numel() < 64 or right.numel() < 64:
             raise PlfxError(ERR_INVALID, "EV needs 16, left/right 64 values")
-        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n or not wgt.is_cuda):
-            raise PlfxError(ERR_INVALID, "wgt must be an int32 device tensor of >= n elements")
-        if scaler is not None and (scaler.dtype != torch.uint8 or scaler.numel() < n):
-            raise PlfxError(ERR_INVALID, "scaler must be a uint8 device tensor of >= n elements")
-        if scaler_sum is not None and (scaler_sum.dtype != torch.int64 or scaler_sum.numel() < 1):
-            raise PlfxError(ERR_INVALID, "scaler_sum must be an int64 device tensor")
+        _check_aux(n, wgt, scaler, scaler_sum)
         fn = self._L.plfx_plf_dev_f32 if dt == torch.float32 else self._L.plfx_plf_dev_f64
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         self._check(fn(self.h, p(x1), p(x2), p(x3), p(EV), n, p(left), p(right), p(wgt),
-                       p(scaler), p(scaler_sum), _stream_handle(stream)))
+                       p(scaler), p(scaler_sum), _stream_handle(stream, self.device)))
 
     def bind_plf_dev(self, x1, x2, x3, EV, left, right, wgt=None, scaler=None, scaler_sum=None,
                      n=None):
@@ -266,9 +269,10 @@ class Context:
         args = (self.h, p(x1), p(x2), p(x3), p(EV), C.c_int64(n), p(left), p(right), p(wgt),
                 p(scaler), p(scaler_sum))
         check = self._check
+        dev = self.device
 
         def run(stream=None):
-            check(fn(*args, _stream_handle(stream)))
+            check(fn(*args, _stream_handle(stream, self.device)))
 
         return run
 
@@ -291,7 +295,7 @@ class Context:
         self._check(self._L.plfx_instance_run(self.h, p(in_left), p(in_right), p(out_clv),
                                               p(out_scaler), n, int(window_size), int(layout),
                                               F32 if dt == torch.float32 else F64,
-                                              _stream_handle(stream)))
+                                              _stream_handle(stream, self.device)))
 
     def instance_run_host(self, in_left, in_right, out_clv, out_scaler, alignment_sites,
                           window_size, layout):
@@ -336,17 +340,12 @@ class Context:
             raise PlfxError(ERR_INVALID, "CLV tensors shorter than 4*states*n")
         if EV.numel() < states * states or min(left.numel(), right.numel()) < 4 * states * states:
             raise PlfxError(ERR_INVALID, "EV needs S*S, left/right 4*S*S values")
-        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n):
-            raise PlfxError(ERR_INVALID, "wgt must be int32 with >= n elements")
-        if scaler is not None and (scaler.dtype != torch.uint8 or scaler.numel() < n):
-            raise PlfxError(ERR_INVALID, "scaler must be uint8 with >= n elements")
-        if scaler_sum is not None and scaler_sum.dtype != torch.int64:
-            raise PlfxError(ERR_INVALID, "scaler_sum must be int64")
+        _check_aux(n, wgt, scaler, scaler_sum)
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         self._check(self._L.plfx_plf_dev_gen(self.h, F32 if dt == torch.float32 else F64, int(states),
                                              FMA if fma else EXACT, p(x1), p(x2), p(x3), p(EV), n,
                                              p(left), p(right), p(wgt), p(scaler), p(scaler_sum),
-                                             _stream_handle(stream)))
+                                             _stream_handle(stream, self.device)))
 
     # -- (6) batched nodes / traversal ---------------------------------------
     def plf_batch_dev(self, nodes, EV, n, wgt=None, stream=None, states=4):
@@ -362,18 +361,48 @@ class Context:
         for i, nd in enumerate(nodes):
             for k in ("x1", "x2", "x3"):
                 t = nd[k]
-                if t.dtype != dt or t.numel() < V * n or not t.is_contiguous():
-                    raise PlfxError(ERR_INVALID, f"node {i}: {k} must be contiguous {dt} >= {V}*n")
+                if t.dtype != dt or t.numel() < V * n or not t.is_contiguous() or not t.is_cuda:
+                    raise PlfxError(ERR_INVALID, f"node {i}: {k} must be a contiguous {dt} device "
+                                                 f"tensor >= {V}*n")
             for k in ("left", "right"):
-                if nd[k].dtype != dt or nd[k].numel() < M:
-                    raise PlfxError(ERR_INVALID, f"node {i}: {k} needs {M} values")
+                if nd[k].dtype != dt or nd[k].numel() < M or not nd[k].is_cuda:
+                    raise PlfxError(ERR_INVALID, f"node {i}: {k} needs {M} device values")
+            try:
+                _check_aux(n, None, nd.get("scaler"), nd.get("scaler_sum"))
+            except PlfxError as e:
+                raise PlfxError(ERR_INVALID, f"node {i}: {e}") from None
             arr[i] = Node(ptr(nd["x1"]), ptr(nd["x2"]), ptr(nd["x3"]), ptr(nd["left"]),
                           ptr(nd["right"]), ptr(nd.get("scaler")), ptr(nd.get("scaler_sum")))
-        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n):
-            raise PlfxError(ERR_INVALID, "wgt must be int32 with >= n elements")
+        _check_aux(n, wgt, None, None)
+        if not EV.is_cuda:
+            raise PlfxError(ERR_INVALID, "EV must be a device tensor")
         self._check(self._L.plfx_plf_batch_dev(self.h, F32 if dt == torch.float32 else F64, states, arr,
                                                len(nodes), C.c_void_p(EV.data_ptr()), int(n),
-                                               C.c_void_p(ptr(wgt)), _stream_handle(stream)))
+                                               C.c_void_p(ptr(wgt)), _stream_handle(stream, self.device)))
+
+    def bind_plf_batch_dev(self, nodes, EV, n, wgt=None, states=4):
+        """Validate once (as plf_batch_dev) and return a launcher
+        ``run(stream=None)`` issuing the same batched call with a prebuilt
+        node array (graph capture / launch-rate bound loops).  The tensors must
+        stay alive and unchanged while the launcher is used."""
+        import torch
+
+        if not nodes:
+            return lambda stream=None: None
+        self.plf_batch_dev(nodes, EV, n, wgt, stream=torch.cuda.current_stream(self.device).cuda_stream,
+                           states=states)  # validates
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        arr = (Node * len(nodes))(*[Node(ptr(nd["x1"]), ptr(nd["x2"]), ptr(nd["x3"]), ptr(nd["left"]),
+                                         ptr(nd["right"]), ptr(nd.get("scaler")),
+                                         ptr(nd.get("scaler_sum"))) for nd in nodes])
+        fn, h, check, dev = self._L.plfx_plf_batch_dev, self.h, self._check, self.device
+        args = (F32 if EV.dtype == torch.float32 else F64, states, arr, len(nodes),
+                C.c_void_p(EV.data_ptr()), int(n), C.c_void_p(ptr(wgt)))
+
+        def run(stream=None):
+            check(fn(h, *args, _stream_handle(stream, dev)))
+
+        return run
 
     def traverse(self, ops, clv, pmats, EV, n, wgt=None, scalers=None, scaler_sums=None,
                  stream=None, tips=None, tipvec=None, states=4, fma=False):
@@ -397,15 +426,31 @@ class Context:
         for s_, t in enumerate(clv):
             tip = None if tips is None else tips[s_]
             if tip is not None:
-                if tip.dtype != torch.uint8 or tip.numel() < n or not tip.is_contiguous():
+                if tip.dtype != torch.uint8 or tip.numel() < n or not tip.is_contiguous() or not tip.is_cuda:
                     raise PlfxError(ERR_INVALID, f"tip slot {s_}: contiguous uint8 >= n required")
                 continue
-            if t is None or t.dtype != dt or t.numel() < V * n or not t.is_contiguous():
-                raise PlfxError(ERR_INVALID, f"every CLV slot must be contiguous, same dtype, >= {V}*n")
+            if t is None or t.dtype != dt or t.numel() < V * n or not t.is_contiguous() or not t.is_cuda:
+                raise PlfxError(ERR_INVALID, f"every CLV slot must be a contiguous device tensor, "
+                                             f"same dtype, >= {V}*n")
         if pmats.dtype != dt or pmats.numel() % (2 * M):
             raise PlfxError(ERR_INVALID, f"pmats must hold whole (left, right) pairs of {M} values")
-        if scaler_sums is not None and (scaler_sums.dtype != torch.int64 or scaler_sums.numel() < nops):
-            raise PlfxError(ERR_INVALID, "scaler_sums must be int64 with >= nops entries")
+        if scaler_sums is not None and (scaler_sums.dtype != torch.int64 or scaler_sums.numel() < nops
+                                        or not scaler_sums.is_cuda):
+            raise PlfxError(ERR_INVALID, "scaler_sums must be an int64 device tensor with >= nops entries")
+        if scalers is not None:
+            if len(scalers) > nops:
+                raise PlfxError(ERR_INVALID, "more scaler tensors than ops")
+            scalers = list(scalers) + [None] * (nops - len(scalers))
+            for j, t in enumerate(scalers):
+                if t is not None and (t.dtype != torch.uint8 or not t.is_cuda or not t.is_contiguous()
+                                      or t.numel() < n):
+                    raise PlfxError(ERR_INVALID, f"scaler of op {j} must be a contiguous uint8 "
+                                                 f"device tensor of >= n elements")
+        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n or not wgt.is_cuda):
+            raise PlfxError(ERR_INVALID, "wgt must be an int32 device tensor of >= n elements")
+        for t in (pmats, EV):
+            if not t.is_cuda or not t.is_contiguous():
+                raise PlfxError(ERR_INVALID, "pmats and EV must be contiguous device tensors")
         top = (TravOp * nops)(*[TravOp(*map(int, r)) for r in ops])
         slots = (C.c_void_p * nslots)(*[None if t is None else t.data_ptr() for t in clv])
         tp = None
@@ -420,7 +465,7 @@ class Context:
             C.c_void_p(EV.data_ptr()), int(n),
             C.c_void_p(None if wgt is None else wgt.data_ptr()), sc,
             C.c_void_p(None if scaler_sums is None else scaler_sums.data_ptr()),
-            self._tipvec(tipvec, dt, states), _stream_handle(stream)))
+            self._tipvec(tipvec, dt, states), _stream_handle(stream, self.device)))
 
     @staticmethod
     def _tipvec(tipvec, dt, states=4):
@@ -444,16 +489,30 @@ class Context:
         dt = EV.dtype
         V = 4 * states
         for k, t in (("x3", x3), ("x1", x1), ("x2", x2)):
-            if t is not None and (t.dtype != dt or t.numel() < V * n or not t.is_contiguous()):
-                raise PlfxError(ERR_INVALID, f"{k} must be contiguous {dt} >= {V}*n")
+            if t is not None and (t.dtype != dt or t.numel() < V * n or not t.is_contiguous()
+                                  or not t.is_cuda):
+                raise PlfxError(ERR_INVALID, f"{k} must be a contiguous {dt} device tensor >= {V}*n")
         for k, t in (("tip1", tip1), ("tip2", tip2)):
-            if t is not None and (t.dtype != torch.uint8 or t.numel() < n or not t.is_contiguous()):
-                raise PlfxError(ERR_INVALID, f"{k} must be contiguous uint8 >= n")
+            if t is not None and (t.dtype != torch.uint8 or t.numel() < n or not t.is_contiguous()
+                                  or not t.is_cuda):
+                raise PlfxError(ERR_INVALID, f"{k} must be a contiguous uint8 device tensor >= n")
+        for k, t in (("EV", EV), ("left", left), ("right", right)):
+            if t.dtype != dt or not t.is_cuda or t.numel() < (states * states if k == "EV"
+                                                               else 4 * states * states):
+                raise PlfxError(ERR_INVALID, f"{k} must be a {dt} device tensor of the model's size")
+        _check_aux(n, wgt, scaler, scaler_sum)
         p = lambda t: C.c_void_p(None if t is None else t.data_ptr())  # noqa: E731
         self._check(self._L.plfx_plf_tips_dev_gen(
             self.h, F32 if dt == torch.float32 else F64, states, FMA if fma else EXACT, p(tip1),
             p(x1), p(tip2), p(x2), p(x3), p(EV), int(n), p(left), p(right), p(wgt), p(scaler),
-            p(scaler_sum), self._tipvec(tipvec, dt, states), _stream_handle(stream)))
+            p(scaler_sum), self._tipvec(tipvec, dt, states), _stream_handle(stream, self.device)))
+
+    def last_schedule(self):
+        """The schedule the last traverse() on this context chose
+        (plfx_traverse_schedule): dict over SCHED_KEYS."""
+        c = (C.c_int * len(SCHED_KEYS))()
+        m = self._L.plfx_traverse_schedule(self.h, c, len(SCHED_KEYS))
+        return {k: int(c[i]) for i, k in enumerate(SCHED_KEYS[:m])}
 
     # -- (9) P matrices from branch lengths --------------------------------
     def pmatrix(self, eigen, rates, blen, out, states=4, convention=PMAT_STATE, stream=None):
@@ -473,7 +532,7 @@ class Context:
         self._check(self._L.plfx_pmatrix(
             self.h, F32 if out.dtype == torch.float32 else F64, S, convention,
             C.c_void_p(eigen.data_ptr()), C.c_void_p(rates.data_ptr()), ncat,
-            C.c_void_p(blen.data_ptr()), nb, C.c_void_p(out.data_ptr()), _stream_handle(stream)))
+            C.c_void_p(blen.data_ptr()), nb, C.c_void_p(out.data_ptr()), _stream_handle(stream, self.device)))
 
     # -- (7) root log-likelihood --------------------------------------------
     def root_lnl(self, x, n, out, catw=None, freq=None, wgt=None, scaler_sums=None,
@@ -492,7 +551,7 @@ class Context:
         nsums = 0 if scaler_sums is None else scaler_sums.numel()
         self._check(self._L.plfx_root_lnl(self.h, F32 if x.dtype == torch.float32 else F64, states,
                                           p(x), int(n), p(catw), p(freq), p(wgt), p(scaler_sums),
-                                          nsums, p(out), p(site_lnl), _stream_handle(stream)))
+                                          nsums, p(out), p(site_lnl), _stream_handle(stream, self.device)))
 
     # -- (4) scaler reduction ----------------------------------------------
     def scaler_sum(self, scaler, wgt, out_sum, n=None, stream=None):
@@ -506,17 +565,87 @@ class Context:
             raise PlfxError(ERR_INVALID, "wgt int32 with >= n elements")
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         self._check(self._L.plfx_scaler_sum(self.h, p(scaler), p(wgt), int(n), p(out_sum),
-                                            _stream_handle(stream)))
+                                            _stream_handle(stream, self.device)))
 
 
-def _stream_handle(stream):
+def _stream_handle(stream, device=None):
+    """None = torch's current stream ON THE CONTEXT'S DEVICE (not the current
+    device's), a torch.cuda.Stream, or a raw hipStream_t int."""
     if stream is None:
         import torch
 
-        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
     if isinstance(stream, int):
         return C.c_void_p(stream)
     return C.c_void_p(stream.cuda_stream)
+
+
+def _check_aux(n, wgt, scaler, scaler_sum):
+    """Shapes/dtypes/devices of the optional per-site weight, scaler bytes and
+    scaler-sum outputs (the C ABI cannot see tensor sizes)."""
+    import torch
+
+    if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n or not wgt.is_cuda
+                            or not wgt.is_contiguous()):
+        raise PlfxError(ERR_INVALID, "wgt must be a contiguous int32 device tensor of >= n elements")
+    if scaler is not None and (scaler.dtype != torch.uint8 or scaler.numel() < n or not scaler.is_cuda
+                               or not scaler.is_contiguous()):
+        raise PlfxError(ERR_INVALID, "scaler must be a contiguous uint8 device tensor of >= n elements")
+    if scaler_sum is not None and (scaler_sum.dtype != torch.int64 or scaler_sum.numel() < 1
+                                   or not scaler_sum.is_cuda):
+        raise PlfxError(ERR_INVALID, "scaler_sum must be an int64 device tensor")
+
+
+def shard(total, parts, k):
+    """The reference's partition (include.h:181-189; host_mem.cpp:229): part k
+    of `total` items over `parts` -> (offset, count).  Used for inner nodes
+    over ranks (BASELINE configs[3]) and sites over instances."""
+    off, cnt = C.c_uint64(0), C.c_uint64(0)
+    rc = load().plfx_shard(int(total), int(parts), int(k), C.byref(off), C.byref(cnt))
+    if rc != OK:
+        raise PlfxError(rc, f"plfx_shard({total}, {parts}, {k}): the reference's split underflows")
+    return int(off.value), int(cnt.value)
+
+
+def gen_hostmem(n, dtype=np.float64, seed=20250117, wgt=True):
+    """host_mem.cpp:179-209 inputs (std::mt19937 + uniform_real_distribution,
+    x1 x 1e-12 on every 4th site, wgt = 1) with a fixed seed, generated by
+    libplfx (plfx_gen_hostmem).  Returns dict(EV, left, right, x1, x2, wgt)."""
+    dt = np.dtype(dtype)
+    out = dict(EV=np.empty(16, dt), left=np.empty(64, dt), right=np.empty(64, dt),
+               x1=np.empty(16 * n, dt), x2=np.empty(16 * n, dt),
+               wgt=np.empty(n, np.int32) if wgt else None)
+    p = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    rc = load().plfx_gen_hostmem(F32 if dt == np.float32 else F64, int(seed), int(n), p(out["EV"]),
+                                 p(out["left"]), p(out["right"]), p(out["x1"]), p(out["x2"]),
+                                 p(out["wgt"]))
+    if rc != OK:
+        raise PlfxError(rc, "plfx_gen_hostmem")
+    return out
+
+
+def swemu_instance_run(in_left, in_right, out_clv, out_scaler, alignment_sites, window_size,
+                       layout, aie_type=AIE_WINDOW):
+    """The sw_emu target (plfx.h section 5b, BASELINE configs[0]): one
+    accelerator instance emulated on the CPU as its dataflow -- movers, AIE
+    lanes, s2mm -- over the whole padded host instance buffers.  No GPU."""
+    dt = in_left.dtype
+    if dt not in (np.float32, np.float64) or in_right.dtype != dt or out_clv.dtype != dt:
+        raise PlfxError(ERR_INVALID, "instance buffers must share a float dtype")
+    for a in (in_left, in_right, out_clv, out_scaler):
+        if a is not None and not (isinstance(a, np.ndarray) and a.flags.c_contiguous):
+            raise PlfxError(ERR_INVALID, "instance buffers must be C-contiguous numpy arrays")
+    n = int(alignment_sites)
+    tb = Testbench(n, 1, window_size or 1024, layout, aie_type)
+    if in_left.size < tb.instance_elements_left() or in_right.size < tb.instance_elements_right() \
+            or out_clv.size < 16 * n or (out_scaler is not None and out_scaler.size < n):
+        raise PlfxError(ERR_INVALID, "buffers smaller than the padded instance")
+    p = lambda a: None if a is None else C.c_void_p(a.ctypes.data)  # noqa: E731
+    rc = load().plfx_swemu_instance_run(p(in_left), p(in_right), p(out_clv), p(out_scaler), n,
+                                        int(window_size), int(layout), int(aie_type),
+                                        F32 if dt == np.float32 else F64)
+    if rc != OK:
+        raise PlfxError(rc, "plfx_swemu_instance_run")
 
 
 _default_ctx = None

@@ -39,10 +39,28 @@
  * context.  `stream` arguments are hipStream_t values passed as void* (NULL =
  * the HIP null stream, as everywhere in HIP; plfx_ctx_stream() gives the
  * context's own non-blocking stream).  Device pointers must come from the same HIP
- * device as the context; CLV pointers must be 16-byte aligned.  A context
- * may be used from one host thread at a time; distinct contexts are
- * independent.  No allocation happens per call after warm-up (the host
- * entry points keep grow-only staging buffers in the context).
+ * device as the context; CLV pointers must be 16-byte aligned.  Every entry
+ * point binds the context's device for its duration and restores the
+ * caller's current device on return.  A context may be used from one host
+ * thread at a time; distinct contexts are independent.
+ *
+ * Streams and the scaler-sum workspace.  Sum-producing launches (scaler_sum
+ * outputs, plfx_scaler_sum, plfx_root_lnl) reduce across thread blocks through
+ * a small self-resetting device workspace.  The context keeps ONE workspace
+ * PER STREAM (up to PLFX_MAX_STREAMS distinct streams per context, created on
+ * a stream's first use), so launches on different streams may run
+ * concurrently; launches on one stream are ordered by the stream.  A stream's
+ * first sum-producing use must not happen inside hipStreamBeginCapture (the
+ * workspace is allocated then): issue one call on it before capturing.  A
+ * captured graph keeps the workspace of the stream it was captured on, so its
+ * replays must not overlap other work on that stream's workspace.
+ * The reduction encodes arrival counts next to the sums and needs
+ * sum_j |wgt[j]| < 2^40 per launch (the reference's own scalerIncrement is a
+ * 32-bit int); the host entry points check this, the device entry points
+ * cannot check it cheaply and leave it to the caller.
+ *
+ * No allocation happens per call after warm-up (the host entry points keep
+ * grow-only staging buffers in the context).
  */
 #ifndef PLFX_H
 #define PLFX_H
@@ -54,7 +72,8 @@
 extern "C" {
 #endif
 
-#define PLFX_VERSION 10000 /* 1.0.0 */
+#define PLFX_VERSION 10100 /* 1.1.0 */
+#define PLFX_MAX_STREAMS 64 /* distinct streams with a workspace, per context */
 
 typedef enum {
   PLFX_OK = 0,
@@ -245,6 +264,15 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
                        uint8_t *const *scalers, int64_t *scaler_sums, const void *tipvec,
                        void *stream);
 
+/* The schedule the last plfx_traverse(_tips) call on this context chose:
+ * counts[i] for i < ncounts (extra entries are not written) of
+ *   0: fused six-level passes (63 ops)   1: five-level (31)   2: four-level (15)
+ *   3: three-level passes (7 ops)        4: level pairs (3 ops)
+ *   5: ops run unfused                   6: kernel launches issued
+ * Returns the number of entries written. */
+#define PLFX_SCHED_COUNTS 7
+int plfx_traverse_schedule(const plfx_ctx *ctx, int *counts, int ncounts);
+
 /* ---- (7) root log-likelihood (extension) -- */
 /* lnL = sum_i wgt_i * log( sum_c catw[c] * sum_s freq[s] * x[i][c][s] )
  *       + (sum_{j<nsums} scaler_sums[j]) * log(2^-32)
@@ -287,6 +315,44 @@ int plfx_pack_instance(const plfx_testbench *tb, int instance, int dtype,
                        const void *EV, const void *left, const void *right,
                        const void *x1_all, const void *x2_all, void *out_left,
                        void *out_right);
+
+/* The reference's partition of `total` items over `parts` (include.h:181-189,
+ * offsets host_mem.cpp:229,290-291): n0 = ceil(total/parts), part k covers
+ * [k*n0, k*n0 + count), the last part short by n0*parts - total.  Used for
+ * sites over instances and for independent inner nodes over ranks (BASELINE
+ * configs[3]).  PLFX_ERR_INVALID where the reference's arithmetic underflows
+ * (the padding reaches a whole share, e.g. 10 items over 8 parts). */
+int plfx_shard(uint64_t total, uint32_t parts, uint32_t k, uint64_t *offset, uint64_t *count);
+
+/* The host_mem.cpp:179-209 input protocol with a fixed seed (the reference
+ * uses std::random_device): std::mt19937(seed) + uniform_real_distribution
+ * <double>(0,1): EV[16], then left[64]/right[64] interleaved, then x1/x2
+ * (16*n each) interleaved, x1 x 1e-12 on every 4th site; wgt (may be NULL)
+ * = 1.  Host arrays of `dtype`. */
+int plfx_gen_hostmem(int dtype, uint32_t seed, uint64_t n, void *EV, void *left, void *right,
+                     void *x1, void *x2, int32_t *wgt);
+
+/* ---- (5b) sw_emu: the accelerator instance emulated on the CPU ----------
+ * The reference's software-emulation target (make run TARGET=sw_emu,
+ * Makefile:199-220; host_mem.cpp:160-164; BASELINE configs[0]): one instance
+ * run as its dataflow on the host, window by window -- mm2sleft/mm2sright
+ * (hls/src/mm2s{left,right}_memDNAwindow{Comb,Sep}.cpp, stream:
+ * mm2sleft_memDNAstreamComb.cpp) split each 512-bit site word into 4 lane
+ * beats and prepend the EV half and the transposed P_c (transpose.cpp:6-24)
+ * to every window, each lane runs mmul_branch x2 -> combine -> ev
+ * (aie/src/128x9DNAwindow8192Comb/kernels/), and s2mm
+ * (hls/src/s2mm_memDNAwindowComb.cpp:45-99) reassembles the 16 values, tests
+ * and rescales them with the padding mask.  Host buffers only, no GPU, no
+ * context; in_left/in_right must hold the whole padded instance
+ * (plfx_tb_instance_elements_left/right).  Writes alignment_sites CLVs and
+ * scaler bytes (never the padding, as plfx_instance_run).  Arithmetic in
+ * plf()'s order: results are bit-identical to plfx_instance_run.  An explicit
+ * target like the reference's, never a fallback of the GPU entry points.
+ * aie_type: PLFX_AIE_WINDOW (window_size bytes, a multiple of 32) or
+ * PLFX_AIE_STREAM (COMBINED only; window_size ignored). */
+int plfx_swemu_instance_run(const void *in_left, const void *in_right, void *out_clv,
+                            uint8_t *out_scaler, uint32_t alignment_sites, uint32_t window_size,
+                            int layout, int aie_type, int dtype);
 
 /* ---- (9) model setup: P matrices and EV from branch lengths (extension,
  * SURVEY section 8f row 3; the reference's inputs are random or precomputed,

@@ -110,10 +110,43 @@ def lib():
     return _lib
 
 
+def native_lib():
+    """The restatement built on THIS machine at -O3 -march=native
+    -ffp-contract=off (oracle/Makefile `native`), for the CPU-baseline
+    variant; None when it cannot be built here."""
+    global _native
+    if _native is None:
+        import subprocess
+
+        p = ORACLE_DIR / "_native" / "liboracle_native.so"
+        try:
+            subprocess.run(["make", "-s", "-C", str(ORACLE_DIR), "native"], check=True,
+                           capture_output=True, timeout=120)
+        except (OSError, subprocess.SubprocessError):
+            _native = False
+            return None
+        L = C.CDLL(str(p))
+        for sfx, fp in (("f32", _f32p), ("f64", _f64p)):
+            f = getattr(L, f"plfo_plf_{sfx}")
+            f.argtypes = [fp, fp, fp, fp, C.c_longlong, fp, fp, C.c_void_p,
+                          C.POINTER(C.c_int), C.c_void_p]
+            f.restype = None
+            f = getattr(L, f"plfo_plf_{sfx}_omp")
+            f.argtypes = [fp, fp, fp, fp, C.c_longlong, fp, fp, C.c_void_p,
+                          C.POINTER(C.c_int), C.c_void_p, C.c_int]
+            f.restype = None
+        _native = L
+    return _native or None
+
+
+_native = None
+
+
 def ref_lib(opt: str = "O0"):
-    """The reference plf() itself (oracle/_ref), or None if it was not built."""
+    """The reference plf() itself (oracle/_ref), or None if it was not built.
+    opt: "O0" (its own host flags), "O3", "O3v4" (-O3 -march=x86-64-v4)."""
     if opt not in _refs:
-        p = REF_O0 if opt == "O0" else REF_O3
+        p = {"O0": REF_O0, "O3": REF_O3}.get(opt, ORACLE_DIR / "_ref" / f"libplfref_{opt}.so")
         if not p.exists():
             _refs[opt] = None
         else:
@@ -136,11 +169,12 @@ def _sfx(dtype):
 # --------------------------------------------------------------------------
 # plf() and friends
 # --------------------------------------------------------------------------
-def plf(x1, x2, EV, left, right, wgt=None, n=None, threads=0, out=None):
+def plf(x1, x2, EV, left, right, wgt=None, n=None, threads=0, out=None, L=None):
     """Restated plf(): returns (x3, scaler_bytes, scalerIncrement).
 
     threads > 0 uses the OpenMP variant (identical results); `out` may supply
-    preallocated (x3, scaler) arrays."""
+    preallocated (x3, scaler) arrays; L another build of the same source
+    (native_lib())."""
     dt = x1.dtype
     if n is None:
         n = x1.size // 16
@@ -150,7 +184,7 @@ def plf(x1, x2, EV, left, right, wgt=None, n=None, threads=0, out=None):
         x3 = np.empty(n * 16, dtype=dt)
         sc = np.empty(n, dtype=np.uint8)
     inc = C.c_int(0)
-    L = lib()
+    L = L or lib()
     if wgt is not None:
         wgt = np.ascontiguousarray(wgt, dtype=np.int32)
     if threads > 0:

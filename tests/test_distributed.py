@@ -1,9 +1,14 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the multi-GPU plumbing:
+"""Multi-process (world_size 2, gloo, CPU) tests of the multi-GPU path:
 bench.combine_ranks (max-over-ranks timing + the one all-reduce of scaler
-totals) and the node sharding used by the multi-node workloads."""
+totals), the partition of BASELINE configs[3]'s independent nodes over ranks
+(plfx.shard, the reference's ceil rule include.h:181-189) and the one lnL
+all-reduce (bench.reduce_node_lnls): each rank evaluates its share of real
+nodes with the oracle, and the reduced per-node lnL, job lnL and scaler totals
+equal the single-process values bit for bit."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -16,6 +21,20 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q, *args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
 
 
 def _worker(rank, world, port, q):
@@ -34,17 +53,7 @@ def _worker(rank, world, port, q):
 
 
 def test_combine_ranks_gloo_world2():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    for rank, wall, devt, ok, bad in res:
+    for rank, wall, devt, ok, bad in _spawn(_worker, 2):
         assert wall == 11.0 and devt == 10.0   # max over ranks
         assert ok is True                      # sum of got == sum of expected
         assert bad is False                    # one rank's mismatch is seen by every rank
@@ -54,6 +63,63 @@ def test_combine_ranks_single():
     import bench
 
     assert bench.combine_ranks(3.0, 2.0, torch.tensor(5), 5, torch.device("cpu"), 1) == (3.0, 2.0, True)
+
+
+# --- BASELINE configs[3] on the CPU: real nodes, the product's partition, the
+# one all-reduce, the oracle's plf() + root lnL as each rank's "GPU" ---------
+TOTAL_NODES, SITES = 11, 301
+
+
+def _node_inputs(oracle, j):
+    """Node j's inputs (global index j: identical for any rank count)."""
+    d = oracle.gen_hostmem(SITES, np.float64, 1000 + j)
+    w = ((np.arange(SITES) + j) % 3 + 1).astype(np.int32)
+    return d, w
+
+
+def _node_lnl(oracle, j):
+    d, w = _node_inputs(oracle, j)
+    x3, _, inc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], w)
+    return oracle.root_lnl(4, 4, x3, SITES, wgt=w, scaler_sums=np.array([inc])), inc
+
+
+def _nodes_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        import oracle
+        import plfx
+
+        off, cnt = plfx.shard(TOTAL_NODES, world, rank)
+        vals = [_node_lnl(oracle, j) for j in range(off, off + cnt)]
+        per, tot, ev = bench.reduce_node_lnls([v[0] for v in vals], [v[1] for v in vals], off,
+                                              TOTAL_NODES, torch.device("cpu"), world)
+        q.put((rank, off, cnt, per, tot, ev))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_nodes_partition_lnl_allreduce_equals_single_process(oracle, world):
+    """configs[3] at world 2 and 3 (gloo): ranks take the reference's ceil
+    split of the nodes, evaluate their nodes (oracle plf + root lnL), and one
+    all-reduce gives every rank the per-node lnL vector, the job lnL and the
+    scaler totals of the single-process run -- bit for bit (so well inside the
+    1e-12 relative bound)."""
+    import bench
+
+    single = [_node_lnl(oracle, j) for j in range(TOTAL_NODES)]
+    exp_per, exp_tot, exp_ev = bench.reduce_node_lnls([v[0] for v in single], [v[1] for v in single],
+                                                      0, TOTAL_NODES, torch.device("cpu"), 1)
+    assert exp_ev == sum(v[1] for v in single) > 0
+    res = _spawn(_nodes_worker, world)
+    covered = sorted((off, cnt) for _, off, cnt, *_ in res)
+    assert sum(c for _, c in covered) == TOTAL_NODES and covered[0][0] == 0
+    for rank, off, cnt, per, tot, ev in res:
+        assert np.array_equal(per, exp_per)
+        assert tot == exp_tot and ev == exp_ev
+        assert abs(tot - exp_tot) <= 1e-12 * abs(exp_tot)
 
 
 def _tree_worker(rank, world, port, q):
@@ -66,7 +132,7 @@ def _tree_worker(rank, world, port, q):
 
         wl = types.SimpleNamespace(lnl=torch.tensor([-(rank + 1) * 100.5], dtype=torch.float64),
                                    sums=torch.tensor([rank, 2], dtype=torch.int64), n=1000)
-        q.put((rank, bench.Tree64Workload.post(wl, world, torch.device("cpu"))))
+        q.put((rank, bench.Tree64Workload.post(wl, world, rank, torch.device("cpu"))))
     finally:
         dist.destroy_process_group()
 
@@ -74,17 +140,7 @@ def _tree_worker(rank, world, port, q):
 def test_tree64_site_shards_lnl_allreduce_gloo_world2():
     """tree64 at N GPUs: every rank sweeps the tree over its own block of sites;
     the tree lnL and scaler totals are summed over ranks by one all-reduce."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_tree_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted((q.get(timeout=120) for _ in procs), key=lambda t: t[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    for rank, out in res:
+    for rank, out in _spawn(_tree_worker, 2):
         assert out["root_lnl_rank0"] == -(rank + 1) * 100.5
         assert out["tree_lnl_all_ranks"] == -301.5
         assert out["scaler_events_all_ranks"] == 5

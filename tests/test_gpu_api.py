@@ -1,0 +1,177 @@
+"""GPU tests of the C ABI's concurrency and capture rules (plfx.h "Streams and
+the scaler-sum workspace") and of the configurations the bench times at their
+benchmarked sizes: protein FMA at 2^18 sites (BASELINE configs[4]) and 64
+batched nodes x 2^20 sites (configs[3]'s per-GPU shard).  Bar: CLVs, scaler
+bytes and sums bit-exact against the oracle; protein FMA also within 1e-12
+(relative to the site's largest value) of the unfused loop."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    a = np.asarray(a)
+    return a.view(np.uint32 if a.dtype == np.float32 else np.uint64)
+
+
+def dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def test_sums_on_two_streams_concurrently(ctx, oracle):
+    """Sum-producing launches in flight on two streams of ONE context at the
+    same time (each stream has its own reduction workspace): every sum exact,
+    the CLVs bit-exact.  Also the root lnL on both streams."""
+    import torch
+
+    n = 1 << 20
+    d = oracle.gen_hostmem(n, np.float64, 41)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right")}
+    ws = [dev(np.full(n, i + 1, np.int32)) for i in range(2)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.empty_like(t["x1"]) for _ in range(2)]
+    sums = torch.zeros(2, 8, dtype=torch.int64, device="cuda")
+    lnl = torch.zeros(2, 8, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    for r in range(8):  # interleaved issue: both streams' kernels overlap on the device
+        for i, s in enumerate(streams):
+            ctx.plf_dev(t["x1"], t["x2"], outs[i], t["EV"], t["left"], t["right"], ws[i], None,
+                        sums[i, r:r + 1], stream=s)
+            ctx.root_lnl(outs[i], n, lnl[i, r:r + 1], wgt=ws[i], scaler_sums=sums[i, r:r + 1],
+                         stream=s)
+    torch.cuda.synchronize()
+    n_sc = n // 4
+    assert sums[0].tolist() == [n_sc] * 8 and sums[1].tolist() == [2 * n_sc] * 8
+    e3, _, _ = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], threads=16)
+    for o in outs:
+        assert np.array_equal(bits(o.cpu().numpy()), bits(e3))
+    l0 = oracle.root_lnl(4, 4, e3, n, wgt=np.ones(n, np.int32), scaler_sums=np.array([n_sc]))
+    got = lnl.cpu().numpy()
+    assert np.all(np.abs(got[0] - l0) <= 1e-12 * abs(l0))
+    assert np.all(got[0] == got[0][0]) and np.all(got[1] == got[1][0])  # deterministic
+
+
+def test_graph_capture_needs_a_warm_stream(ctx, oracle):
+    """A stream's first sum-producing call may not be inside a capture (its
+    workspace is allocated then): rejected with PlfxError.  After one call the
+    stream captures, and replays produce exact sums."""
+    import plfx
+    import torch
+
+    n = 70001
+    d = oracle.gen_hostmem(n, np.float64, 43)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    o3 = torch.empty_like(t["x1"])
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cold = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(plfx.PlfxError):
+        with torch.cuda.graph(g, stream=cold):
+            ctx.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s,
+                        stream=cold)
+    warm = torch.cuda.Stream()
+    ctx.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s, stream=warm)
+    torch.cuda.synchronize()
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2, stream=warm):
+        for _ in range(3):
+            ctx.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s,
+                        stream=warm)
+    s.zero_()
+    o3.zero_()
+    torch.cuda.synchronize()
+    for _ in range(4):
+        g2.replay()
+    torch.cuda.synchronize()
+    e3, _, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+    assert int(s.item()) == einc
+    assert np.array_equal(bits(o3.cpu().numpy()), bits(e3))
+
+
+def test_context_keeps_callers_device(ctx):
+    """Entry points bind the context's device and give the caller's current
+    device back (one visible GPU: the current device stays 0 across calls)."""
+    import plfx
+    import torch
+
+    before = torch.cuda.current_device()
+    with plfx.Context(0) as c:
+        x = torch.zeros(16 * 64, dtype=torch.float64, device="cuda")
+        c.plf_dev(x, x.clone(), torch.empty_like(x), x[:16], x[:64], x[:64])
+        torch.cuda.synchronize()
+    assert torch.cuda.current_device() == before
+
+
+def test_protein_fma_full_size_256k(ctx, oracle):
+    """BASELINE configs[4] in the mode the bench times (FMA, f64 matrix cores)
+    at its size, 2^18 sites: bit-exact against the oracle's fma() restatement,
+    within 1e-12 of the unfused loop, identical scaler decisions."""
+    import torch
+
+    S, CAT, n = 20, 4, 1 << 18
+    V = S * CAT
+    rng = np.random.default_rng(2026)
+    x1 = rng.random(V * n)
+    x1.reshape(n, V)[0::4] *= 1e-14
+    x2 = rng.random(V * n)
+    left, right = rng.random(CAT * S * S), rng.random(CAT * S * S)
+    EV = rng.random(S * S) - 0.25
+    w = rng.integers(0, 4, n).astype(np.int32)
+    t = [dev(a) for a in (x1, x2, EV, left, right, w)]
+    x3 = torch.empty(V * n, dtype=torch.float64, device="cuda")
+    sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    ctx.plf_dev_gen(t[0], t[1], x3, t[2], t[3], t[4], S, t[5], sc, s, n=n, fma=True)
+    torch.cuda.synchronize()
+    got, gsc = x3.cpu().numpy(), sc.cpu().numpy()
+    f3, fsc, finc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
+    assert np.array_equal(bits(got), bits(f3))
+    assert np.array_equal(gsc, fsc) and int(s.item()) == finc
+    e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w)
+    assert np.array_equal(gsc, esc) and finc == einc
+    scale = np.abs(e3).reshape(n, V).max(axis=1, keepdims=True)
+    assert (np.abs(got - e3).reshape(n, V) / scale).max() <= 1e-12
+
+
+def test_nodes64_full_size_windows(ctx, oracle):
+    """configs[3]'s per-GPU shard as the bench times it: 64 independent nodes
+    x 2^20 f64 sites in two 32-node batched launches.  A 4096-site window of
+    every node is checked bit for bit against the oracle on that window, and
+    every node's scaler sum equals the sum of its scaler bytes (full size)."""
+    import torch
+
+    n, nn = 1 << 20, 64
+    g = torch.Generator(device="cuda")
+    g.manual_seed(64)
+    EV = torch.rand(16, dtype=torch.float64, device="cuda", generator=g)
+    wgt = torch.randint(0, 4, (n,), dtype=torch.int32, device="cuda", generator=g)
+    sums = torch.full((nn,), -1, dtype=torch.int64, device="cuda")
+    nodes = []
+    for j in range(nn):
+        x1 = torch.rand(16 * n, dtype=torch.float64, device="cuda", generator=g)
+        x1.view(-1, 16)[j % 4::4] *= 1e-12
+        nodes.append(dict(x1=x1, x2=torch.rand(16 * n, dtype=torch.float64, device="cuda", generator=g),
+                          x3=torch.empty(16 * n, dtype=torch.float64, device="cuda"),
+                          left=torch.rand(64, dtype=torch.float64, device="cuda", generator=g),
+                          right=torch.rand(64, dtype=torch.float64, device="cuda", generator=g),
+                          scaler=torch.empty(n, dtype=torch.uint8, device="cuda"),
+                          scaler_sum=sums[j:j + 1]))
+    ctx.plf_batch_dev(nodes[:32], EV, n, wgt)
+    ctx.plf_batch_dev(nodes[32:], EV, n, wgt)
+    torch.cuda.synchronize()
+    h = lambda x: x.cpu().numpy()  # noqa: E731
+    for j, nd in enumerate(nodes):
+        lo = (j * 12289) % (n - 4096)
+        sl = slice(16 * lo, 16 * (lo + 4096))
+        e3, esc, einc = oracle.plf(h(nd["x1"][sl]), h(nd["x2"][sl]), h(EV), h(nd["left"]),
+                                   h(nd["right"]), h(wgt[lo:lo + 4096]))
+        assert np.array_equal(bits(h(nd["x3"][sl])), bits(e3)), j
+        assert np.array_equal(h(nd["scaler"][lo:lo + 4096]), esc), j
+        full = int((nd["scaler"].to(torch.int64) * wgt.to(torch.int64)).sum().item())
+        assert int(sums[j].item()) == full, j
+        assert int(nd["scaler"].sum().item()) >= n // 4
+    del nodes
+    torch.cuda.empty_cache()

@@ -1,0 +1,104 @@
+"""GPU tests of BASELINE configs[3] end to end through bench.py: 512-node
+style workloads split over ranks with the reference's ceil rule, the real HIP
+kernels, the per-node root lnL and the ONE all-reduce.  On the one-GPU box the
+ranks share the device: 2 ranks over gloo, and 1 rank under
+torch.distributed.run over RCCL (the nccl backend), so the RCCL collective is
+exercised on hardware.  The all-reduced lnL of N ranks must equal the
+1-rank value bit for bit (the reduction is exact by construction,
+bench.reduce_node_lnls) and the oracle's lnL of the same nodes within 1e-12."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+NODES, SITES = 12, 4099
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(nproc, backend, *extra):
+    args = ["--gpus", str(nproc), "--workload", "nodes512", "--nodes", str(NODES), "--sites",
+            str(SITES), "--steps", "3", "--warmup", "1", "--no-cpu-baseline", *extra]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"), *args]
+    env = {**os.environ, "PLFX_DIST_BACKEND": backend, "OMP_NUM_THREADS": "4"}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def _oracle_lnls(oracle):
+    """The same nodes (bench.NodesWorkload: node j from a generator seeded
+    SEED + 1 + j) evaluated by the oracle: plf() then root lnL."""
+    import torch
+
+    import bench
+    import plfx
+
+    a = bench.parse(["--workload", "nodes512", "--nodes", str(NODES), "--sites", str(SITES)])
+    dev = torch.device("cuda", 0)
+    with plfx.Context(0) as ctx:
+        wl = bench.NodesWorkload(ctx, a, dev, None, torch.float64, 8, 1, 0)
+        EV = wl.EV.cpu().numpy()
+        out = []
+        for nd in wl.nodes:
+            h = {k: nd[k].cpu().numpy() for k in ("x1", "x2", "left", "right")}
+            x3, _, inc = oracle.plf(h["x1"], h["x2"], EV, h["left"], h["right"])
+            out.append((oracle.root_lnl(4, 4, x3, SITES, scaler_sums=np.array([inc])), inc))
+        del wl
+    return out
+
+
+def test_nodes_two_ranks_gloo_equal_one_rank_rccl(oracle):
+    """2 ranks (gloo) and 1 rank (RCCL under torch.distributed.run) on the
+    same 12 nodes: identical job lnL and scaler totals, equal to the oracle."""
+    one = _bench(1, "nccl")
+    two = _bench(2, "gloo")
+    assert one["config"]["distributed"] == "nccl" and two["config"]["distributed"] == "gloo"
+    assert one["check"] == two["check"] == "ok"
+    assert one["scaling"] == "strong" and one["config"]["nodes_in_job"] == NODES
+    k = "lnl_all_nodes_all_ranks"
+    assert one[k] == two[k]                                   # bit for bit
+    assert one["scaler_events_all_ranks"] == two["scaler_events_all_ranks"] == NODES * ((SITES + 3) // 4)
+    assert one["config"]["lnl_rank_nodes"] == [0, NODES]
+    exp = _oracle_lnls(oracle)
+    tot = sum(v[0] for v in exp)
+    assert abs(one[k] - tot) <= 1e-12 * abs(tot)
+    assert sum(v[1] for v in exp) == one["scaler_events_all_ranks"]
+    assert np.allclose(one["config"]["lnl_first_nodes"], [v[0] for v in exp[:4]], rtol=1e-12, atol=0)
+
+
+def test_nodes_three_ranks_ragged_split():
+    """12 nodes over 3 ranks (4 each) and the default node workload at 2
+    ranks: the one all-reduce carries every rank's values (gloo on one GPU)."""
+    three = _bench(3, "gloo")
+    one = _bench(1, "gloo")
+    assert three["lnl_all_nodes_all_ranks"] == one["lnl_all_nodes_all_ranks"]
+    assert three["scaler_events_all_ranks"] == one["scaler_events_all_ranks"]
+    port = _port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "2",
+           "--sites", "65536", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--buffer-sets", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT),
+                       env={**os.environ, "PLFX_DIST_BACKEND": "gloo", "OMP_NUM_THREADS": "4"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert d["n_gpus"] == 2 and len(d["config"]["lnl_per_rank"]) == 2
+    assert d["config"]["lnl_all_ranks"] == sum(d["config"]["lnl_per_rank"])
+    assert d["config"]["scaler_events_all_ranks"] == 2 * (65536 // 4)

@@ -339,6 +339,9 @@ def test_host_driver_end_to_end(oracle, tmp_path):
             assert np.array_equal(bits(got), bits(e3))
             assert np.array_equal(sc, esc) and inc == einc
         assert "GPU PLF kernel" in r.stdout
+        # the driver's own check (host_mem.cpp:403-442): CPU plf() vs the GPU, exact
+        assert "Test result: Passed" in r.stdout
+        assert "Reference (CPU plf" in r.stdout and "Speed up (excluding transfers)" in r.stdout
 
 
 def test_dropin_header_reference_call(tmp_path):

@@ -156,6 +156,8 @@ def test_tree64_full_size_window(ctx, oracle):
     sums = torch.zeros(ops.shape[0], dtype=torch.int64, device="cuda")
     scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(ops.shape[0])]
     ctx.traverse(ops, clv, pm, EV, n, None, scal, sums)
+    sched = ctx.last_schedule()
+    assert sched["deep6"] == 1 and sched["launches"] == 1, sched  # PLFX_FUSE=3 default
     out = torch.zeros(1, dtype=torch.float64, device="cuda")
     ctx.root_lnl(clv[-1], n, out, scaler_sums=sums)
     torch.cuda.synchronize()
@@ -317,18 +319,25 @@ def test_six_level_pass_tiny_alignments(oracle, n, dtype, monkeypatch):
     c = plfx.Context(0)
     try:
         tt = torch.float64 if dtype == np.float64 else torch.float32
-        clv = [dev(d) for d in dense] + [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nslots - ntax)]
+        # oversized buffers with sentinels past n: a tail write would land there
+        big = [torch.full((16 * (n + 24),), -1.0, dtype=tt, device="cuda") for _ in range(nslots - ntax)]
+        clv = [dev(d) for d in dense] + [b[:16 * n] for b in big]
         sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
-        scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
-        c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums)
+        sbig = [torch.full((n + 24,), 7, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+        c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), [x[:n] for x in sbig], sums)
         torch.cuda.synchronize()
+        sched = c.last_schedule()
     finally:
         c.close()
+    assert sched["deep6"] == 1 and sched["launches"] == 1, sched   # the 63-node pass ran
     for s_ in range(ntax, nslots):
         assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
+        assert (big[s_ - ntax][16 * n:].cpu().numpy() == -1.0).all(), s_
     assert np.array_equal(sums.cpu().numpy(), esums)
     for j in range(nops):
-        assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+        got = sbig[j].cpu().numpy()
+        assert np.array_equal(got[:n], escal[j]), j
+        assert (got[n:] == 7).all(), j
 
 
 def _balanced_ops(tips, slot, pmat):
@@ -390,8 +399,13 @@ def test_fused_depth4_depth5_subtrees(oracle, tipmode, dtype, monkeypatch):
         scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
         c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips)
         torch.cuda.synchronize()
+        sched = c.last_schedule()
     finally:
         c.close()
+    if tipmode == "dense":  # the 16-taxon subtree one depth-4 pass, the 32-taxon one depth-5
+        assert sched["deep5"] == 1 and sched["deep4"] == 1, sched
+    else:  # the coded half keeps three-level passes; the dense 16-taxon parts run depth-4
+        assert sched["deep5"] == 0 and sched["deep4"] >= 1 and sched["septets"] >= 1, sched
     for s_ in range(ntax, nslots):
         assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
     assert np.array_equal(sums.cpu().numpy(), esums)
@@ -590,12 +604,13 @@ def _signed_zero_field(rng, size, dtype, neg=True):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-@pytest.mark.parametrize("fuse", ["0", "1", "2"])
+@pytest.mark.parametrize("fuse", ["0", "1", "2", "3"])
 def test_signed_zero_inputs_bitexact(ctx, oracle, dtype, fuse, monkeypatch):
     """The kernels start ump chains at the first product (plf_dna.hpp,
     site_cat); on inputs full of +-0.0, negative matrix entries and underflow,
     the node kernel and every traversal schedule (one launch per level, fused
-    level pairs, fused three-level subtrees) still equal the oracle's plf()
+    level pairs, fused three-level subtrees, the depth-4 deep pass that
+    PLFX_FUSE=3 takes for a 16-taxon tree) still equal the oracle's plf()
     order bit for bit."""
     import plfx
     import torch
@@ -629,6 +644,11 @@ def test_signed_zero_inputs_bitexact(ctx, oracle, dtype, fuse, monkeypatch):
         scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
         c2.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums)
         torch.cuda.synchronize()
+        sched = c2.last_schedule()
+        if fuse == "3":
+            assert sched["deep4"] == 1 and sched["launches"] == 1, sched
+        elif fuse == "0":
+            assert sched["unfused"] == nops, sched
         for j in range(16, 16 + nops):
             assert np.array_equal(bits(clv[j].cpu().numpy()), bits(host[j])), j
         assert np.array_equal(sums.cpu().numpy(), esums)
