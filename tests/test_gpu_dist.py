@@ -73,15 +73,16 @@ def test_nodes_two_ranks_gloo_equal_one_rank_rccl(oracle):
     assert one["config"]["distributed"] == "nccl" and two["config"]["distributed"] == "gloo"
     assert one["check"] == two["check"] == "ok"
     assert one["scaling"] == "strong" and one["config"]["nodes_in_job"] == NODES
+    c1, c2 = one["config"], two["config"]
     k = "lnl_all_nodes_all_ranks"
-    assert one[k] == two[k]                                   # bit for bit
-    assert one["scaler_events_all_ranks"] == two["scaler_events_all_ranks"] == NODES * ((SITES + 3) // 4)
-    assert one["config"]["lnl_rank_nodes"] == [0, NODES]
+    assert c1[k] == c2[k]                                     # bit for bit
+    assert c1["scaler_events_all_ranks"] == c2["scaler_events_all_ranks"] == NODES * ((SITES + 3) // 4)
+    assert c1["lnl_rank_nodes"] == [0, NODES] and c2["lnl_rank_nodes"] == [0, NODES // 2]
     exp = _oracle_lnls(oracle)
     tot = sum(v[0] for v in exp)
-    assert abs(one[k] - tot) <= 1e-12 * abs(tot)
-    assert sum(v[1] for v in exp) == one["scaler_events_all_ranks"]
-    assert np.allclose(one["config"]["lnl_first_nodes"], [v[0] for v in exp[:4]], rtol=1e-12, atol=0)
+    assert abs(c1[k] - tot) <= 1e-12 * abs(tot)
+    assert sum(v[1] for v in exp) == c1["scaler_events_all_ranks"]
+    assert np.allclose(c1["lnl_first_nodes"], [v[0] for v in exp[:4]], rtol=1e-12, atol=0)
 
 
 def test_nodes_three_ranks_ragged_split():
@@ -89,8 +90,8 @@ def test_nodes_three_ranks_ragged_split():
     ranks: the one all-reduce carries every rank's values (gloo on one GPU)."""
     three = _bench(3, "gloo")
     one = _bench(1, "gloo")
-    assert three["lnl_all_nodes_all_ranks"] == one["lnl_all_nodes_all_ranks"]
-    assert three["scaler_events_all_ranks"] == one["scaler_events_all_ranks"]
+    assert three["config"]["lnl_all_nodes_all_ranks"] == one["config"]["lnl_all_nodes_all_ranks"]
+    assert three["config"]["scaler_events_all_ranks"] == one["config"]["scaler_events_all_ranks"]
     port = _port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "2",
