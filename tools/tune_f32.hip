@@ -148,12 +148,18 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
                          s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
   }
-  ADD("csrc cat U=4", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 1)
-  ADD("csrc cat U=3", (&plf_dna_kernel<float, 3, true, true, 1>), 192, 1)
-  ADD("csrc cat U=4 minw4", (&plf_dna_kernel<float, 4, true, true, 4>), 256, 1)
-  ADD("csrc cat U=3 minw4", (&plf_dna_kernel<float, 3, true, true, 4>), 192, 1)
-  ADD("csrc cat U=2 x1.25", (&plf_dna_kernel<float, 2, true, true, 1>), 128, 1.25)
-  ADD("csrc cat U=4 x1.333", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 1.3334)
+  // grids: the product sizes the grid to the co-resident blocks; at 2^20 sites
+  // U=4 at 3 blocks/CU leaves 16384 wave-trips over 3072 waves = 5.33 trips
+  // (a 6th trip for a third of the waves).  Balanced alternatives:
+  ADD("csrc cat U=4 (product)", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 1)
+  ADD("csrc cat U=4 grid 2/CU (8 trips)", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 0.6667)
+  ADD("csrc cat U=2 grid 4/CU (8 trips)", (&plf_dna_kernel<float, 2, true, true, 1>), 128, 1)
+  ADD("csrc cat U=2 grid 2/CU (16 trips)", (&plf_dna_kernel<float, 2, true, true, 1>), 128, 0.5)
+  ADD("csrc cat U=4 minw4 grid 4/CU (4 trips)", (&plf_dna_kernel<float, 4, true, true, 4>), 256, 1)
+  ADD("csrc cat U=1 grid 8/CU", (&plf_dna_kernel<float, 1, true, true, 1>), 64, 1)
+  ADD("csrc cat U=3 (product grid)", (&plf_dna_kernel<float, 3, true, true, 1>), 192, 1)
+  ADD("pipelined U=2 grid 4/CU", (&cat_pf<2, 1>), 128, 1)
+  ADD("pipelined U=4", (&cat_pf<4, 1>), 256, 1)
   {
     const size_t bytes = n * 64;
     std::vector<char> ref(bytes), got(bytes), rsc(n), gsc(n);
