@@ -48,6 +48,7 @@ constexpr int kGridMul64 = 1, kGridMul32 = 1;
 constexpr bool kNt = true;   // f32: NT CLV loads (74.8% vs 70.2% of HBM peak, r01_tune_f32.log)
 constexpr bool kNtl64 = true;
 constexpr int kMinWaves = 1;
+constexpr int kBlocksPerCu32 = 2;  // f32 node kernel grid (launch_cat)
 constexpr int kTripleU = 1;  // fused level pairs: 16 sites per trip (tools/tune_triple.hip)
 constexpr int kTripleUTips = 2;  // with coded tips: 32 sites per trip (+13-19 % for 2 tip
                                  // children, equal for 1; profiles/r01_ab_fused_tips.log)
@@ -87,12 +88,27 @@ int64_t grid_x(const void *kernel, int &cache, int grid_mul, int64_t n, int site
   return blocks < 1 ? 1 : blocks;
 }
 
+int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus < 1) cus = 256;
+  }
+  return cus;
+}
+
 template <typename T, bool kSum>
 hipError_t launch_cat(const DnaArgs &a, int max_blocks, hipStream_t s) {
   static int cache = 0;
   auto kernel = &dev::plf_dna_kernel<T, kU32, kSum, kNt, kMinWaves>;
+  // 2 blocks per CU rather than the 3 co-resident ones: at 2^20 sites U = 4
+  // leaves 5.33 trips per wave at 3/CU (a sixth trip for a third of the waves)
+  // and exactly 8 at 2/CU -- 35.4 vs 35.8 us, and 68.4 vs 69.2 us at 2^21
+  // (tools/ab_defer.hip, tools/tune_f32.hip; profiles/r02_tune_f32.log)
   const int64_t gx = grid_x((const void *)kernel, cache, kGridMul32, a.n, kWavesPerBlock * 16 * kU32,
-                            1, max_blocks);
+                            1, max_blocks > 0 ? max_blocks : kBlocksPerCu32 * cu_count());
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
                      (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,
                      (const T *)a.right, a.wgt, a.scaler, a.n, a.ws, a.scaler_sum);

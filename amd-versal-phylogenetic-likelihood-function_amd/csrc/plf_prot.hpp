@@ -526,10 +526,27 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
 // k-ordered fma chain (tools/probes/mfma_f64_4x4x4_numerics.hip).
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
+// Exchange the upper 16-lane row of each 32-lane half of v (lanes 16-31,
+// 48-63) with the lower row of w (lanes 0-15, 32-47), per 64-bit value
+// (v_permlane16_swap, gfx950).
+__device__ __forceinline__ void swap_rows16(double &v, double &w) {
+  const long long a = __builtin_bit_cast(long long, v), b = __builtin_bit_cast(long long, w);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)a, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(a >> 32), (unsigned)(b >> 32), false,
+                                                   false);
+  v = __builtin_bit_cast(double, ((long long)hi[0] << 32) | (unsigned)lo[0]);
+  w = __builtin_bit_cast(double, ((long long)hi[1] << 32) | (unsigned)lo[1]);
+}
+
 // kAblate (tuning only, tools/tune_prot.hip): 0 = the kernel; 1 = no matrix-core
 // work (VALU stand-ins keep the LDS reads); 2 = no HBM loads or stores.
+// kSwapX3: the back-transform's results go to the LDS tile as 16-B pairs
+// (l, l+1) after two row swaps (swap_rows16), 3 ds_write_b128 per lane and
+// sub-tile, conflict-free, instead of 5 ds_write_b64 (2-way bank conflicts:
+// sites lo16 and lo16+8 share banks at the 82-double row stride).
+// kEarly: the first child tile's loads go out before the matrix fragments'.
 template <bool kSum, int kMinWaves = 2, bool kPrefetch = true, int kAblate = 0, bool kMix4 = true,
-          int kTips = 0>
+          int kTips = 0, bool kSwapX3 = false, bool kEarly = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                      double *__restrict__ x3, const double *__restrict__ EV,
@@ -546,6 +563,14 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lo16 = lane & 15, g = lane >> 4;
+  // kPrefetch: the next child tile's loads are in flight while the current
+  // one is multiplied (x2 during phase 1, the next trip's x1 during phase 2)
+  f64x2 pf[PT::kChunks / kBlock];
+  const int64_t stride = (int64_t)gridDim.x * 64;
+  if constexpr (kAblate == 2)
+    for (auto &q : pf) q = f64x2{1.0, 1.0};
+  if constexpr (kEarly && kPrefetch && kAblate != 2 && !T2)  // the first dense child's first tile
+    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
   // A fragments: [mt][s] -> lane holds M[row = 16mt + lo16][col = 4s + g]
   // (kMix4: [1][s] -> M[row = 16 + lane%4][col = 4s + g], the 4x4x4_4b form)
   double AL[2][5], AR[2][5], AE[2][5];
@@ -574,13 +599,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   const double *td = reinterpret_cast<const double *>(tile);
   double *tw = reinterpret_cast<double *>(tile);
   long long acc = 0;
-  // kPrefetch: the next child tile's loads are in flight while the current
-  // one is multiplied (x2 during phase 1, the next trip's x1 during phase 2)
-  f64x2 pf[PT::kChunks / kBlock];
-  const int64_t stride = (int64_t)gridDim.x * 64;
-  if constexpr (kAblate == 2)
-    for (auto &q : pf) q = f64x2{1.0, 1.0};
-  if constexpr (kPrefetch && kAblate != 2 && !T2)  // the first dense child's first tile
+  if constexpr (!kEarly && kPrefetch && kAblate != 2 && !T2)  // the first dense child's first tile
     if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
   for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
     f64x4 P[4][2];  // per sub-tile: U_L^T, then p = U_L^T * U_R^T
@@ -675,9 +694,26 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       // site lo16 of sub-tile t is small in category c iff its 4 lanes agree
       mine |= (b & (b >> 16) & (b >> 32) & (b >> 48) & 0xFFFFull) << (16 * t);
       double *w = tw + (16 * t + lo16) * kRow + c * S;
+      if constexpr (kSwapX3) {
+        // lane of row g holds l = g + 4r (X0[r]) and 16 + g (X1).  After
+        // swap_rows16(X0[1], X0[0]) a lane of an even row holds (g+4, g+5),
+        // of an odd row (g-1, g); after swap_rows16(X0[3], X0[2]) (g+12, g+13)
+        // resp. (g+7, g+8); after swap_rows16(X1, copy) even rows hold
+        // (16+g, 17+g).  b128 groups of 8 lanes: row stride 164 dwords = 4
+        // banks, so 8 sites x 4 dwords cover the 32 banks once.
+        double a0 = X0[0], a1 = X0[1], a2 = X0[2], a3 = X0[3], b0 = X1[0], b1 = X1[0];
+        swap_rows16(a1, a0);
+        swap_rows16(a3, a2);
+        swap_rows16(b0, b1);
+        const bool odd = g & 1;
+        *reinterpret_cast<f64x2 *>(w + (odd ? g - 1 : g + 4)) = f64x2{a1, a0};
+        *reinterpret_cast<f64x2 *>(w + (odd ? g + 7 : g + 12)) = f64x2{a3, a2};
+        if (!odd) *reinterpret_cast<f64x2 *>(w + 16 + g) = f64x2{b0, b1};
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; r++) w[g + 4 * r] = X0[r];
-      w[16 + g] = X1[0];
+        for (int r = 0; r < 4; r++) w[g + 4 * r] = X0[r];
+        w[16 + g] = X1[0];
+      }
     }
     if (lane == 0) small_mask[c] = mine;
     __syncthreads();

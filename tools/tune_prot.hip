@@ -172,6 +172,11 @@ int main(int argc, char **argv) {
   ADD_K11("mfma probe: ring traffic only", (&probe_tiles<0>), 64)
   ADD_K11("mfma probe: ring traffic + LDS + barriers", (&probe_tiles<1>), 64)
   ADD_K11("mfma ring minw=1", (&plf_prot_mfma_ring_kernel<true, 1>), 64)
+  // round 2: X3 written as conflict-free b128 pairs after permlane16 row
+  // swaps (kSwapX3), the first tile's loads before the matrix fragments (kEarly)
+  ADD_K("mfma v2 swapX3", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, true, false>), 64)
+  ADD_K("mfma v2 early", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, false, true>), 64)
+  ADD_K("mfma v2 swapX3+early", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, true, true>), 64)
 
   // FMA-mode reference for the mfma variants
   std::vector<uint64_t> h_fref(n * 80);
