@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-2 measurement session (GPU box, via gpurun from the repo root): the GPU
+# tests, then bench + rocprofv3 trace + PMC traffic for each BASELINE config
+# the bench times (tools/gpu_r02_measure.sh).  Stops at the first failure.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+T=${1:-r02m}
+cd $R
+mkdir -p gpurun_out/$T
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/$T/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/$T/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/$T/pytest_gpu.log
+KERNEL=plf_dna_f64_pair_kernel bash tools/gpu_r02_measure.sh $T/node 40 || exit 1
+KERNEL=plf_dna_kernel DTYPE=f32 bash tools/gpu_r02_measure.sh $T/node_f32 40 --dtype f32 || exit 1
+bash tools/gpu_r02_measure.sh $T/protein 20 --workload protein --steps 100 --warmup 5 || exit 1
+bash tools/gpu_r02_measure.sh $T/tree64 20 --workload tree64 --steps 50 --warmup 5 || exit 1
+EXTRA_STEPS=1 bash tools/gpu_r02_measure.sh $T/nodes512 2 --workload nodes512 --steps 10 --warmup 2 || exit 1

@@ -35,7 +35,7 @@ if [ -n "${KERNEL:-}" ]; then
   python3 $R/tools/pmc_traffic.py $FCSV $WCSV $OUT/pmc_traffic.json --sites ${SITES:-1048576} --dtype ${DTYPE:-f64} --kernel $KERNEL > /dev/null
   python3 -c "import json; d=json.load(open('$OUT/pmc_traffic.json')); print('traffic', d['hbm_bytes_per_launch'], d['traffic_over_algorithmic'])"
 else
-  python3 $R/tools/pmc_step.py $FCSV $WCSV $OUT/pmc_traffic.json --steps $((P + 2)) --alg-bytes $ALG --key $KEY --exclude root_lnl > /dev/null
+  python3 $R/tools/pmc_step.py $FCSV $WCSV $OUT/pmc_traffic.json --steps $((P + 2 + ${EXTRA_STEPS:-0})) --alg-bytes $ALG --key $KEY --exclude root_lnl > /dev/null
   python3 -c "import json; d=json.load(open('$OUT/pmc_traffic.json')); print('traffic', d['hbm_bytes_per_step'], d['traffic_over_algorithmic'])"
 fi
 find $OUT/trace -name "*kernel_stats.csv" -exec head -5 {} \;
