@@ -191,7 +191,10 @@ template <bool kSum, int kTips>
 hipError_t launch_prot_mfma_t(const DnaArgs &a, int max_blocks, hipStream_t s,
                               const double *tipvec) {
   static int cache = 0;
-  auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, true, 0, true, kTips, false, true>;
+  // X3 to LDS through permuted back-transform rows (kX3 = 2: conflict-free
+  // b128 writes; 90.2 vs 91.2 us at 2^18, 342 vs 345 at 2^20, tools/tune_prot.hip,
+  // profiles/r02_tune_protein_v3.log); first tile's loads before the matrix fragments
+  auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, true, 0, true, kTips, 2, true>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV,

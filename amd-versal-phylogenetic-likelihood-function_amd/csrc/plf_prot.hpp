@@ -540,13 +540,27 @@ __device__ __forceinline__ void swap_rows16(double &v, double &w) {
 
 // kAblate (tuning only, tools/tune_prot.hip): 0 = the kernel; 1 = no matrix-core
 // work (VALU stand-ins keep the LDS reads); 2 = no HBM loads or stores.
-// kSwapX3: the back-transform's results go to the LDS tile as 16-B pairs
-// (l, l+1) after two row swaps (swap_rows16), 3 ds_write_b128 per lane and
-// sub-tile, conflict-free, instead of 5 ds_write_b64 (2-way bank conflicts:
-// sites lo16 and lo16+8 share banks at the 82-double row stride).
+// kX3 = how the back-transform's results reach the LDS tile: 0 = five
+// ds_write_b64 per lane and sub-tile (2-way bank conflicts: sites lo16 and
+// lo16+8 share banks at the 82-double row stride); 1 = 16-B pairs (l, l+1)
+// after row swaps (swap_rows16), 3 ds_write_b128, conflict-free; 2 = the
+// back-transform's A rows permuted (row g + 4r computes state 4g + r) so a
+// lane's four 16x16x4 results are four consecutive states: 2 conflict-free
+// ds_write_b128 + 1 ds_write_b64, no lane movement (bit-identical: a row
+// permutation of the A operand permutes the outputs, nothing else).
 // kEarly: the first child tile's loads go out before the matrix fragments'.
+// kFirstX2 (dense children): the first trip's x2 tile is fetched at kernel
+// start too, instead of after the first x1 tile has landed (one HBM latency
+// less in the start-up; the first trip is peeled so the extra registers are
+// not live in the loop).
+// kSplitB: the B-fragment reads stay separate ds_read_b64 (banks (a/4) mod 64,
+// 2 x 32 lanes: conflict-free at the 164-dword row stride); left alone the
+// compiler pairs the k-steps 32 B apart into ds_read2_b64, which banks mod 32
+// in 16-lane groups (sites lo16 and lo16+8 collide: 2-way) and takes 8 LDS
+// cycles instead of 2 x 2.
 template <bool kSum, int kMinWaves = 2, bool kPrefetch = true, int kAblate = 0, bool kMix4 = true,
-          int kTips = 0, bool kSwapX3 = false, bool kEarly = false>
+          int kTips = 0, int kX3 = 0, bool kEarly = false, bool kFirstX2 = false,
+          bool kSplitB = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                      double *__restrict__ x3, const double *__restrict__ EV,
@@ -569,8 +583,12 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   const int64_t stride = (int64_t)gridDim.x * 64;
   if constexpr (kAblate == 2)
     for (auto &q : pf) q = f64x2{1.0, 1.0};
+  constexpr bool kX2Early = kFirstX2 && kEarly && kPrefetch && kAblate != 2 && kTips == 0;
+  f64x2 pf2[kX2Early ? PT::kChunks / kBlock : 1];
   if constexpr (kEarly && kPrefetch && kAblate != 2 && !T2)  // the first dense child's first tile
     if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
+  if constexpr (kX2Early)
+    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(x2, (int64_t)blockIdx.x * 64, n, pf2);
   // A fragments: [mt][s] -> lane holds M[row = 16mt + lo16][col = 4s + g]
   // (kMix4: [1][s] -> M[row = 16 + lane%4][col = 4s + g], the 4x4x4_4b form)
   double AL[2][5], AR[2][5], AE[2][5];
@@ -581,7 +599,9 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       const int row = (kMix4 && mt == 1) ? 16 + (lane & 3) : 16 * mt + lo16, col = 4 * st + g;
       AL[mt][st] = row < S ? left[c * S * S + row * S + col] : 0.0;   // P_L[k=row][l=col]
       AR[mt][st] = row < S ? right[c * S * S + row * S + col] : 0.0;
-      AE[mt][st] = row < S ? EV[col * S + row] : 0.0;                // EV^T[l=row][k=col]
+      // EV^T[l=row][k=col]; kX3 == 2: A row i of the first tile computes state 4*(i%4) + i/4
+      const int erow = (kX3 == 2 && mt == 0) ? 4 * (lo16 & 3) + (lo16 >> 2) : row;
+      AE[mt][st] = erow < S ? EV[col * S + erow] : 0.0;
     }
   const double m = Num<double>::minlik();
   __shared__ double tabs[(T1 ? 1 : 0) + (T2 ? 1 : 0) + (T1 ? 0 : 1)][T1 ? 4 * kProtCodes * 20 : 1];
@@ -599,9 +619,25 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   const double *td = reinterpret_cast<const double *>(tile);
   double *tw = reinterpret_cast<double *>(tile);
   long long acc = 0;
+  // the five B-fragment values of sub-tile row xr (kSplitB: each read from its
+  // own laundered LDS address, so no two are paired into a ds_read2_b64)
+  auto bfrag = [&](const double *xr, double (&bv)[5]) {
+#pragma unroll
+    for (int st = 0; st < 5; st++) {
+      if constexpr (kSplitB) {
+        using L = const __attribute__((address_space(3))) double;
+        L *q = (L *)(xr + 4 * st);
+        asm volatile("" : "+v"(q));
+        bv[st] = *q;
+      } else {
+        bv[st] = xr[4 * st];
+      }
+    }
+  };
   if constexpr (!kEarly && kPrefetch && kAblate != 2 && !T2)  // the first dense child's first tile
     if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
-  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
+  auto trip = [&](const int64_t base, auto first_tag) {
+    constexpr bool kFirst = decltype(first_tag)::value;
     f64x4 P[4][2];  // per sub-tile: U_L^T, then p = U_L^T * U_R^T
     const int64_t sq = base + lane < n ? base + lane : n - 1;
     const int code1 = T1 ? prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) : 0;
@@ -612,7 +648,12 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
     } else if constexpr (kPrefetch) {
       tile_put<double>(tile, pf);
       __syncthreads();
-      if constexpr (kAblate != 2) tile_fetch<double>(x2, base, n, pf);
+      if constexpr (kFirst && kX2Early) {
+#pragma unroll
+        for (int i = 0; i < PT::kChunks / kBlock; i++) pf[i] = pf2[i];
+      } else if constexpr (kAblate != 2) {
+        tile_fetch<double>(x2, base, n, pf);
+      }
     } else {
       tile_load<double>(x1, base, n, tile);
       __syncthreads();
@@ -620,15 +661,16 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
     if constexpr (!T1) {
 #pragma unroll
       for (int t = 0; t < 4; t++) {
-        const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
+        double bv[5];
+        bfrag(td + (16 * t + lo16) * kRow + c * S + g, bv);
 #pragma unroll
         for (int mt = 0; mt < 2; mt++) {
           f64x4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int st = 0; st < 5; st++) {
-            if constexpr (kAblate == 1) u[st & 3] += xr[4 * st] * AL[mt][st];
-            else if (kMix4 && mt == 1) u[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(AL[1][st], xr[4 * st], u[0], 0, 0, 0);
-            else u = __builtin_amdgcn_mfma_f64_16x16x4f64(AL[mt][st], xr[4 * st], u, 0, 0, 0);
+            if constexpr (kAblate == 1) u[st & 3] += bv[st] * AL[mt][st];
+            else if (kMix4 && mt == 1) u[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(AL[1][st], bv[st], u[0], 0, 0, 0);
+            else u = __builtin_amdgcn_mfma_f64_16x16x4f64(AL[mt][st], bv[st], u, 0, 0, 0);
           }
           P[t][mt] = u;
         }
@@ -655,15 +697,16 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
     }
 #pragma unroll
     for (int t = 0; t < 4; t++) {
-      const double *xr = td + (16 * t + lo16) * kRow + c * S + g;
+      double bv[5];
+      bfrag(td + (16 * t + lo16) * kRow + c * S + g, bv);
 #pragma unroll
       for (int mt = 0; mt < 2; mt++) {
         f64x4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int st = 0; st < 5; st++) {
-          if constexpr (kAblate == 1) u[st & 3] += xr[4 * st] * AR[mt][st];
-          else if (kMix4 && mt == 1) u[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(AR[1][st], xr[4 * st], u[0], 0, 0, 0);
-          else u = __builtin_amdgcn_mfma_f64_16x16x4f64(AR[mt][st], xr[4 * st], u, 0, 0, 0);
+          if constexpr (kAblate == 1) u[st & 3] += bv[st] * AR[mt][st];
+          else if (kMix4 && mt == 1) u[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(AR[1][st], bv[st], u[0], 0, 0, 0);
+          else u = __builtin_amdgcn_mfma_f64_16x16x4f64(AR[mt][st], bv[st], u, 0, 0, 0);
         }
         P[t][mt] = P[t][mt] * u;  // prod[k] = umpL[k] * umpR[k]
       }
@@ -694,7 +737,11 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       // site lo16 of sub-tile t is small in category c iff its 4 lanes agree
       mine |= (b & (b >> 16) & (b >> 32) & (b >> 48) & 0xFFFFull) << (16 * t);
       double *w = tw + (16 * t + lo16) * kRow + c * S;
-      if constexpr (kSwapX3) {
+      if constexpr (kX3 == 2) {
+        *reinterpret_cast<f64x2 *>(w + 4 * g) = f64x2{X0[0], X0[1]};
+        *reinterpret_cast<f64x2 *>(w + 4 * g + 2) = f64x2{X0[2], X0[3]};
+        w[16 + g] = X1[0];
+      } else if constexpr (kX3 == 1) {
         // lane of row g holds l = g + 4r (X0[r]) and 16 + g (X1).  After
         // swap_rows16(X0[1], X0[0]) a lane of an even row holds (g+4, g+5),
         // of an odd row (g-1, g); after swap_rows16(X0[3], X0[2]) (g+12, g+13)
@@ -756,7 +803,13 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       }
     }
     __syncthreads();
+  };
+  int64_t base = (int64_t)blockIdx.x * 64;
+  if constexpr (kX2Early) {
+    if (base < n) trip(base, std::true_type{});
+    base += stride;
   }
+  for (; base < n; base += stride) trip(base, std::false_type{});
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
 

@@ -1,0 +1,115 @@
+// clock_drift.hip -- probe (not product code): per-launch duration of the
+// protein FMA kernel and of the headline DNA f64 kernel over a long run of
+// back-to-back launches, and the shader clock between launches.  Every K-th
+// launch is followed by a one-wave probe that spins 3 us and reports
+// d(s_memtime) / d(s_memrealtime) x 100 MHz -- the clock the chip holds right
+// after that launch (MI355X_MICROARCH.md, DVFS give-back item 6).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//     -I amd-versal-phylogenetic-likelihood-function_amd/csrc tools/probes/clock_drift.hip -o build/clock_drift
+//   build/clock_drift [launches] [probe_every]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "plf_dna.hpp"
+#include "plf_prot.hpp"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+using namespace plfx::dev;
+
+__global__ void fill(double *p, int64_t n, uint64_t seed, double scale_every4, int rec) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    double v = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    if (scale_every4 != 1.0 && ((i / rec) % 4) == 0) v *= scale_every4;
+    p[i] = v;
+  }
+}
+
+__global__ void clk_probe(float *out, int i) {
+  if (threadIdx.x) return;
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r1 = r0;
+  while (r1 - r0 < 300) r1 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[i] = (float)((double)(t1 - t0) * 100.0 / (double)(r1 - r0));  // MHz
+}
+
+struct Set { double *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
+
+int main(int argc, char **argv) {
+  const int N = argc > 1 ? atoi(argv[1]) : 400;
+  const int K = argc > 2 ? atoi(argv[2]) : 5;
+  hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
+  const int CUs = prop.multiProcessorCount;
+  const int R = 4;
+  double *EV, *L, *Rm; unsigned long long *ws; float *clk;
+  CK(hipMalloc(&EV, 400 * 8)); CK(hipMalloc(&L, 1600 * 8)); CK(hipMalloc(&Rm, 1600 * 8));
+  CK(hipMalloc(&ws, kWsWords * 8)); CK(hipMemset(ws, 0, kWsWords * 8));
+  CK(hipMalloc(&clk, N * sizeof(float)));
+  fill<<<8, 64>>>(EV, 400, 7, 1.0, 1); fill<<<32, 64>>>(L, 1600, 8, 1.0, 1); fill<<<32, 64>>>(Rm, 1600, 9, 1.0, 1);
+  const int64_t np = 1 << 18, nd = 1 << 20;  // protein / DNA sites (same 80 doubles x n vs 16 x n)
+  std::vector<Set> sets(R);
+  for (auto &s : sets) {
+    const int64_t vals = np * 80;  // = 20.97 M doubles; DNA uses nd*16 = 16.8 M of it
+    CK(hipMalloc(&s.x1, vals * 8)); CK(hipMalloc(&s.x2, vals * 8)); CK(hipMalloc(&s.x3, vals * 8));
+    CK(hipMalloc(&s.wgt, nd * 4)); CK(hipMalloc(&s.sc, nd)); CK(hipMalloc(&s.sum, 8));
+    CK(hipMemset(s.wgt, 0, nd * 4));
+    fill<<<2048, 256>>>(s.x1, vals, 10 + (&s - sets.data()), 1e-14, 80);
+    fill<<<2048, 256>>>(s.x2, vals, 20 + (&s - sets.data()), 1.0, 80);
+  }
+  CK(hipDeviceSynchronize());
+  auto prot = &plf_prot_mfma_kernel<true, 2, true, 0, true, 0, false, true>;
+  auto dna = &plf_dna_f64_pair_kernel<2, true, 1, true, false>;
+  int op = 0, od = 0;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&op, prot, kBlock, 0));
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&od, dna, kBlock, 0));
+  const int gp = std::min<int64_t>(op * CUs, (np + 63) / 64), gd = od * CUs;
+  std::vector<hipEvent_t> ev(2 * N);
+  for (auto &evt : ev) CK(hipEventCreate(&evt));
+  for (int which = 0; which < 2; which++) {
+    for (int pass = 0; pass < 2; pass++) {  // pass 0: no probes; pass 1: probe every K-th launch
+      CK(hipMemset(clk, 0, N * sizeof(float)));
+      CK(hipDeviceSynchronize());
+      for (int i = 0; i < N; i++) {
+        const Set &s = sets[i % R];
+        CK(hipEventRecord(ev[2 * i], 0));
+        if (which == 0)
+          hipLaunchKernelGGL(prot, dim3(gp), dim3(kBlock), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm, (const int32_t *)nullptr,
+                             s.sc, np, ws, s.sum, (const double *)nullptr);
+        else
+          hipLaunchKernelGGL(dna, dim3(gd), dim3(kBlock), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm, (const int32_t *)nullptr,
+                             s.sc, nd, ws, s.sum);
+        CK(hipEventRecord(ev[2 * i + 1], 0));
+        if (pass == 1 && i % K == K - 1) clk_probe<<<1, 64>>>(clk, i);
+      }
+      CK(hipDeviceSynchronize());
+      CK(hipGetLastError());
+      std::vector<float> us(N), mhz(N);
+      CK(hipMemcpy(mhz.data(), clk, N * sizeof(float), hipMemcpyDeviceToHost));
+      for (int i = 0; i < N; i++) { CK(hipEventElapsedTime(&us[i], ev[2 * i], ev[2 * i + 1])); us[i] *= 1000.f; }
+      float t0; CK(hipEventElapsedTime(&t0, ev[0], ev[2 * N - 1]));
+      printf("%s pass %d (%s): %d launches in %.1f ms; per-launch us in windows of %d:\n",
+             which ? "dna f64 pair 2^20" : "protein fma 2^18", pass, pass ? "clock probes" : "no probes",
+             N, t0, N / 20);
+      for (int w = 0; w < 20; w++) {
+        std::vector<float> v(us.begin() + w * (N / 20), us.begin() + (w + 1) * (N / 20));
+        std::sort(v.begin(), v.end());
+        float cs = 0; int cn = 0;
+        for (int i = w * (N / 20); i < (w + 1) * (N / 20); i++) if (mhz[i] > 0) { cs += mhz[i]; cn++; }
+        printf("  [%4d..%4d) median %7.1f us min %7.1f%s", w * (N / 20), (w + 1) * (N / 20), v[v.size() / 2], v[0],
+               cn ? "" : "\n");
+        if (cn) printf("  clock %6.0f MHz\n", cs / cn);
+      }
+    }
+  }
+  return 0;
+}

@@ -16,6 +16,7 @@
 
 #include "plf_prot.hpp"
 #include "prot_variants.hpp"
+#include "prot_v8.hpp"
 
 using namespace plfx::dev;
 
@@ -162,8 +163,19 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,  \
                            s.wgt, s.sc, n, ws, s.sum); }, {}, true});                           \
   }
+#define ADD_KT(NAME, KERNEL, TS)                                                                   \
+  {                                                                                                \
+    auto k = KERNEL;                                                                               \
+    int o = 0; CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, (TS) * 8, 0));                \
+    const int64_t grid = std::min<int64_t>((n + (TS) - 1) / (TS), (int64_t)o * CUs);               \
+    char nm[200]; snprintf(nm, sizeof nm, "%s occ=%d/CU grid=%lld", NAME, o, (long long)grid);      \
+    if (!only || strstr(nm, only) || strstr(nm, "product"))                                        \
+      vs.push_back({nm, [=](const Set &s) {                                                        \
+        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3((TS) * 8), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm, \
+                           s.wgt, s.sc, n, ws, s.sum); }, {}, true});                              \
+  }
   ADD_K("product exact", (&plf_prot_kernel<double, false, true>), 64)
-  ADD_K("product fma-mfma", (&plf_prot_mfma_kernel<true>), 64)
+  ADD_K("product fma-mfma", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
   ADD_K("product exact-lds (NS=1)", (&plf_prot_exact_f64_kernel<true>), 64)
   ADD_K("mfma ablate: no matrix cores", (&plf_prot_mfma_kernel<true, 2, true, 1>), 64)
   ADD_K("mfma ablate: no HBM traffic", (&plf_prot_mfma_kernel<true, 2, true, 2>), 64)
@@ -177,6 +189,13 @@ int main(int argc, char **argv) {
   ADD_K("mfma v2 swapX3", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, true, false>), 64)
   ADD_K("mfma v2 early", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, false, true>), 64)
   ADD_K("mfma v2 swapX3+early", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, true, true>), 64)
+  // round 2: 8-wave blocks, three LDS tiles, both next tiles in flight per trip
+  ADD_K("mfma v3 permX3+early", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
+  ADD_K("mfma v3 permX3+early+splitB", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, true>), 64)
+  ADD_KT("mfma v8 perm late", (&plf_prot_mfma8_kernel<true, true, false, 64>), 64)
+  ADD_KT("mfma v4x2 perm late", (&plf_prot_mfma8_kernel<true, true, false, 32>), 32)
+  ADD_KT("mfma v4x2 perm early", (&plf_prot_mfma8_kernel<true, true, true, 32>), 32)
+  ADD_KT("mfma v4x2 noperm late", (&plf_prot_mfma8_kernel<true, false, false, 32>), 32)
 
   // FMA-mode reference for the mfma variants
   std::vector<uint64_t> h_fref(n * 80);
