@@ -80,6 +80,151 @@ cat_pf(const float *__restrict__ x1, const float *__restrict__ x2, float *__rest
   block_ticket_sum(acc, ws, scaler_sum);
 }
 
+// Trip epilogue variants (U = 4: a wave-trip is 64 consecutive sites, one per
+// lane): kPackW -- lane l loads the weight of site base+l (one coalesced dword
+// load per trip instead of U loads of the same word by 4 lanes each);
+// kPackSc -- lane l stores the scaler byte of site base+l (one 64-B store per
+// trip instead of U 16-B ones).  Full trips only (harness n multiple of 4096).
+template <bool kPackW, bool kPackSc>
+__global__ void __launch_bounds__(256, 1)
+cat_epi(const float *__restrict__ x1, const float *__restrict__ x2, float *__restrict__ x3,
+        const float *__restrict__ EV, const float *__restrict__ left, const float *__restrict__ right,
+        const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+        int64_t *scaler_sum) {
+  constexpr int U = 4;
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 3, q = lane >> 2, nib = lane & 60;
+  float PL[16], PR[16], E[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) { PL[i] = left[c * 16 + i]; PR[i] = right[c * 16 + i]; E[i] = EV[i]; }
+  const float m = Num<float>::minlik();
+  long long acc = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  for (int64_t base = wave * 16 * U; base < n; base += stride) {
+    float a[U][4], b[U][4];
+    int w[U], wl = 0;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      Num<float>::load4<true>(x1 + site * 16 + c * 4, a[u]);
+      Num<float>::load4<true>(x2 + site * 16 + c * 4, b[u]);
+      if constexpr (!kPackW) w[u] = wgt_at(wgt, site, ws);
+    }
+    if constexpr (kPackW) wl = wgt_at(wgt, base + lane, ws);
+    unsigned long long mk[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      float o[4];
+      site_cat<float>(a[u], b[u], PL, PR, E, o);
+      const bool small = (Num<float>::abs(o[0]) < m) && (Num<float>::abs(o[1]) < m) &&
+                         (Num<float>::abs(o[2]) < m) && (Num<float>::abs(o[3]) < m);
+      mk[u] = __ballot(small);
+      const bool sc = ((mk[u] >> nib) & 0xFull) == 0xFull;
+#pragma unroll
+      for (int l = 0; l < 4; l++) { const float s = o[l] * Num<float>::two32(); o[l] = sc ? s : o[l]; }
+      Num<float>::store4_nt(x3 + site * 16 + c * 4, o);
+      if constexpr (!kPackSc) if (c == 0 && scaler) scaler[site] = (uint8_t)sc;
+      if constexpr (!kPackW) acc += (c == 0 && sc) ? (long long)w[u] : 0ll;
+    }
+    // site base+lane: step u = lane>>4, slot q = lane&15
+    const int ul = lane >> 4;
+    const unsigned long long ml = ul == 0 ? mk[0] : ul == 1 ? mk[1] : ul == 2 ? mk[2] : mk[3];
+    const bool scl = ((ml >> (4 * (lane & 15))) & 0xFull) == 0xFull;
+    if constexpr (kPackSc) if (scaler) scaler[base + lane] = (uint8_t)scl;
+    if constexpr (kPackW) acc += scl ? (long long)wl : 0ll;
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
+// Reducer-wave variant: 4 working waves + 1 wave that does no CLV work and
+// makes the block's scaler-sum ticket after the block barrier -- its returned
+// atomics do not queue behind any store acknowledgements (a working wave's
+// returned atomic waits, in vmcnt order, for its final trip's x3 stores).
+// kMode 0: full; 1: weights read but no ticket (partial to ws by plain store);
+// 2: ticket but no weight reads (every scaled site counts 1).
+template <int U, int kMode>
+__global__ void __launch_bounds__(320, 1)
+cat_red(const float *__restrict__ x1, const float *__restrict__ x2, float *__restrict__ x3,
+        const float *__restrict__ EV, const float *__restrict__ left, const float *__restrict__ right,
+        const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+        int64_t *scaler_sum) {
+  __shared__ long long part[4];
+  const int w4 = threadIdx.x >> 6;
+  long long acc = 0;
+  if (w4 < 4) {
+    const int lane = threadIdx.x & 63;
+    const int c = lane & 3, q = lane >> 2, nib = lane & 60;
+    float PL[16], PR[16], E[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) { PL[i] = left[c * 16 + i]; PR[i] = right[c * 16 + i]; E[i] = EV[i]; }
+    const float m = Num<float>::minlik();
+    const int64_t wave = (int64_t)blockIdx.x * 4 + w4;
+    const int64_t stride = (int64_t)gridDim.x * 4 * 16 * U;
+    for (int64_t base = wave * 16 * U; base < n; base += stride) {
+      float a[U][4], b[U][4];
+      int w[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t site = base + u * 16 + q;
+        Num<float>::load4<true>(x1 + site * 16 + c * 4, a[u]);
+        Num<float>::load4<true>(x2 + site * 16 + c * 4, b[u]);
+        w[u] = kMode == 2 ? 1 : wgt_at(wgt, site, ws);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t site = base + u * 16 + q;
+        float o[4];
+        site_cat<float>(a[u], b[u], PL, PR, E, o);
+        const bool small = (Num<float>::abs(o[0]) < m) && (Num<float>::abs(o[1]) < m) &&
+                           (Num<float>::abs(o[2]) < m) && (Num<float>::abs(o[3]) < m);
+        const unsigned long long mk = __ballot(small);
+        const bool sc = ((mk >> nib) & 0xFull) == 0xFull;
+#pragma unroll
+        for (int l = 0; l < 4; l++) { const float sv = o[l] * Num<float>::two32(); o[l] = sc ? sv : o[l]; }
+        Num<float>::store4_nt(x3 + site * 16 + c * 4, o);
+        if (c == 0 && scaler) scaler[site] = (uint8_t)sc;
+        acc += (c == 0 && sc) ? (long long)w[u] : 0ll;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if constexpr (kMode == 3) {  // per-wave partial by plain store, no barrier, no ticket
+      if ((threadIdx.x & 63) == 0) reinterpret_cast<long long *>(ws)[kWsWords + blockIdx.x * 4 + w4] = acc;
+      return;
+    }
+    if constexpr (kMode == 4) {  // per-wave ticket (no block barrier): 4x the arrivals
+      if ((threadIdx.x & 63) == 0) {
+        long long *wsl = reinterpret_cast<long long *>(ws);
+        const long long G = gridDim.x * 4, id = blockIdx.x * 4 + w4, slot = id % kSlots;
+        const long long nslots = G < kSlots ? G : kSlots, arrivals = (G - slot + kSlots - 1) / kSlots;
+        const long long old = __hip_atomic_fetch_add(wsl + slot * 16, kTick + acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (decode_count(old) == arrivals - 1) {
+          const long long ss = old + kTick + acc - arrivals * kTick;
+          __hip_atomic_store(wsl + slot * 16, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const long long told = __hip_atomic_fetch_add(wsl + kSlots * 16, kTick + ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (decode_count(told) == nslots - 1) {
+            *scaler_sum = (int64_t)(told + kTick + ss - nslots * kTick);
+            __hip_atomic_store(wsl + kSlots * 16, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+      return;
+    }
+    if ((threadIdx.x & 63) == 0) part[w4] = acc;
+  }
+  if constexpr (kMode >= 3) return;
+  __syncthreads();
+  if (threadIdx.x != 256) return;
+  const long long tot = part[0] + part[1] + part[2] + part[3];
+  if constexpr (kMode == 1) {
+    reinterpret_cast<long long *>(ws)[kWsWords + blockIdx.x] = tot;  // beyond the ticket words
+  } else {
+    ticket_publish(tot, ws, scaler_sum);
+  }
+}
+
 __global__ void fill(float *p, int64_t n, uint64_t seed, float scale4) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
@@ -119,7 +264,7 @@ int main(int argc, char **argv) {
   const int CUs = prop.multiProcessorCount;
   float *EV, *L, *Rm; unsigned long long *ws;
   CK(hipMalloc(&EV, 64)); CK(hipMalloc(&L, 256)); CK(hipMalloc(&Rm, 256));
-  CK(hipMalloc(&ws, kWsWords * 8)); CK(hipMemset(ws, 0, kWsWords * 8));
+  CK(hipMalloc(&ws, (kWsWords + 65536) * 8)); CK(hipMemset(ws, 0, (kWsWords + 65536) * 8));
   fill<<<1, 64>>>(EV, 16, 1, 1.f); fill<<<1, 64>>>(L, 64, 2, 1.f); fill<<<1, 64>>>(Rm, 64, 3, 1.f);
   std::vector<Set> sets(R);
   for (int r = 0; r < R; r++) {
@@ -148,6 +293,15 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
                          s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
   }
+#define ADDB(NAME, K, SPB, BLK)                                                                    \
+  {                                                                                                \
+    auto k = K;                                                                                    \
+    const int64_t grid = std::min<int64_t>((n + SPB - 1) / SPB, (int64_t)(2 * CUs));               \
+    vs.push_back({std::string(NAME) + " grid " + std::to_string(grid), 197.0 * n,                 \
+                  [=](const Set &s) {                                                              \
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BLK), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
+                         s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
+  }
   // grids: the product sizes the grid to the co-resident blocks; at 2^20 sites
   // U=4 at 3 blocks/CU leaves 16384 wave-trips over 3072 waves = 5.33 trips
   // (a 6th trip for a third of the waves).  Balanced alternatives:
@@ -158,6 +312,16 @@ int main(int argc, char **argv) {
   ADD("csrc cat U=4 minw4 grid 4/CU (4 trips)", (&plf_dna_kernel<float, 4, true, true, 4>), 256, 1)
   ADD("csrc cat U=1 grid 8/CU", (&plf_dna_kernel<float, 1, true, true, 1>), 64, 1)
   ADD("csrc cat U=3 (product grid)", (&plf_dna_kernel<float, 3, true, true, 1>), 192, 1)
+  ADDB("reducer wave U=4 grid 2/CU", (&cat_red<4, 0>), 256, 320)
+  ADDB("reducer wave U=4 no ticket", (&cat_red<4, 1>), 256, 320)
+  ADDB("reducer wave U=4 no weights", (&cat_red<4, 2>), 256, 320)
+  ADDB("4 waves U=4 per-wave partials (no barrier, no ticket)", (&cat_red<4, 3>), 256, 256)
+  ADDB("4 waves U=4 per-wave ticket (no barrier)", (&cat_red<4, 4>), 256, 256)
+  ADD("epi packW grid 2/CU", (&cat_epi<true, false>), 256, 0.5)
+  ADD("epi packSc grid 2/CU", (&cat_epi<false, true>), 256, 0.5)
+  ADD("epi packW+packSc grid 2/CU", (&cat_epi<true, true>), 256, 0.5)
+  ADD("epi none grid 2/CU", (&cat_epi<false, false>), 256, 0.5)
+  ADD("csrc cat U=4 nosum grid 2/CU", (&plf_dna_kernel<float, 4, false, true, 1>), 256, 0.5)
   ADD("pipelined U=2 grid 4/CU", (&cat_pf<2, 1>), 128, 1)
   ADD("pipelined U=4", (&cat_pf<4, 1>), 256, 1)
   {
