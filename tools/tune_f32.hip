@@ -85,7 +85,7 @@ cat_pf(const float *__restrict__ x1, const float *__restrict__ x2, float *__rest
 // load per trip instead of U loads of the same word by 4 lanes each);
 // kPackSc -- lane l stores the scaler byte of site base+l (one 64-B store per
 // trip instead of U 16-B ones).  Full trips only (harness n multiple of 4096).
-template <bool kPackW, bool kPackSc>
+template <bool kPackW, bool kPackSc, int kWMode = 0>
 __global__ void __launch_bounds__(256, 1)
 cat_epi(const float *__restrict__ x1, const float *__restrict__ x2, float *__restrict__ x3,
         const float *__restrict__ EV, const float *__restrict__ left, const float *__restrict__ right,
@@ -109,7 +109,11 @@ cat_epi(const float *__restrict__ x1, const float *__restrict__ x2, float *__res
       const int64_t site = base + u * 16 + q;
       Num<float>::load4<true>(x1 + site * 16 + c * 4, a[u]);
       Num<float>::load4<true>(x2 + site * 16 + c * 4, b[u]);
-      if constexpr (!kPackW) w[u] = wgt_at(wgt, site, ws);
+      if constexpr (!kPackW) {
+        if constexpr (kWMode == 0) w[u] = wgt_at(wgt, site, ws);
+        else if constexpr (kWMode == 1) w[u] = wgt[site];  // plain (temporal) load
+        else w[u] = __builtin_nontemporal_load(wgt + base + u * 16 + (lane >> 2));
+      }
     }
     if constexpr (kPackW) wl = wgt_at(wgt, base + lane, ws);
     unsigned long long mk[U];
@@ -321,6 +325,7 @@ int main(int argc, char **argv) {
   ADD("epi packSc grid 2/CU", (&cat_epi<false, true>), 256, 0.5)
   ADD("epi packW+packSc grid 2/CU", (&cat_epi<true, true>), 256, 0.5)
   ADD("epi none grid 2/CU", (&cat_epi<false, false>), 256, 0.5)
+  ADD("epi plain weight loads grid 2/CU", (&cat_epi<false, false, 1>), 256, 0.5)
   ADD("csrc cat U=4 nosum grid 2/CU", (&plf_dna_kernel<float, 4, false, true, 1>), 256, 0.5)
   ADD("pipelined U=2 grid 4/CU", (&cat_pf<2, 1>), 128, 1)
   ADD("pipelined U=4", (&cat_pf<4, 1>), 256, 1)
