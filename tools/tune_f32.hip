@@ -229,6 +229,76 @@ cat_red(const float *__restrict__ x1, const float *__restrict__ x2, float *__res
   }
 }
 
+// Weights preloaded: every wave loads the weights of its first 8 trips (8 x 64
+// sites = 2 KiB: lane l holds the 8 weights of trip l/8, sites 8*(l%8)..+7, in
+// two 16-B loads) right after its first trip's CLV loads, and later trips
+// take them from registers: no weight loads inside the steady-state loop.  At
+// the end of trip k the 8 lanes 8k..8k+7 add sum_j sc(site) * w over their 8
+// sites, from the trip's 4 ballot masks (wave-uniform).  Full trips, at most
+// 8 trips per wave (harness: 2^20 sites at 2 blocks per CU).
+__global__ void __launch_bounds__(256, 1)
+cat_wpre(const float *__restrict__ x1, const float *__restrict__ x2, float *__restrict__ x3,
+         const float *__restrict__ EV, const float *__restrict__ left, const float *__restrict__ right,
+         const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+         int64_t *scaler_sum) {
+  constexpr int U = 4;
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 3, q = lane >> 2, nib = lane & 60;
+  float PL[16], PR[16], E[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) { PL[i] = left[c * 16 + i]; PR[i] = right[c * 16 + i]; E[i] = EV[i]; }
+  const float m = Num<float>::minlik();
+  long long acc = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  i32x4 wa = {0, 0, 0, 0}, wb = {0, 0, 0, 0};
+  int k = 0;
+  for (int64_t base = wave * 16 * U; base < n; base += stride, k++) {
+    float a[U][4], b[U][4];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      Num<float>::load4<true>(x1 + site * 16 + c * 4, a[u]);
+      Num<float>::load4<true>(x2 + site * 16 + c * 4, b[u]);
+    }
+    if (k == 0) {  // the weights of trips 0..7: trip l/8, sites 8*(l%8)..+7
+      const int64_t wbase = wave * 16 * U + (int64_t)(lane >> 3) * stride + 8 * (lane & 7);
+      if (wbase < n) {
+        const i32x4 *p = reinterpret_cast<const i32x4 *>(wgt + wbase);
+        wa = __builtin_nontemporal_load(p);
+        wb = __builtin_nontemporal_load(p + 1);
+      }
+    }
+    unsigned long long mk[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = base + u * 16 + q;
+      float o[4];
+      site_cat<float>(a[u], b[u], PL, PR, E, o);
+      const bool small = (Num<float>::abs(o[0]) < m) && (Num<float>::abs(o[1]) < m) &&
+                         (Num<float>::abs(o[2]) < m) && (Num<float>::abs(o[3]) < m);
+      mk[u] = __ballot(small);
+      const bool sc = ((mk[u] >> nib) & 0xFull) == 0xFull;
+#pragma unroll
+      for (int l = 0; l < 4; l++) { const float sv = o[l] * Num<float>::two32(); o[l] = sc ? sv : o[l]; }
+      Num<float>::store4_nt(x3 + site * 16 + c * 4, o);
+      if (c == 0 && scaler) scaler[site] = (uint8_t)sc;
+    }
+    if ((lane >> 3) == k) {  // this lane's 8 sites s = 8*(lane%8)+j of this trip
+      const int s0 = 8 * (lane & 7), u = s0 >> 4;
+      const unsigned long long mu = u == 0 ? mk[0] : u == 1 ? mk[1] : u == 2 ? mk[2] : mk[3];
+      const int w8[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int qq = (s0 + j) & 15;
+        if (((mu >> (4 * qq)) & 0xFull) == 0xFull) acc += w8[j];
+      }
+    }
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
 __global__ void fill(float *p, int64_t n, uint64_t seed, float scale4) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
@@ -321,6 +391,7 @@ int main(int argc, char **argv) {
   ADDB("reducer wave U=4 no weights", (&cat_red<4, 2>), 256, 320)
   ADDB("4 waves U=4 per-wave partials (no barrier, no ticket)", (&cat_red<4, 3>), 256, 256)
   ADDB("4 waves U=4 per-wave ticket (no barrier)", (&cat_red<4, 4>), 256, 256)
+  ADD("weights preloaded grid 2/CU", (&cat_wpre), 256, 0.5)
   ADD("epi packW grid 2/CU", (&cat_epi<true, false>), 256, 0.5)
   ADD("epi packSc grid 2/CU", (&cat_epi<false, true>), 256, 0.5)
   ADD("epi packW+packSc grid 2/CU", (&cat_epi<true, true>), 256, 0.5)
