@@ -145,3 +145,59 @@ def test_tree64_site_shards_lnl_allreduce_gloo_world2():
         assert out["tree_lnl_all_ranks"] == -301.5
         assert out["scaler_events_all_ranks"] == 5
         assert out["alignment_sites"] == 2000
+
+
+# --- tree64's site sharding with real per-rank sweeps: a 16-taxon tree over
+# TREE_SITES sites, split by the reference's ceil rule (plfx.shard); each rank
+# sweeps the whole tree over its block with the oracle and takes its block's
+# root lnL; bench's one all-reduce must give the single-process tree lnL -----
+TREE_TAXA, TREE_SITES = 16, 1001
+
+
+def _tree_block(oracle, off, cnt):
+    """The tree lnL and per-op scaler sums of sites [off, off + cnt)."""
+    rng = np.random.default_rng(77)
+    tips = [rng.random(16 * TREE_SITES) for _ in range(TREE_TAXA)]
+    ops = oracle.balanced_tree_ops(TREE_TAXA)
+    pm = rng.random(ops.shape[0] * 128) * 0.25
+    EV = rng.random(16) * 0.25
+    wgt = (np.arange(TREE_SITES) % 3 + 1).astype(np.int32)[off:off + cnt]
+    clv = [t[16 * off:16 * (off + cnt)].copy() for t in tips]
+    clv += [np.zeros(16 * cnt) for _ in range(ops.shape[0])]
+    sums, _ = oracle.traverse(4, 4, ops, clv, pm, EV, cnt, wgt)
+    return oracle.root_lnl(4, 4, clv[-1], cnt, wgt=wgt, scaler_sums=sums), sums
+
+
+def _tree_shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import types
+
+        import bench
+        import oracle
+        import plfx
+
+        off, cnt = plfx.shard(TREE_SITES, world, rank)
+        lnl, sums = _tree_block(oracle, off, cnt)
+        wl = types.SimpleNamespace(lnl=torch.tensor([lnl], dtype=torch.float64),
+                                   sums=torch.from_numpy(sums), n=cnt)
+        q.put((rank, off, cnt, bench.Tree64Workload.post(wl, world, rank, torch.device("cpu"))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tree_site_shards_equal_single_process(oracle, world):
+    """Each rank's block sweep + the one lnL all-reduce = the whole-alignment
+    tree lnL (1e-12 relative: only the summation order differs) and exactly
+    its scaler events; the blocks tile the alignment (ragged last block)."""
+    exp_lnl, exp_sums = _tree_block(oracle, 0, TREE_SITES)
+    assert int(exp_sums.sum()) > 0  # deep levels underflow: the correction is exercised
+    res = _spawn(_tree_shard_worker, world)
+    blocks = sorted((off, cnt) for _, off, cnt, _ in res)
+    assert blocks[0][0] == 0 and sum(c for _, c in blocks) == TREE_SITES
+    assert all(a[0] + a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
+    for _, _, _, out in res:
+        assert abs(out["tree_lnl_all_ranks"] - exp_lnl) <= 1e-12 * abs(exp_lnl)
+        assert out["scaler_events_all_ranks"] == int(exp_sums.sum())
