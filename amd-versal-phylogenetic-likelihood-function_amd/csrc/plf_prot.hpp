@@ -600,7 +600,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       AL[mt][st] = row < S ? left[c * S * S + row * S + col] : 0.0;   // P_L[k=row][l=col]
       AR[mt][st] = row < S ? right[c * S * S + row * S + col] : 0.0;
       // EV^T[l=row][k=col]; kX3 == 2: A row i of the first tile computes state 4*(i%4) + i/4
-      const int erow = (kX3 == 2 && mt == 0) ? 4 * (lo16 & 3) + (lo16 >> 2) : row;
+      const int erow = (kX3 >= 2 && mt == 0) ? 4 * (lo16 & 3) + (lo16 >> 2) : row;
       AE[mt][st] = erow < S ? EV[col * S + erow] : 0.0;
     }
   const double m = Num<double>::minlik();
@@ -741,6 +741,14 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
         *reinterpret_cast<f64x2 *>(w + 4 * g) = f64x2{X0[0], X0[1]};
         *reinterpret_cast<f64x2 *>(w + 4 * g + 2) = f64x2{X0[2], X0[3]};
         w[16 + g] = X1[0];
+      } else if constexpr (kX3 == 3) {
+        // kX3 == 2, and states 16..19 as 16-B pairs: after swap_rows16(X1,
+        // copy) the lanes of even rows hold (16 + g, 17 + g)
+        *reinterpret_cast<f64x2 *>(w + 4 * g) = f64x2{X0[0], X0[1]};
+        *reinterpret_cast<f64x2 *>(w + 4 * g + 2) = f64x2{X0[2], X0[3]};
+        double b0 = X1[0], b1 = X1[0];
+        swap_rows16(b0, b1);
+        if (!(g & 1)) *reinterpret_cast<f64x2 *>(w + 16 + g) = f64x2{b0, b1};
       } else if constexpr (kX3 == 1) {
         // lane of row g holds l = g + 4r (X0[r]) and 16 + g (X1).  After
         // swap_rows16(X0[1], X0[0]) a lane of an even row holds (g+4, g+5),

@@ -192,6 +192,8 @@ int main(int argc, char **argv) {
   // round 2: 8-wave blocks, three LDS tiles, both next tiles in flight per trip
   ADD_K("mfma v3 permX3+early", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
   ADD_K("mfma v3 permX3+early+splitB", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, true>), 64)
+  ADD_K("mfma v3 permX3b128+early", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 3, true, false, false>), 64)
+  ADD_K("mfma v3 permX3b128+early+splitB", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 3, true, false, true>), 64)
   ADD_KT("mfma v8 perm late", (&plf_prot_mfma8_kernel<true, true, false, 64>), 64)
   ADD_KT("mfma v4x2 perm late", (&plf_prot_mfma8_kernel<true, true, false, 32>), 32)
   ADD_KT("mfma v4x2 perm early", (&plf_prot_mfma8_kernel<true, true, true, 32>), 32)
