@@ -1,0 +1,217 @@
+// tune_f32_r3.hip -- tuning only: the f32 DNA node kernel (csrc dna_cat_body,
+// lane = category) against two start-up / bytes-in-flight variants, checked
+// bit-for-bit against csrc before timing, interleaved in one process.
+//
+//  * peel: the product's prologue loads the P rows (8 x 16-B vector loads per
+//    lane) and waits for all of them (vmcnt(0), register copies into the
+//    loop-carried set) BEFORE the first trip's CLV loads issue, so every wave
+//    starts one full memory latency late.  The peeled form issues the first
+//    trip's CLV and weight loads first, then the matrices, computes the
+//    first trip, and enters the unchanged loop for the rest.
+//  * group: the trip's loads go out per 16-site step with a wait after each
+//    (one step's 2 KiB per wave in flight), the f64 pair kernel's regime
+//    (Load order; the stream probe's V = 1 rows).
+//
+// Also measured with temporary knobs in csrc dna_cat_body (not kept): the
+// peel inside the product body, and default-policy (L2-acknowledged) stores
+// for the wave's last trip or every trip.  Results of all of it:
+// profiles/r02_tune_f32_peel_stores.log -- none faster than the product.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//     -I amd-versal-phylogenetic-likelihood-function_amd/csrc tools/tune_f32_r3.hip -o build/tune_f32_r3
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "plf_dna.hpp"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+using namespace plfx::dev;
+
+// kPeel: first trip's loads before the matrices; kGroup: wait after each step's
+// loads.  Full trips only plus the csrc tail (harness n multiple of 4096).
+template <int U, bool kPeel, bool kGroup>
+__global__ void __launch_bounds__(256, 1)
+cat_v(const float *__restrict__ x1, const float *__restrict__ x2, float *__restrict__ x3,
+      const float *__restrict__ EV, const float *__restrict__ left, const float *__restrict__ right,
+      const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+      int64_t *scaler_sum) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 3, q = lane >> 2, nib = lane & 60;
+  const float m = Num<float>::minlik();
+  long long acc = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  const int64_t nfull = n - (16 * U - 1);
+  int64_t base = wave * 16 * U;
+  float a[U][4], b[U][4];
+  int w[U];
+  auto load = [&](int64_t bs) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = bs + u * 16 + q;
+      Num<float>::load4<true>(x1 + site * 16 + c * 4, a[u]);
+      Num<float>::load4<true>(x2 + site * 16 + c * 4, b[u]);
+      w[u] = wgt_at(wgt, site, ws);
+      if constexpr (kGroup) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  auto trip = [&](int64_t bs, const float (&PL)[16], const float (&PR)[16], const float (&E)[16],
+                  bool live = true) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t site = bs + u * 16 + q;
+      float o[4];
+      site_cat<float>(a[u], b[u], PL, PR, E, o);
+      const bool small = (Num<float>::abs(o[0]) < m) && (Num<float>::abs(o[1]) < m) &&
+                         (Num<float>::abs(o[2]) < m) && (Num<float>::abs(o[3]) < m);
+      const unsigned long long mask = __ballot(small);
+      const bool sc = ((mask >> nib) & 0xFull) == 0xFull;
+#pragma unroll
+      for (int l = 0; l < 4; l++) { const float s = o[l] * Num<float>::two32(); o[l] = sc ? s : o[l]; }
+      if (live) {
+        Num<float>::store4_nt(x3 + site * 16 + c * 4, o);
+        if (c == 0 && scaler) scaler[site] = (uint8_t)sc;
+        acc += (c == 0 && sc) ? (long long)w[u] : 0ll;
+      }
+    }
+  };
+  const bool first = base < nfull;
+  if constexpr (kPeel) {
+    // unconditional (a load in a branch makes the join copy -- and wait for --
+    // its values): a wave with no full trip reads sites clamped into [0, n)
+    const int64_t b0 = first ? base : 0;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int64_t site = b0 + u * 16 + q;
+      site = site < n ? site : n - 1;
+      Num<float>::load4<true>(x1 + site * 16 + c * 4, a[u]);
+      Num<float>::load4<true>(x2 + site * 16 + c * 4, b[u]);
+      w[u] = wgt_at(wgt, site, ws);
+    }
+    // keep the matrix loads (and anything waiting on them) behind these
+    asm volatile("" ::: "memory");
+  }
+  float PL[16], PR[16], E[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) { PL[i] = left[c * 16 + i]; PR[i] = right[c * 16 + i]; E[i] = EV[i]; }
+  if constexpr (kPeel) {
+    // computed by every wave (the ballots keep the loads from sinking into a
+    // branch), stored only by waves that own a full first trip
+    trip(base, PL, PR, E, first);
+    base += stride;
+  }
+  for (; base < nfull; base += stride) {
+    load(base);
+    trip(base, PL, PR, E);
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
+__global__ void fill(float *p, int64_t n, uint64_t seed, float scale4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    float v = (float)((double)(z >> 11) * (1.0 / 9007199254740992.0));
+    if (scale4 != 1.0f && ((i / 16) % 4) == 0) v *= scale4;
+    p[i] = v;
+  }
+}
+
+struct Set { float *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
+
+int main(int argc, char **argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : (1 << 20);
+  const int reps = argc > 2 ? atoi(argv[2]) : 60, rounds = 7, R = 6;
+  if (n % 4096) { printf("n must be a multiple of 4096\n"); return 1; }
+  hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
+  const int CUs = prop.multiProcessorCount;
+  float *EV, *L, *Rm; unsigned long long *ws;
+  CK(hipMalloc(&EV, 64)); CK(hipMalloc(&L, 256)); CK(hipMalloc(&Rm, 256));
+  CK(hipMalloc(&ws, (kWsWords + 65536) * 8)); CK(hipMemset(ws, 0, (kWsWords + 65536) * 8));
+  fill<<<1, 64>>>(EV, 16, 1, 1.f); fill<<<1, 64>>>(L, 64, 2, 1.f); fill<<<1, 64>>>(Rm, 64, 3, 1.f);
+  std::vector<Set> sets(R);
+  for (int r = 0; r < R; r++) {
+    Set &s = sets[r];
+    CK(hipMalloc(&s.x1, n * 64)); CK(hipMalloc(&s.x2, n * 64)); CK(hipMalloc(&s.x3, n * 64));
+    CK(hipMalloc(&s.wgt, n * 4)); CK(hipMalloc(&s.sc, n)); CK(hipMalloc(&s.sum, 8));
+    fill<<<2048, 256>>>(s.x1, n * 16, 10 + r, 1e-12f);
+    fill<<<2048, 256>>>(s.x2, n * 16, 20 + r, 1.f);
+    std::vector<int> wv(n);
+    for (int64_t i = 0; i < n; i++) wv[i] = 1 + (int)(i % 3);
+    CK(hipMemcpy(s.wgt, wv.data(), n * 4, hipMemcpyHostToDevice));
+  }
+  CK(hipDeviceSynchronize());
+  auto occ = [&](const void *k) { int b = 0; CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, 256, 0)); return b; };
+  struct V { std::string name; double bytes; std::function<void(const Set &)> run; std::vector<float> us; };
+  std::vector<V> vs;
+#define ADD(NAME, K, SPB, PERCU)                                                                   \
+  {                                                                                                \
+    auto k = K;                                                                                    \
+    const int o = occ((const void *)k);                                                            \
+    const int64_t grid = std::min<int64_t>((n + SPB - 1) / SPB, (int64_t)CUs * std::min(o, PERCU)); \
+    vs.push_back({std::string(NAME) + " occ " + std::to_string(o) + " grid " + std::to_string(grid), 193.0 * n, \
+                  [=](const Set &s) {                                                              \
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
+                         s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
+  }
+  ADD("csrc cat U=4 grid 2/CU (product)", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 2)
+  ADD("peel U=4 2/CU", (&cat_v<4, true, false>), 256, 2)
+  ADD("plain U=4 2/CU (harness form of csrc)", (&cat_v<4, false, false>), 256, 2)
+  ADD("group U=4 2/CU", (&cat_v<4, false, true>), 256, 2)
+  ADD("peel+group U=4 2/CU", (&cat_v<4, true, true>), 256, 2)
+  ADD("peel+group U=4 4/CU", (&cat_v<4, true, true>), 256, 4)
+  ADD("peel U=2 4/CU", (&cat_v<2, true, false>), 128, 4)
+  ADD("peel+group U=2 4/CU", (&cat_v<2, true, true>), 128, 4)
+  ADD("peel U=8 1/CU", (&cat_v<8, true, false>), 512, 1)
+  ADD("csrc cat U=4 nosum 2/CU", (&plf_dna_kernel<float, 4, false, true, 1>), 256, 2)
+  {
+    const size_t bytes = n * 64;
+    std::vector<char> ref(bytes), got(bytes), rsc(n), gsc(n);
+    int64_t rsum = 0, gsum = 0;
+    vs[0].run(sets[0]);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(ref.data(), sets[0].x3, bytes, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(rsc.data(), sets[0].sc, n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(&rsum, sets[0].sum, 8, hipMemcpyDeviceToHost));
+    for (size_t i = 1; i + 1 < vs.size(); i++) {
+      CK(hipMemset(sets[0].x3, 0xFF, bytes)); CK(hipMemset(sets[0].sc, 7, n)); CK(hipMemset(sets[0].sum, 0, 8));
+      vs[i].run(sets[0]);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(got.data(), sets[0].x3, bytes, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(gsc.data(), sets[0].sc, n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(&gsum, sets[0].sum, 8, hipMemcpyDeviceToHost));
+      const bool ok = !memcmp(ref.data(), got.data(), bytes) && !memcmp(rsc.data(), gsc.data(), n) && rsum == gsum;
+      printf("check %-44s %s\n", vs[i].name.c_str(), ok ? "bit-exact" : "MISMATCH");
+    }
+  }
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; r++)
+    for (auto &v : vs) {
+      for (int i = 0; i < 3; i++) v.run(sets[i % R]);
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < reps; i++) v.run(sets[i % R]);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      v.us.push_back(ms * 1000.f / reps);
+    }
+  CK(hipGetLastError());
+  printf("n=%lld sites f32, %d reps x %d rounds interleaved, %d buffer sets, %% at 193 B/site\n", (long long)n, reps,
+         rounds, R);
+  for (auto &v : vs) {
+    std::sort(v.us.begin(), v.us.end());
+    const double t = v.us[v.us.size() / 2] * 1e-6;
+    printf("%-48s median %8.2f us (min %8.2f)  %5.1f%% of 8 TB/s\n", v.name.c_str(), v.us[v.us.size() / 2], v.us[0],
+           100.0 * v.bytes / t / 8e12);
+  }
+  return 0;
+}
