@@ -361,7 +361,34 @@ plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restric
 // that consumes the previous row's result pins that distance (left alone, the
 // compiler hoists a phase's 200 reads to its start and spills them), and an
 // opaque per-trip offset keeps the reads inside the site loop.
-template <bool kSum, int kMinWaves = 2, int kTips = 0>
+//
+// kRows > 0: phases 1 and 2 run kRows rows k at a time, streaming the
+// group's columns l (P_L / P_R sit in LDS group-transposed: [group][l][kRows])
+// so a wave carries kRows independent add chains instead of one.  Each chain
+// keeps plf()'s order (ascending l from the first product), so the results
+// are bit-identical; what changes is the issue pattern: a single chain waits
+// the f64 add's ~22-cycle dependent latency after every add
+// (tools/probes/valu_f64.hip), which at two waves per SIMD held the row form
+// to ~40 % of the VALU issue rate.
+// An empty asm that takes and returns every chain value: the compiler can no
+// longer finish one independent chain before starting the next (it did, and
+// held all the chains' operands in registers -- 256 VGPRs and spills).
+template <int R>
+__device__ __forceinline__ void pin_chains(double (&u)[R]) {
+  if constexpr (R == 2) {
+    asm volatile("" : "+v"(u[0]), "+v"(u[1]));
+  } else if constexpr (R == 4) {
+    asm volatile("" : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]));
+  } else if constexpr (R == 10) {
+    asm volatile("" : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]),
+                 "+v"(u[6]), "+v"(u[7]), "+v"(u[8]), "+v"(u[9]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < R; j++) asm volatile("" : "+v"(u[j]));
+  }
+}
+
+template <bool kSum, int kMinWaves = 2, int kTips = 0, int kRows = 0, bool kPf = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                           double *__restrict__ x3, const double *__restrict__ EV,
@@ -381,7 +408,19 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
   // a tip child's matrix lives in its table instead (2 blocks per CU still fit)
   constexpr int oR = T1 ? 0 : 800, oE = oR + (T2 ? 0 : 800);
   __shared__ f64x2 mats[oE + 200];
-  {
+  static_assert(kRows == 0 || (kRows % 2 == 0 && S % kRows == 0), "kRows: even divisor of 20");
+  if constexpr (kRows > 0) {
+    // P[c][k][l] -> [c][k / kRows][l][k % kRows]
+    double *md = reinterpret_cast<double *>(mats);
+    for (int i = threadIdx.x; i < 4 * S * S; i += kBlock) {
+      const int cc = i / (S * S), r = i - cc * S * S, k = r / S, l = r - k * S;
+      const int d = cc * S * S + (k / kRows) * (S * kRows) + l * kRows + (k % kRows);
+      if constexpr (!T1) md[d] = left[i];
+      if constexpr (!T2) md[2 * oR + d] = right[i];
+    }
+    const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
+    for (int i = threadIdx.x; i < 200; i += kBlock) mats[oE + i] = ge[i];
+  } else {
     const f64x2 *gl = reinterpret_cast<const f64x2 *>(left);
     const f64x2 *gr = reinterpret_cast<const f64x2 *>(right);
     const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
@@ -415,89 +454,256 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
       for (int i = 0; i < 10; i++) cur[i] = nxt[i];
     }
   };
-  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
-    int off = 0;
-    asm volatile("" : "+v"(off));
-    const f64x2 *mL = mats + off + c * 200, *mR = mats + off + oR + c * 200, *mE = mats + off + oE;
-    double U[S];
-    const int64_t sq = base + lane < n ? base + lane : n - 1;
-    if constexpr (T1) {  // tip: U from the table row of the site's code
-      const double *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
+  // kRows form of phases 1/2: M = the category's group-transposed matrix,
+  // x = the child's 20 values; fn(k, sum_l x[l] * M[k][l]) for every k.  The
+  // group's column reads run kDist columns ahead of their use (a ring of
+  // registers; the empty asm pins the distance as in phase()).
+  constexpr int kHalf = kRows > 0 ? kRows / 2 : 1, kDist = 2;
+  auto gphase = [&](const f64x2 *M, const double (&x)[S], auto &&fn) {
+    int o = 0;
+    double tok = 0.0;
 #pragma unroll
-      for (int k = 0; k < S; k++) U[k] = r[k];
-    } else {
-      double a[S];
-      tile_load<double>(x1, base, n, tile);
-      __syncthreads();
-      row_read<double>(tile, lane, c, a);
-      __syncthreads();
-      phase(mL, [&](int k, const f64x2 (&p)[10]) {
-        double u = a[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
-        u += a[1] * p[0].y;
+    for (int gk = 0; gk < S / (kRows > 0 ? kRows : S); gk++) {
+      const f64x2 *G = M + gk * S * kHalf;
+      f64x2 ring[kDist + 1][kHalf];
+      double u[kRows > 0 ? kRows : 1];
+      asm volatile("" : "+v"(o) : "v"(tok));  // the group's first columns after the last group's end
 #pragma unroll
-        for (int i = 1; i < 10; i++) {
-          u += a[2 * i] * p[i].x;
-          u += a[2 * i + 1] * p[i].y;
+      for (int l = 0; l < kDist; l++)
+#pragma unroll
+        for (int j = 0; j < kHalf; j++) ring[l][j] = G[o + l * kHalf + j];
+#pragma unroll
+      for (int l = 0; l < S; l++) {
+        asm volatile("" : "+v"(o) : "v"(tok));  // column l+kDist is read after column l-1 is used
+        if (l + kDist < S) {
+#pragma unroll
+          for (int j = 0; j < kHalf; j++) ring[(l + kDist) % (kDist + 1)][j] = G[o + (l + kDist) * kHalf + j];
         }
-        U[k] = u;
-        return u;
-      });
-    }
-    if constexpr (T2) {
-      const double *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
+        const f64x2 *col = ring[l % (kDist + 1)];
+        double pr[kRows > 0 ? kRows : 1];
 #pragma unroll
-      for (int k = 0; k < S; k++) U[k] = U[k] * r[k];
-    } else {
-      double b[S];
-      tile_load<double>(x2, base, n, tile);
-      __syncthreads();
-      row_read<double>(tile, lane, c, b);
-      __syncthreads();
-      phase(mR, [&](int k, const f64x2 (&p)[10]) {
-        double u = b[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
-        u += b[1] * p[0].y;
+        for (int j = 0; j < 2 * kHalf; j++) pr[j] = x[l] * ((j & 1) ? col[j >> 1].y : col[j >> 1].x);
+        // all R products, then all R adds, then the next column: R chains
+        // interleave and no add waits on the multiply just before it
+        pin_chains(pr);
 #pragma unroll
-        for (int i = 1; i < 10; i++) {
-          u += b[2 * i] * p[i].x;
-          u += b[2 * i + 1] * p[i].y;
+        for (int j = 0; j < 2 * kHalf; j++) {
+          if (l == 0) u[j] = pr[j];  // chain starts at q0 (site_cat, plf_dna.hpp)
+          else u[j] += pr[j];
         }
-        U[k] = U[k] * u;
-        return U[k];
-      });
-    }
-    double O[S];
-#pragma unroll
-    for (int l = 0; l < S; l++) O[l] = 0.0;
-    phase(mE, [&](int k, const f64x2 (&e)[10]) {
-#pragma unroll
-      for (int i = 0; i < 10; i++) {
-        O[2 * i] += U[k] * e[i].x;
-        O[2 * i + 1] += U[k] * e[i].y;
+        pin_chains(u);
+        tok = u[2 * kHalf - 1];
       }
-      return O[S - 1];
-    });
-    bool small = base + lane < n;
 #pragma unroll
-    for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
-    const unsigned long long mk = __ballot(small);
-    if (lane == 0) small_mask[c] = mk;
-    __syncthreads();  // also: every wave is done reading x2 from the tile
-    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
-    const bool sc = (all >> lane) & 1ull;
+      for (int j = 0; j < 2 * kHalf; j++) fn(gk * 2 * kHalf + j, u[j]);
+    }
+  };
+  if constexpr (kRows > 0) {
+    // grouped form: phases 1/2 by kRows-row groups (gphase), phase 3 by two
+    // 10-state halves with the same column ring (10 chains each, from +0.0 as
+    // plf()'s x3 loop); kPf: each child tile is fetched into registers while
+    // the previous phase computes (the FMA kernel's schedule): x2 during
+    // phase 1, the next trip's first dense child during phases 2 and 3.
+    constexpr bool kAnyDense = !(T1 && T2);
+    const double *FD = T1 ? x2 : x1;  // the trip's first dense child
+    const int64_t stride = (int64_t)gridDim.x * 64;
+    constexpr int K = PT::kChunks / kBlock;
+    f64x2 pf[kPf ? K : 1];  // unused (and eliminated) when both children are tips
+    if constexpr (kPf && kAnyDense)
+      if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(FD, (int64_t)blockIdx.x * 64, n, pf);
+    for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
+      int off = 0;
+      asm volatile("" : "+v"(off));
+      const f64x2 *mL = mats + off + c * 200, *mR = mats + off + oR + c * 200, *mE = mats + off + oE;
+      double U[S];
+      const int64_t sq = base + lane < n ? base + lane : n - 1;
+      // stage a dense child's tile: from the prefetch registers (then fetch
+      // the next tile in the sequence) or straight from HBM
+      auto stage = [&](const double *g, const double *next, int64_t nbase) {
+        if constexpr (kPf) {
+          tile_put<double>(tile, pf);
+          __syncthreads();
+          if (nbase < n) tile_fetch<double>(next, nbase, n, pf);
+        } else {
+          tile_load<double>(g, base, n, tile);
+          __syncthreads();
+        }
+      };
+      if constexpr (T1) {
+        const double *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
 #pragma unroll
-    for (int l = 0; l < S; l++) {
-      const double sv = O[l] * Num<double>::two32();
-      O[l] = sc ? sv : O[l];
+        for (int k = 0; k < S; k++) U[k] = r[k];
+      } else {
+        double a[S];
+        // next in the sequence: this trip's x2, or the next trip's x1 when x2 is a tip
+        stage(x1, T2 ? x1 : x2, T2 ? base + stride : base);
+        row_read<double>(tile, lane, c, a);
+        __syncthreads();
+        gphase(mL, a, [&](int k, double u) { U[k] = u; });
+      }
+      if constexpr (T2) {
+        const double *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
+#pragma unroll
+        for (int k = 0; k < S; k++) U[k] = U[k] * r[k];
+      } else {
+        double b[S];
+        stage(x2, FD, base + stride);  // next: the next trip's first dense child
+        row_read<double>(tile, lane, c, b);
+        __syncthreads();
+        gphase(mR, b, [&](int k, double u) { U[k] = U[k] * u; });
+      }
+      // phase 3: O[l] = sum_k U[k] * EV[k][l], two halves of 10 chains
+      double O[S];
+      {
+        int o = 0;
+        double tok = 0.0;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const f64x2 *G = mE + 5 * h;  // EV row k, states 10h..10h+9: G[o + 10k + j]
+          f64x2 ring[3][5];
+          double v[10];
+#pragma unroll
+          for (int j = 0; j < 10; j++) v[j] = 0.0;
+          asm volatile("" : "+v"(o) : "v"(tok));
+#pragma unroll
+          for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int j = 0; j < 5; j++) ring[k][j] = G[o + 10 * k + j];
+#pragma unroll
+          for (int k = 0; k < S; k++) {
+            asm volatile("" : "+v"(o) : "v"(tok));
+            if (k + 2 < S) {
+#pragma unroll
+              for (int j = 0; j < 5; j++) ring[(k + 2) % 3][j] = G[o + 10 * (k + 2) + j];
+            }
+            const f64x2 *e = ring[k % 3];
+            double pr[10];
+#pragma unroll
+            for (int j = 0; j < 10; j++) pr[j] = U[k] * ((j & 1) ? e[j >> 1].y : e[j >> 1].x);
+            pin_chains(pr);
+#pragma unroll
+            for (int j = 0; j < 10; j++) v[j] += pr[j];
+            pin_chains(v);
+            tok = v[9];
+          }
+#pragma unroll
+          for (int j = 0; j < 10; j++) O[10 * h + j] = v[j];
+        }
+      }
+      bool small = base + lane < n;
+#pragma unroll
+      for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
+      const unsigned long long mk = __ballot(small);
+      if (lane == 0) small_mask[c] = mk;
+      __syncthreads();  // also: every wave is done reading x2 from the tile
+      const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+      const bool sc = (all >> lane) & 1ull;
+#pragma unroll
+      for (int l = 0; l < S; l++) {
+        const double sv = O[l] * Num<double>::two32();
+        O[l] = sc ? sv : O[l];
+      }
+      row_write<double>(tile, lane, c, O);
+      const int64_t site = base + lane;
+      if (site < n && c == 0) {
+        if (scaler) scaler[site] = (uint8_t)sc;
+        if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+      }
+      __syncthreads();
+      tile_store<double>(x3, base, n, tile);
+      __syncthreads();  // tile and small_mask are reused by the next trip
     }
-    row_write<double>(tile, lane, c, O);
-    const int64_t site = base + lane;
-    if (site < n && c == 0) {
-      if (scaler) scaler[site] = (uint8_t)sc;
-      if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+  } else {
+    for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+      int off = 0;
+      asm volatile("" : "+v"(off));
+      const f64x2 *mL = mats + off + c * 200, *mR = mats + off + oR + c * 200, *mE = mats + off + oE;
+      double U[S];
+      const int64_t sq = base + lane < n ? base + lane : n - 1;
+      if constexpr (T1) {  // tip: U from the table row of the site's code
+        const double *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
+  #pragma unroll
+        for (int k = 0; k < S; k++) U[k] = r[k];
+      } else {
+        double a[S];
+        tile_load<double>(x1, base, n, tile);
+        __syncthreads();
+        row_read<double>(tile, lane, c, a);
+        __syncthreads();
+        if constexpr (kRows > 0)
+          gphase(mL, a, [&](int k, double u) { U[k] = u; });
+        else
+        phase(mL, [&](int k, const f64x2 (&p)[10]) {
+          double u = a[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
+          u += a[1] * p[0].y;
+  #pragma unroll
+          for (int i = 1; i < 10; i++) {
+            u += a[2 * i] * p[i].x;
+            u += a[2 * i + 1] * p[i].y;
+          }
+          U[k] = u;
+          return u;
+        });
+      }
+      if constexpr (T2) {
+        const double *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
+  #pragma unroll
+        for (int k = 0; k < S; k++) U[k] = U[k] * r[k];
+      } else {
+        double b[S];
+        tile_load<double>(x2, base, n, tile);
+        __syncthreads();
+        row_read<double>(tile, lane, c, b);
+        __syncthreads();
+        if constexpr (kRows > 0)
+          gphase(mR, b, [&](int k, double u) { U[k] = U[k] * u; });
+        else
+        phase(mR, [&](int k, const f64x2 (&p)[10]) {
+          double u = b[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
+          u += b[1] * p[0].y;
+  #pragma unroll
+          for (int i = 1; i < 10; i++) {
+            u += b[2 * i] * p[i].x;
+            u += b[2 * i + 1] * p[i].y;
+          }
+          U[k] = U[k] * u;
+          return U[k];
+        });
+      }
+      double O[S];
+  #pragma unroll
+      for (int l = 0; l < S; l++) O[l] = 0.0;
+      phase(mE, [&](int k, const f64x2 (&e)[10]) {
+  #pragma unroll
+        for (int i = 0; i < 10; i++) {
+          O[2 * i] += U[k] * e[i].x;
+          O[2 * i + 1] += U[k] * e[i].y;
+        }
+        return O[S - 1];
+      });
+      bool small = base + lane < n;
+  #pragma unroll
+      for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
+      const unsigned long long mk = __ballot(small);
+      if (lane == 0) small_mask[c] = mk;
+      __syncthreads();  // also: every wave is done reading x2 from the tile
+      const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+      const bool sc = (all >> lane) & 1ull;
+  #pragma unroll
+      for (int l = 0; l < S; l++) {
+        const double sv = O[l] * Num<double>::two32();
+        O[l] = sc ? sv : O[l];
+      }
+      row_write<double>(tile, lane, c, O);
+      const int64_t site = base + lane;
+      if (site < n && c == 0) {
+        if (scaler) scaler[site] = (uint8_t)sc;
+        if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+      }
+      __syncthreads();
+      tile_store<double>(x3, base, n, tile);
+      __syncthreads();  // tile and small_mask are reused by the next trip
     }
-    __syncthreads();
-    tile_store<double>(x3, base, n, tile);
-    __syncthreads();  // tile and small_mask are reused by the next trip
   }
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }

@@ -177,6 +177,13 @@ int main(int argc, char **argv) {
   ADD_K("product exact", (&plf_prot_kernel<double, false, true>), 64)
   ADD_K("product fma-mfma", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
   ADD_K("product exact-lds (NS=1)", (&plf_prot_exact_f64_kernel<true>), 64)
+  ADD_K("exact-lds rows=2", (&plf_prot_exact_f64_kernel<true, 2, 0, 2>), 64)
+  ADD_K("exact-lds rows=4", (&plf_prot_exact_f64_kernel<true, 2, 0, 4>), 64)
+  ADD_K("exact-lds rows=10", (&plf_prot_exact_f64_kernel<true, 2, 0, 10>), 64)
+  ADD_K("exact-lds rows=4 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 4, true>), 64)
+  ADD_K("exact-lds rows=10 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true>), 64)
+  ADD_K("exact-sgpr rows=4 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 4, true, true>), 64)
+  ADD_K("exact-sgpr rows=10 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true>), 64)
   ADD_K("mfma ablate: no matrix cores", (&plf_prot_mfma_kernel<true, 2, true, 1>), 64)
   ADD_K("mfma ablate: no HBM traffic", (&plf_prot_mfma_kernel<true, 2, true, 2>), 64)
   ADD_K("mfma 16x16x4 only (padded rows)", (&plf_prot_mfma_kernel<true, 2, true, 0, false>), 64)
