@@ -179,7 +179,9 @@ hipError_t launch_lnl_t(const T *x, int64_t n, const double *catw, const double 
 template <typename T, bool kFma, bool kSum, int kTips>
 hipError_t launch_prot_t(const DnaArgs &a, int max_blocks, hipStream_t s, const T *tipvec) {
   static int cache = 0;
-  auto kernel = &dev::plf_prot_kernel<T, kFma, kSum, 0, 2, kTips>;
+  // f32: the LDS-matrix kernel, 4-row groups, tile prefetch, packed chains in
+  // FMA mode (tools/tune_prot32.hip, profiles/r02_tune_protein_f32.log)
+  auto kernel = &dev::plf_prot_lds_kernel<T, kFma, kSum, 2, kTips, 4>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
                      (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,
@@ -208,7 +210,7 @@ hipError_t launch_prot_exact64_t(const DnaArgs &a, int max_blocks, hipStream_t s
                                  const double *tipvec) {
   static int cache = 0;
   // 10-row groups + tile prefetch (tools/tune_prot.hip, profiles/r02_tune_protein_exact_rows.log)
-  auto kernel = &dev::plf_prot_exact_f64_kernel<kSum, 2, kTips, 10, true>;
+  auto kernel = &dev::plf_prot_lds_kernel<double, false, kSum, 2, kTips, 10>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV,

@@ -348,33 +348,13 @@ plf_prot_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restric
 }
 
 // ---------------------------------------------------------------------------
-// EXACT mode, f64: the matrices live in LDS (P_L and P_R of the 4 categories
-// and EV, 28.8 KB per block) and every value is a wave-uniform ds_read_b128
-// broadcast -- 2 values per 4 LDS cycles and no VALU issue, where the
-// register-distributed form above pays 2 v_readlane (plus hazard nops) per
-// value on the VALU, which is the binding unit of exact mode (every
-// multiply-add is two f64 instructions).  Phases per 64-site tile and wave
-// (= category), each with plf()'s order:
-//   1: U[k]  = sum_l x1[l] * P_L[k][l]        2: U[k] *= sum_l x2[l] * P_R[k][l]
-//   3: O[l]  = sum_k U[k] * EV[k][l]
-// A matrix streams through registers one row ahead of its use; an empty asm
-// that consumes the previous row's result pins that distance (left alone, the
-// compiler hoists a phase's 200 reads to its start and spills them), and an
-// opaque per-trip offset keeps the reads inside the site loop.
-//
-// kRows > 0: phases 1 and 2 run kRows rows k at a time, streaming the
-// group's columns l (P_L / P_R sit in LDS group-transposed: [group][l][kRows])
-// so a wave carries kRows independent add chains instead of one.  Each chain
-// keeps plf()'s order (ascending l from the first product), so the results
-// are bit-identical; what changes is the issue pattern: a single chain waits
-// the f64 add's ~22-cycle dependent latency after every add
-// (tools/probes/valu_f64.hip), which at two waves per SIMD held the row form
-// to ~40 % of the VALU issue rate.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // An empty asm that takes and returns every chain value: the compiler can no
 // longer finish one independent chain before starting the next (it did, and
 // held all the chains' operands in registers -- 256 VGPRs and spills).
-template <int R>
-__device__ __forceinline__ void pin_chains(double (&u)[R]) {
+template <typename T, int R>
+__device__ __forceinline__ void pin_chains(T (&u)[R]) {
   if constexpr (R == 2) {
     asm volatile("" : "+v"(u[0]), "+v"(u[1]));
   } else if constexpr (R == 4) {
@@ -388,6 +368,312 @@ __device__ __forceinline__ void pin_chains(double (&u)[R]) {
   }
 }
 
+// The LDS-matrix protein kernel (f64 exact, f32 exact and f32 FMA): the
+// matrices live in LDS (P_L and P_R of the 4 categories and EV; 28.8 KB f64)
+// and every value is a wave-uniform ds_read_b128 broadcast, where the
+// register-distributed form (plf_prot_kernel) pays v_readlane per value on
+// the VALU, the binding unit.  Lane = site, wave = category; per 64-site tile,
+// each with plf()'s order:
+//   1: U[k]  = sum_l x1[l] * P_L[k][l]        2: U[k] *= sum_l x2[l] * P_R[k][l]
+//   3: O[l]  = sum_k U[k] * EV[k][l]
+// Phases 1 and 2 run kRows rows k at a time, streaming the group's columns l
+// (P_L / P_R sit in LDS group-transposed: [category][group][l][kRows]), so a
+// wave carries kRows independent chains; phase 3 streams EV rows in pieces of
+// kPh3 states (kPh3 chains).  A single chain waits the f64 add's ~22-cycle
+// dependent latency after every add (tools/probes/valu_f64.hip), which at two
+// waves per SIMD held the round-1 row form (one chain per row k) to ~40 % of
+// the VALU issue rate.  Each chain keeps plf()'s order (ascending l from the
+// first product; x3 from +0.0), so the results are bit-identical to it (exact)
+// or to its fused restatement (kFma: every multiply-add one fma).  The column
+// reads run kDist steps ahead of their use (a register ring; an empty asm on a
+// token from the previous step pins the distance, and an opaque per-trip
+// offset keeps the reads inside the site loop).  kPf: each dense child tile is
+// fetched into registers while the previous phase computes (the FMA kernel's
+// schedule): x2 during phase 1, the next trip's first dense child during
+// phases 2 and 3.
+template <typename T, bool kFma, bool kSum, int kTips, int kRows, bool kPf, bool kPack>
+__device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T *__restrict__ x2,
+                                              T *__restrict__ x3, const T *__restrict__ EV,
+                                              const T *__restrict__ left, const T *__restrict__ right,
+                                              const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler,
+                                              int64_t n, unsigned long long *ws, int64_t *scaler_sum,
+                                              const T *__restrict__ tipvec) {
+  constexpr int S = 20;
+  constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
+  using PT = ProtTile<T>;
+  using V = typename PT::V;
+  constexpr int E = 16 / (int)sizeof(T);          // elements per 16-B LDS read
+  constexpr int kPh3 = sizeof(T) == 8 ? 10 : 20;  // phase-3 chains per pass
+  static_assert(kRows % E == 0 && S % kRows == 0, "kRows: a divisor of 20, whole 16-B reads");
+  constexpr int RV = kRows / E, PV = kPh3 / E, kDist = 2;
+  constexpr bool kPacked = kPack && sizeof(T) == 4;  // f32: packed VALU on chain pairs
+  // elements 2q, 2q+1 of a run of 16-B reads, as a pair
+  auto pair2 = [](const V *r, int q) -> f32x2 {
+    if constexpr (sizeof(T) == 4) {
+      const f32x4 w = r[(2 * q) / 4];
+      return (q & 1) ? f32x2{w.z, w.w} : f32x2{w.x, w.y};
+    } else {
+      return f32x2{};
+    }
+  };
+  __shared__ T tabs[(T1 ? 1 : 0) + (T2 ? 1 : 0) + (T1 ? 0 : 1)][T1 ? 4 * kProtCodes * 20 : 1];
+  if constexpr (T1) build_prot_tip_table<T, kFma>(left, tipvec, tabs[0]);
+  if constexpr (T2) build_prot_tip_table<T, kFma>(right, tipvec, tabs[1]);
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  // P_L[4][400] (unless x1 is a tip) | P_R[4][400] (unless x2 is a tip) | EV[400]
+  // in T elements; a tip child's matrix lives in its table instead
+  constexpr int oR = T1 ? 0 : 4 * S * S, oE = oR + (T2 ? 0 : 4 * S * S);
+  __shared__ V mats[(oE + S * S) / E];
+  {
+    T *md = reinterpret_cast<T *>(mats);
+    for (int i = threadIdx.x; i < 4 * S * S; i += kBlock) {  // P[c][k][l] -> [c][k/kRows][l][k%kRows]
+      const int cc = i / (S * S), r = i - cc * S * S, k = r / S, l = r - k * S;
+      const int d = cc * S * S + (k / kRows) * (S * kRows) + l * kRows + (k % kRows);
+      if constexpr (!T1) md[d] = left[i];
+      if constexpr (!T2) md[oR + d] = right[i];
+    }
+    for (int i = threadIdx.x; i < S * S; i += kBlock) md[oE + i] = EV[i];
+  }
+  const T m = Num<T>::minlik();
+  __shared__ V tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock];
+  long long acc = 0;
+  __syncthreads();
+  // phases 1/2: M = the category's group-transposed matrix, x = the child's 20
+  // values; fn(k, sum_l x[l] * M[k][l]) for every k
+  auto gphase = [&](const V *M, const T (&x)[S], auto &&fn) {
+    int o = 0;
+    T tok = T(0);
+#pragma unroll
+    for (int gk = 0; gk < S / kRows; gk++) {
+      const V *G = M + gk * S * RV;
+      V ring[kDist + 1][RV];
+      T u[kPacked ? 1 : kRows];
+      f32x2 u2[kPacked ? kRows / 2 : 1];
+      asm volatile("" : "+v"(o) : "v"(tok));  // the group's first columns after the last group's end
+#pragma unroll
+      for (int l = 0; l < kDist; l++)
+#pragma unroll
+        for (int j = 0; j < RV; j++) ring[l][j] = G[o + l * RV + j];
+#pragma unroll
+      for (int l = 0; l < S; l++) {
+        asm volatile("" : "+v"(o) : "v"(tok));  // column l+kDist is read after column l-1 is used
+        if (l + kDist < S) {
+#pragma unroll
+          for (int j = 0; j < RV; j++) ring[(l + kDist) % (kDist + 1)][j] = G[o + (l + kDist) * RV + j];
+        }
+        const V *col = ring[l % (kDist + 1)];
+        if constexpr (kPacked) {
+          // f32: chain pairs on the packed VALU (v_pk_mul/add/fma_f32, two
+          // IEEE f32 operations per lane and instruction)
+          const f32x2 xv = {x[l], x[l]};
+          if (l == 0 || !kFma) {
+            f32x2 pr[kRows / 2];
+#pragma unroll
+            for (int q = 0; q < kRows / 2; q++) pr[q] = xv * pair2(col, q);
+            pin_chains(pr);
+#pragma unroll
+            for (int q = 0; q < kRows / 2; q++) u2[q] = l == 0 ? pr[q] : u2[q] + pr[q];
+          } else {
+#pragma unroll
+            for (int q = 0; q < kRows / 2; q++) u2[q] = __builtin_elementwise_fma(xv, pair2(col, q), u2[q]);
+          }
+          pin_chains(u2);
+          tok = u2[kRows / 2 - 1].y;
+        } else {
+        if (l == 0 || !kFma) {
+          // all kRows products, then all kRows adds: no add waits on the
+          // multiply just before it (chains start at q0: site_cat, plf_dna.hpp)
+          T pr[kRows];
+#pragma unroll
+          for (int j = 0; j < kRows; j++) pr[j] = x[l] * col[j / E][j % E];
+          pin_chains(pr);
+#pragma unroll
+          for (int j = 0; j < kRows; j++) u[j] = l == 0 ? pr[j] : u[j] + pr[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < kRows; j++) u[j] = madd<T, true>(x[l], col[j / E][j % E], u[j]);
+        }
+        pin_chains(u);
+        tok = u[kRows - 1];
+        }
+      }
+      if constexpr (kPacked) {
+#pragma unroll
+        for (int q = 0; q < kRows / 2; q++) {
+          fn(gk * kRows + 2 * q, (T)u2[q].x);
+          fn(gk * kRows + 2 * q + 1, (T)u2[q].y);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kRows; j++) fn(gk * kRows + j, u[j]);
+      }
+    }
+  };
+  constexpr bool kAnyDense = !(T1 && T2);
+  const T *FD = T1 ? x2 : x1;  // the trip's first dense child
+  const int64_t stride = (int64_t)gridDim.x * 64;
+  constexpr int K = PT::kChunks / kBlock;
+  V pf[kPf ? K : 1];  // unused (and eliminated) when both children are tips
+  if constexpr (kPf && kAnyDense)
+    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<T>(FD, (int64_t)blockIdx.x * 64, n, pf);
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    const V *mL = mats + off + c * (S * S / E), *mR = mats + off + (oR + c * S * S) / E,
+            *mE = mats + off + oE / E;
+    T U[S];
+    const int64_t sq = base + lane < n ? base + lane : n - 1;
+    // stage a dense child's tile: from the prefetch registers (then fetch the
+    // next tile in the sequence) or straight from HBM
+    auto stage = [&](const T *g, const T *next, int64_t nbase) {
+      if constexpr (kPf) {
+        tile_put<T>(tile, pf);
+        __syncthreads();
+        if (nbase < n) tile_fetch<T>(next, nbase, n, pf);
+      } else {
+        tile_load<T>(g, base, n, tile);
+        __syncthreads();
+      }
+    };
+    if constexpr (T1) {  // tip: U from the table row of the site's code
+      const T *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
+#pragma unroll
+      for (int k = 0; k < S; k++) U[k] = r[k];
+    } else {
+      T a[S];
+      // next in the sequence: this trip's x2, or the next trip's x1 when x2 is a tip
+      stage(x1, T2 ? x1 : x2, T2 ? base + stride : base);
+      row_read<T>(tile, lane, c, a);
+      __syncthreads();
+      gphase(mL, a, [&](int k, T u) { U[k] = u; });
+    }
+    if constexpr (T2) {
+      const T *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
+#pragma unroll
+      for (int k = 0; k < S; k++) U[k] = U[k] * r[k];
+    } else {
+      T b[S];
+      stage(x2, FD, base + stride);  // next: the next trip's first dense child
+      row_read<T>(tile, lane, c, b);
+      __syncthreads();
+      gphase(mR, b, [&](int k, T u) { U[k] = U[k] * u; });
+    }
+    // phase 3: O[l] = sum_k U[k] * EV[k][l] from +0.0, kPh3 chains per pass
+    T O[S];
+    {
+      int o = 0;
+      T tok = T(0);
+#pragma unroll
+      for (int h = 0; h < S / kPh3; h++) {
+        const V *G = mE + h * PV;  // EV row k, states h*kPh3..: G[o + k*(S/E) + j]
+        V ring[3][PV];
+        T v[kPacked ? 1 : kPh3];
+        f32x2 v2[kPacked ? kPh3 / 2 : 1];
+#pragma unroll
+        for (int j = 0; j < (kPacked ? 1 : kPh3); j++) v[j] = T(0);
+#pragma unroll
+        for (int q = 0; q < (kPacked ? kPh3 / 2 : 1); q++) v2[q] = f32x2{0.f, 0.f};
+        asm volatile("" : "+v"(o) : "v"(tok));
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+          for (int j = 0; j < PV; j++) ring[k][j] = G[o + (S / E) * k + j];
+#pragma unroll
+        for (int k = 0; k < S; k++) {
+          asm volatile("" : "+v"(o) : "v"(tok));
+          if (k + 2 < S) {
+#pragma unroll
+            for (int j = 0; j < PV; j++) ring[(k + 2) % 3][j] = G[o + (S / E) * (k + 2) + j];
+          }
+          const V *e = ring[k % 3];
+          if constexpr (kPacked) {
+            const f32x2 uv = {(float)U[k], (float)U[k]};
+            if constexpr (kFma) {
+#pragma unroll
+              for (int q = 0; q < kPh3 / 2; q++) v2[q] = __builtin_elementwise_fma(uv, pair2(e, q), v2[q]);
+            } else {
+              f32x2 pr[kPh3 / 2];
+#pragma unroll
+              for (int q = 0; q < kPh3 / 2; q++) pr[q] = uv * pair2(e, q);
+              pin_chains(pr);
+#pragma unroll
+              for (int q = 0; q < kPh3 / 2; q++) v2[q] += pr[q];
+            }
+            pin_chains(v2);
+            tok = v2[kPh3 / 2 - 1].y;
+            continue;
+          }
+          if constexpr (kFma) {
+#pragma unroll
+            for (int j = 0; j < kPh3; j++) v[j] = madd<T, true>(U[k], e[j / E][j % E], v[j]);
+          } else {
+            T pr[kPh3];
+#pragma unroll
+            for (int j = 0; j < kPh3; j++) pr[j] = U[k] * e[j / E][j % E];
+            pin_chains(pr);
+#pragma unroll
+            for (int j = 0; j < kPh3; j++) v[j] += pr[j];
+          }
+          pin_chains(v);
+          tok = v[kPh3 - 1];
+        }
+        if constexpr (kPacked) {
+#pragma unroll
+          for (int q = 0; q < kPh3 / 2; q++) {
+            O[h * kPh3 + 2 * q] = (T)v2[q].x;
+            O[h * kPh3 + 2 * q + 1] = (T)v2[q].y;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < kPh3; j++) O[h * kPh3 + j] = v[j];
+        }
+      }
+    }
+    bool small = base + lane < n;
+#pragma unroll
+    for (int l = 0; l < S; l++) small = small && (Num<T>::abs(O[l]) < m);
+    const unsigned long long mk = __ballot(small);
+    if (lane == 0) small_mask[c] = mk;
+    __syncthreads();  // also: every wave is done reading x2 from the tile
+    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+    const bool sc = (all >> lane) & 1ull;
+#pragma unroll
+    for (int l = 0; l < S; l++) {
+      const T sv = O[l] * Num<T>::two32();
+      O[l] = sc ? sv : O[l];
+    }
+    row_write<T>(tile, lane, c, O);
+    const int64_t site = base + lane;
+    if (site < n && c == 0) {
+      if (scaler) scaler[site] = (uint8_t)sc;
+      if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+    }
+    __syncthreads();
+    tile_store<T>(x3, base, n, tile);
+    __syncthreads();  // tile and small_mask are reused by the next trip
+  }
+  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
+// kPack (f32): chain pairs on v_pk_* -- faster in FMA mode (one v_pk_fma_f32
+// per two multiply-adds), slower in exact mode at 4-row groups
+// (tools/tune_prot32.hip, profiles/r02_tune_protein_f32.log).
+template <typename T, bool kFma, bool kSum, int kMinWaves, int kTips, int kRows, bool kPf = true,
+          bool kPack = kFma>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_lds_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
+                    const T *__restrict__ EV, const T *__restrict__ left, const T *__restrict__ right,
+                    const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                    unsigned long long *ws, int64_t *scaler_sum, const T *__restrict__ tipvec = nullptr) {
+  prot_lds_body<T, kFma, kSum, kTips, kRows, kPf, kPack>(x1, x2, x3, EV, left, right, wgt, scaler, n,
+                                                          ws, scaler_sum, tipvec);
+}
+
+// The round-1 EXACT f64 form, kept for same-process comparisons
+// (tools/tune_prot.hip): one chain per row k, the row streamed one ahead.
+// kRows > 0 runs the product body (plf_prot_lds_kernel) instead.
 template <bool kSum, int kMinWaves = 2, int kTips = 0, int kRows = 0, bool kPf = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
@@ -396,6 +682,11 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
                           const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
                           unsigned long long *ws, int64_t *scaler_sum,
                           const double *__restrict__ tipvec = nullptr) {
+  if constexpr (kRows > 0) {
+    prot_lds_body<double, false, kSum, kTips, kRows, kPf, false>(x1, x2, x3, EV, left, right, wgt,
+                                                                 scaler, n, ws, scaler_sum, tipvec);
+    return;
+  } else {
   constexpr int S = 20;
   constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
   __shared__ double tabs[(T1 ? 1 : 0) + (T2 ? 1 : 0) + (T1 ? 0 : 1)][T1 ? 4 * kProtCodes * 20 : 1];
@@ -404,23 +695,9 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
   using PT = ProtTile<double>;
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  // P_L[4][400] (unless x1 is a tip) | P_R[4][400] (unless x2 is a tip) | EV[400]:
-  // a tip child's matrix lives in its table instead (2 blocks per CU still fit)
   constexpr int oR = T1 ? 0 : 800, oE = oR + (T2 ? 0 : 800);
   __shared__ f64x2 mats[oE + 200];
-  static_assert(kRows == 0 || (kRows % 2 == 0 && S % kRows == 0), "kRows: even divisor of 20");
-  if constexpr (kRows > 0) {
-    // P[c][k][l] -> [c][k / kRows][l][k % kRows]
-    double *md = reinterpret_cast<double *>(mats);
-    for (int i = threadIdx.x; i < 4 * S * S; i += kBlock) {
-      const int cc = i / (S * S), r = i - cc * S * S, k = r / S, l = r - k * S;
-      const int d = cc * S * S + (k / kRows) * (S * kRows) + l * kRows + (k % kRows);
-      if constexpr (!T1) md[d] = left[i];
-      if constexpr (!T2) md[2 * oR + d] = right[i];
-    }
-    const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
-    for (int i = threadIdx.x; i < 200; i += kBlock) mats[oE + i] = ge[i];
-  } else {
+  {
     const f64x2 *gl = reinterpret_cast<const f64x2 *>(left);
     const f64x2 *gr = reinterpret_cast<const f64x2 *>(right);
     const f64x2 *ge = reinterpret_cast<const f64x2 *>(EV);
@@ -454,258 +731,92 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
       for (int i = 0; i < 10; i++) cur[i] = nxt[i];
     }
   };
-  // kRows form of phases 1/2: M = the category's group-transposed matrix,
-  // x = the child's 20 values; fn(k, sum_l x[l] * M[k][l]) for every k.  The
-  // group's column reads run kDist columns ahead of their use (a ring of
-  // registers; the empty asm pins the distance as in phase()).
-  constexpr int kHalf = kRows > 0 ? kRows / 2 : 1, kDist = 2;
-  auto gphase = [&](const f64x2 *M, const double (&x)[S], auto &&fn) {
-    int o = 0;
-    double tok = 0.0;
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    const f64x2 *mL = mats + off + c * 200, *mR = mats + off + oR + c * 200, *mE = mats + off + oE;
+    double U[S];
+    const int64_t sq = base + lane < n ? base + lane : n - 1;
+    if constexpr (T1) {  // tip: U from the table row of the site's code
+      const double *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
 #pragma unroll
-    for (int gk = 0; gk < S / (kRows > 0 ? kRows : S); gk++) {
-      const f64x2 *G = M + gk * S * kHalf;
-      f64x2 ring[kDist + 1][kHalf];
-      double u[kRows > 0 ? kRows : 1];
-      asm volatile("" : "+v"(o) : "v"(tok));  // the group's first columns after the last group's end
-#pragma unroll
-      for (int l = 0; l < kDist; l++)
-#pragma unroll
-        for (int j = 0; j < kHalf; j++) ring[l][j] = G[o + l * kHalf + j];
-#pragma unroll
-      for (int l = 0; l < S; l++) {
-        asm volatile("" : "+v"(o) : "v"(tok));  // column l+kDist is read after column l-1 is used
-        if (l + kDist < S) {
-#pragma unroll
-          for (int j = 0; j < kHalf; j++) ring[(l + kDist) % (kDist + 1)][j] = G[o + (l + kDist) * kHalf + j];
-        }
-        const f64x2 *col = ring[l % (kDist + 1)];
-        double pr[kRows > 0 ? kRows : 1];
-#pragma unroll
-        for (int j = 0; j < 2 * kHalf; j++) pr[j] = x[l] * ((j & 1) ? col[j >> 1].y : col[j >> 1].x);
-        // all R products, then all R adds, then the next column: R chains
-        // interleave and no add waits on the multiply just before it
-        pin_chains(pr);
-#pragma unroll
-        for (int j = 0; j < 2 * kHalf; j++) {
-          if (l == 0) u[j] = pr[j];  // chain starts at q0 (site_cat, plf_dna.hpp)
-          else u[j] += pr[j];
-        }
-        pin_chains(u);
-        tok = u[2 * kHalf - 1];
-      }
-#pragma unroll
-      for (int j = 0; j < 2 * kHalf; j++) fn(gk * 2 * kHalf + j, u[j]);
-    }
-  };
-  if constexpr (kRows > 0) {
-    // grouped form: phases 1/2 by kRows-row groups (gphase), phase 3 by two
-    // 10-state halves with the same column ring (10 chains each, from +0.0 as
-    // plf()'s x3 loop); kPf: each child tile is fetched into registers while
-    // the previous phase computes (the FMA kernel's schedule): x2 during
-    // phase 1, the next trip's first dense child during phases 2 and 3.
-    constexpr bool kAnyDense = !(T1 && T2);
-    const double *FD = T1 ? x2 : x1;  // the trip's first dense child
-    const int64_t stride = (int64_t)gridDim.x * 64;
-    constexpr int K = PT::kChunks / kBlock;
-    f64x2 pf[kPf ? K : 1];  // unused (and eliminated) when both children are tips
-    if constexpr (kPf && kAnyDense)
-      if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(FD, (int64_t)blockIdx.x * 64, n, pf);
-    for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
-      int off = 0;
-      asm volatile("" : "+v"(off));
-      const f64x2 *mL = mats + off + c * 200, *mR = mats + off + oR + c * 200, *mE = mats + off + oE;
-      double U[S];
-      const int64_t sq = base + lane < n ? base + lane : n - 1;
-      // stage a dense child's tile: from the prefetch registers (then fetch
-      // the next tile in the sequence) or straight from HBM
-      auto stage = [&](const double *g, const double *next, int64_t nbase) {
-        if constexpr (kPf) {
-          tile_put<double>(tile, pf);
-          __syncthreads();
-          if (nbase < n) tile_fetch<double>(next, nbase, n, pf);
-        } else {
-          tile_load<double>(g, base, n, tile);
-          __syncthreads();
-        }
-      };
-      if constexpr (T1) {
-        const double *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
-#pragma unroll
-        for (int k = 0; k < S; k++) U[k] = r[k];
-      } else {
-        double a[S];
-        // next in the sequence: this trip's x2, or the next trip's x1 when x2 is a tip
-        stage(x1, T2 ? x1 : x2, T2 ? base + stride : base);
-        row_read<double>(tile, lane, c, a);
-        __syncthreads();
-        gphase(mL, a, [&](int k, double u) { U[k] = u; });
-      }
-      if constexpr (T2) {
-        const double *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
-#pragma unroll
-        for (int k = 0; k < S; k++) U[k] = U[k] * r[k];
-      } else {
-        double b[S];
-        stage(x2, FD, base + stride);  // next: the next trip's first dense child
-        row_read<double>(tile, lane, c, b);
-        __syncthreads();
-        gphase(mR, b, [&](int k, double u) { U[k] = U[k] * u; });
-      }
-      // phase 3: O[l] = sum_k U[k] * EV[k][l], two halves of 10 chains
-      double O[S];
-      {
-        int o = 0;
-        double tok = 0.0;
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const f64x2 *G = mE + 5 * h;  // EV row k, states 10h..10h+9: G[o + 10k + j]
-          f64x2 ring[3][5];
-          double v[10];
-#pragma unroll
-          for (int j = 0; j < 10; j++) v[j] = 0.0;
-          asm volatile("" : "+v"(o) : "v"(tok));
-#pragma unroll
-          for (int k = 0; k < 2; k++)
-#pragma unroll
-            for (int j = 0; j < 5; j++) ring[k][j] = G[o + 10 * k + j];
-#pragma unroll
-          for (int k = 0; k < S; k++) {
-            asm volatile("" : "+v"(o) : "v"(tok));
-            if (k + 2 < S) {
-#pragma unroll
-              for (int j = 0; j < 5; j++) ring[(k + 2) % 3][j] = G[o + 10 * (k + 2) + j];
-            }
-            const f64x2 *e = ring[k % 3];
-            double pr[10];
-#pragma unroll
-            for (int j = 0; j < 10; j++) pr[j] = U[k] * ((j & 1) ? e[j >> 1].y : e[j >> 1].x);
-            pin_chains(pr);
-#pragma unroll
-            for (int j = 0; j < 10; j++) v[j] += pr[j];
-            pin_chains(v);
-            tok = v[9];
-          }
-#pragma unroll
-          for (int j = 0; j < 10; j++) O[10 * h + j] = v[j];
-        }
-      }
-      bool small = base + lane < n;
-#pragma unroll
-      for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
-      const unsigned long long mk = __ballot(small);
-      if (lane == 0) small_mask[c] = mk;
-      __syncthreads();  // also: every wave is done reading x2 from the tile
-      const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
-      const bool sc = (all >> lane) & 1ull;
-#pragma unroll
-      for (int l = 0; l < S; l++) {
-        const double sv = O[l] * Num<double>::two32();
-        O[l] = sc ? sv : O[l];
-      }
-      row_write<double>(tile, lane, c, O);
-      const int64_t site = base + lane;
-      if (site < n && c == 0) {
-        if (scaler) scaler[site] = (uint8_t)sc;
-        if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
-      }
+      for (int k = 0; k < S; k++) U[k] = r[k];
+    } else {
+      double a[S];
+      tile_load<double>(x1, base, n, tile);
       __syncthreads();
-      tile_store<double>(x3, base, n, tile);
-      __syncthreads();  // tile and small_mask are reused by the next trip
-    }
-  } else {
-    for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
-      int off = 0;
-      asm volatile("" : "+v"(off));
-      const f64x2 *mL = mats + off + c * 200, *mR = mats + off + oR + c * 200, *mE = mats + off + oE;
-      double U[S];
-      const int64_t sq = base + lane < n ? base + lane : n - 1;
-      if constexpr (T1) {  // tip: U from the table row of the site's code
-        const double *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
-  #pragma unroll
-        for (int k = 0; k < S; k++) U[k] = r[k];
-      } else {
-        double a[S];
-        tile_load<double>(x1, base, n, tile);
-        __syncthreads();
-        row_read<double>(tile, lane, c, a);
-        __syncthreads();
-        if constexpr (kRows > 0)
-          gphase(mL, a, [&](int k, double u) { U[k] = u; });
-        else
-        phase(mL, [&](int k, const f64x2 (&p)[10]) {
-          double u = a[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
-          u += a[1] * p[0].y;
-  #pragma unroll
-          for (int i = 1; i < 10; i++) {
-            u += a[2 * i] * p[i].x;
-            u += a[2 * i + 1] * p[i].y;
-          }
-          U[k] = u;
-          return u;
-        });
-      }
-      if constexpr (T2) {
-        const double *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
-  #pragma unroll
-        for (int k = 0; k < S; k++) U[k] = U[k] * r[k];
-      } else {
-        double b[S];
-        tile_load<double>(x2, base, n, tile);
-        __syncthreads();
-        row_read<double>(tile, lane, c, b);
-        __syncthreads();
-        if constexpr (kRows > 0)
-          gphase(mR, b, [&](int k, double u) { U[k] = U[k] * u; });
-        else
-        phase(mR, [&](int k, const f64x2 (&p)[10]) {
-          double u = b[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
-          u += b[1] * p[0].y;
-  #pragma unroll
-          for (int i = 1; i < 10; i++) {
-            u += b[2 * i] * p[i].x;
-            u += b[2 * i + 1] * p[i].y;
-          }
-          U[k] = U[k] * u;
-          return U[k];
-        });
-      }
-      double O[S];
-  #pragma unroll
-      for (int l = 0; l < S; l++) O[l] = 0.0;
-      phase(mE, [&](int k, const f64x2 (&e)[10]) {
-  #pragma unroll
-        for (int i = 0; i < 10; i++) {
-          O[2 * i] += U[k] * e[i].x;
-          O[2 * i + 1] += U[k] * e[i].y;
+      row_read<double>(tile, lane, c, a);
+      __syncthreads();
+      phase(mL, [&](int k, const f64x2 (&p)[10]) {
+        double u = a[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
+        u += a[1] * p[0].y;
+#pragma unroll
+        for (int i = 1; i < 10; i++) {
+          u += a[2 * i] * p[i].x;
+          u += a[2 * i + 1] * p[i].y;
         }
-        return O[S - 1];
+        U[k] = u;
+        return u;
       });
-      bool small = base + lane < n;
-  #pragma unroll
-      for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
-      const unsigned long long mk = __ballot(small);
-      if (lane == 0) small_mask[c] = mk;
-      __syncthreads();  // also: every wave is done reading x2 from the tile
-      const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
-      const bool sc = (all >> lane) & 1ull;
-  #pragma unroll
-      for (int l = 0; l < S; l++) {
-        const double sv = O[l] * Num<double>::two32();
-        O[l] = sc ? sv : O[l];
-      }
-      row_write<double>(tile, lane, c, O);
-      const int64_t site = base + lane;
-      if (site < n && c == 0) {
-        if (scaler) scaler[site] = (uint8_t)sc;
-        if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
-      }
-      __syncthreads();
-      tile_store<double>(x3, base, n, tile);
-      __syncthreads();  // tile and small_mask are reused by the next trip
     }
+    if constexpr (T2) {
+      const double *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
+#pragma unroll
+      for (int k = 0; k < S; k++) U[k] = U[k] * r[k];
+    } else {
+      double b[S];
+      tile_load<double>(x2, base, n, tile);
+      __syncthreads();
+      row_read<double>(tile, lane, c, b);
+      __syncthreads();
+      phase(mR, [&](int k, const f64x2 (&p)[10]) {
+        double u = b[0] * p[0].x;  // chain starts at q0: same x3 bits (site_cat, plf_dna.hpp)
+        u += b[1] * p[0].y;
+#pragma unroll
+        for (int i = 1; i < 10; i++) {
+          u += b[2 * i] * p[i].x;
+          u += b[2 * i + 1] * p[i].y;
+        }
+        U[k] = U[k] * u;
+        return U[k];
+      });
+    }
+    double O[S];
+#pragma unroll
+    for (int l = 0; l < S; l++) O[l] = 0.0;
+    phase(mE, [&](int k, const f64x2 (&e)[10]) {
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        O[2 * i] += U[k] * e[i].x;
+        O[2 * i + 1] += U[k] * e[i].y;
+      }
+      return O[S - 1];
+    });
+    bool small = base + lane < n;
+#pragma unroll
+    for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
+    const unsigned long long mk = __ballot(small);
+    if (lane == 0) small_mask[c] = mk;
+    __syncthreads();  // also: every wave is done reading x2 from the tile
+    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+    const bool sc = (all >> lane) & 1ull;
+#pragma unroll
+    for (int l = 0; l < S; l++) {
+      const double sv = O[l] * Num<double>::two32();
+      O[l] = sc ? sv : O[l];
+    }
+    row_write<double>(tile, lane, c, O);
+    const int64_t site = base + lane;
+    if (site < n && c == 0) {
+      if (scaler) scaler[site] = (uint8_t)sc;
+      if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+    }
+    __syncthreads();
+    tile_store<double>(x3, base, n, tile);
+    __syncthreads();  // tile and small_mask are reused by the next trip
   }
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+  }
 }
 
 // ---------------------------------------------------------------------------
