@@ -1138,5 +1138,191 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
 
+
+// ---------------------------------------------------------------------------
+// FMA mode on the matrix cores, f32: v_mfma_f32_16x16x4_f32 is exact f32, a
+// k-ordered fmaf chain bit for bit (MI355X_MICROARCH.md, FP32-input MFMA), so
+// this kernel is bit-identical to the f32 VALU FMA kernels and the oracle's
+// fused restatement.  The f64 kernel's scheme with the f32 operand maps
+// (A: lane l = A[row l&15][k l>>4], B: lane l = B[k l>>4][col l&15],
+// C/D: lane l reg r = D[row 4(l>>4) + r][col l&15] -- rows by 4 per lane group,
+// where f64 interleaves them):
+//   U^T[k][site] = P[k][l] . X^T[l][site]: A row i of tile mt computes
+//     k = pi(16 mt + i) = 16 mt + 4 (i&3) + (i>>2), so lane group g, reg r holds
+//     k = 16 mt + 4 r + g -- exactly the B fragment of k-step s = 4 mt + r of
+//     the back-transform (lane group g = k 4s + g); tile 1 keeps only reg 0
+//     (k = 16 + g), its other rows are zero;
+//   X3^T[l][site] = EV^T[l][k] . p[k][site]: natural rows, so lane group g
+//     holds states 4g..4g+3 of its site (tile 0) and lane group 0 states 16..19
+//     (tile 1): one 16-B LDS write each, no lane movement.
+// Per 16-site sub-tile and category: 20 + 10 MFMAs of 32 cycles (960 cycles;
+// f32 has no 4x4x4 form for rows 16..19).  Tiles as the f64 kernel (prefetch:
+// x2 during phase 1, the next trip's first dense child during phase 2).
+typedef float f32x4m __attribute__((ext_vector_type(4)));
+
+template <bool kSum, int kMinWaves = 2, int kTips = 0>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x2,
+                       float *__restrict__ x3, const float *__restrict__ EV,
+                       const float *__restrict__ left, const float *__restrict__ right,
+                       const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                       unsigned long long *ws, int64_t *scaler_sum,
+                       const float *__restrict__ tipvec = nullptr) {
+  constexpr int S = 20;
+  constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
+  using PT = ProtTile<float>;
+  constexpr int kRow = 4 * PT::kStride;  // floats per site in the LDS tile (84)
+  constexpr int K = PT::kChunks / kBlock;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lo16 = lane & 15, g = lane >> 4;
+  const int64_t stride = (int64_t)gridDim.x * 64;
+  f32x4 pf[K];
+  // the first dense child's first tile, before the matrix fragments
+  if constexpr (!(T1 && T2))
+    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<float>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
+  float AL[2][5], AR[2][5], AE[2][5];
+#pragma unroll
+  for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+    for (int st = 0; st < 5; st++) {
+      const int i = lo16, col = 4 * st + g;
+      const int k = 16 * mt + 4 * (i & 3) + (i >> 2);  // pi: accumulators = back-transform B fragments
+      AL[mt][st] = k < S ? left[c * S * S + k * S + col] : 0.f;   // P_L[k][l]
+      AR[mt][st] = k < S ? right[c * S * S + k * S + col] : 0.f;
+      const int lrow = 16 * mt + i;  // EV^T[l][k]: natural rows
+      AE[mt][st] = lrow < S ? EV[col * S + lrow] : 0.f;
+    }
+  const float m = Num<float>::minlik();
+  __shared__ float tabs[(T1 ? 1 : 0) + (T2 ? 1 : 0) + (T1 ? 0 : 1)][T1 ? 4 * kProtCodes * 20 : 1];
+  if constexpr (T1) build_prot_tip_table<float, true>(left, tipvec, tabs[0]);
+  if constexpr (T2) build_prot_tip_table<float, true>(right, tipvec, tabs[1]);
+  if constexpr (T1) __syncthreads();
+  // U^T of a tip child for sub-tile t in the accumulator layout (reg r of
+  // lane group g = k 4r + g; tile 1 reg 0 = k 16 + g)
+  auto tip_u = [&](const float *tab, int code_lane, int t, f32x4 &u0, f32x4 &u1) {
+    const float *r = tab + c * kProtCodes * 20 + __shfl(code_lane, 16 * t + lo16) * 20;
+    u0 = f32x4{r[g], r[g + 4], r[g + 8], r[g + 12]};
+    u1 = f32x4{r[16 + g], 0.f, 0.f, 0.f};
+  };
+  __shared__ f32x4 tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock];
+  const float *td = reinterpret_cast<const float *>(tile);
+  float *tw = reinterpret_cast<float *>(tile);
+  long long acc = 0;
+  // one child's product U^T for the 4 sub-tiles from the LDS tile (mul: into P)
+  auto product = [&](const float (&A)[2][5], f32x4 (&P)[4][2], bool mul) {
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const float *xr = td + (16 * t + lo16) * kRow + c * S + g;
+      float bv[5];
+#pragma unroll
+      for (int st = 0; st < 5; st++) bv[st] = xr[4 * st];
+#pragma unroll
+      for (int mt = 0; mt < 2; mt++) {
+        f32x4 u = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < 5; st++) u = __builtin_amdgcn_mfma_f32_16x16x4f32(A[mt][st], bv[st], u, 0, 0, 0);
+        P[t][mt] = mul ? P[t][mt] * u : u;  // prod[k] = umpL[k] * umpR[k]
+      }
+    }
+  };
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
+    f32x4 P[4][2];
+    const int64_t sq = base + lane < n ? base + lane : n - 1;
+    const int code1 = T1 ? prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) : 0;
+    const int code2 = T2 ? prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) : 0;
+    if constexpr (T1) {
+#pragma unroll
+      for (int t = 0; t < 4; t++) tip_u(tabs[0], code1, t, P[t][0], P[t][1]);
+    } else {
+      tile_put<float>(tile, pf);
+      __syncthreads();
+      // next: this trip's x2, or the next trip's x1 when x2 is a tip
+      if constexpr (T2) {
+        if (base + stride < n) tile_fetch<float>(x1, base + stride, n, pf);
+      } else {
+        tile_fetch<float>(x2, base, n, pf);
+      }
+      product(AL, P, false);
+      __syncthreads();
+    }
+    if constexpr (T2) {
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        f32x4 u0, u1;
+        tip_u(tabs[1], code2, t, u0, u1);
+        P[t][0] = P[t][0] * u0;
+        P[t][1] = P[t][1] * u1;
+      }
+    } else {
+      tile_put<float>(tile, pf);
+      __syncthreads();
+      if (base + stride < n) tile_fetch<float>(T1 ? x2 : x1, base + stride, n, pf);
+      product(AR, P, true);
+      __syncthreads();  // every wave is done reading x2: the tile takes X3 now
+    }
+    // back-transform: B fragment of k-step s = P[t][s >> 2][s & 3]
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      f32x4 X0 = {0.f, 0.f, 0.f, 0.f}, X1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 5; st++) {
+        const float b = P[t][st >> 2][st & 3];
+        X0 = __builtin_amdgcn_mfma_f32_16x16x4f32(AE[0][st], b, X0, 0, 0, 0);
+        X1 = __builtin_amdgcn_mfma_f32_16x16x4f32(AE[1][st], b, X1, 0, 0, 0);
+      }
+      // lane group g holds states 4g..4g+3 (X0) and, for g = 0, 16..19 (X1)
+      bool small = (__builtin_fabsf(X0[0]) < m) && (__builtin_fabsf(X0[1]) < m) &&
+                   (__builtin_fabsf(X0[2]) < m) && (__builtin_fabsf(X0[3]) < m);
+      if (g == 0)
+        small = small && (__builtin_fabsf(X1[0]) < m) && (__builtin_fabsf(X1[1]) < m) &&
+                (__builtin_fabsf(X1[2]) < m) && (__builtin_fabsf(X1[3]) < m);
+      const unsigned long long b = __ballot(small);
+      mine |= (b & (b >> 16) & (b >> 32) & (b >> 48) & 0xFFFFull) << (16 * t);
+      float *w = tw + (16 * t + lo16) * kRow + c * S;
+      *reinterpret_cast<f32x4 *>(w + 4 * g) = X0;
+      if (g == 0) *reinterpret_cast<f32x4 *>(w + 16) = X1;
+    }
+    if (lane == 0) small_mask[c] = mine;
+    __syncthreads();
+    const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
+    if (c == 0) {
+      const int64_t site = base + lane;
+      const bool sc = (all >> lane) & 1ull;
+      if (site < n) {
+        if (scaler) scaler[site] = (uint8_t)sc;
+        if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+      }
+    }
+    // coalesced store with the rescale of the scaled sites (exact: x 2^32)
+    {
+      f32x4 *dst = reinterpret_cast<f32x4 *>(x3 + base * 80);
+      f32x4 v[K];
+#pragma unroll
+      for (int i = 0; i < K; i++) {
+        const int j = threadIdx.x + i * kBlock;
+        const int sl = j / PT::kChunksPerSite, q = j - sl * PT::kChunksPerSite;
+        v[i] = tile[sl * PT::kStride + q];
+        if ((all >> sl) & 1ull) v[i] = v[i] * Num<float>::two32();
+      }
+      if (base + 64 <= n) {
+#pragma unroll
+        for (int i = 0; i < K; i++) __builtin_nontemporal_store(v[i], dst + threadIdx.x + i * kBlock);
+      } else {
+        const int64_t lim = (n - base) * PT::kChunksPerSite;
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+          const int j = threadIdx.x + i * kBlock;
+          if (j < lim) __builtin_nontemporal_store(v[i], dst + j);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
 }  // namespace dev
 }  // namespace plfx

@@ -79,6 +79,10 @@ int main(int argc, char **argv) {
   ADD("lds fma rows=4 packed", 1, (&plf_prot_lds_kernel<float, true, true, 2, 0, 4, true, true>))
   ADD("lds fma rows=20 packed", 1, (&plf_prot_lds_kernel<float, true, true, 2, 0, 20, true, true>))
   ADD("lds fma rows=4 packed no prefetch", 1, (&plf_prot_lds_kernel<float, true, true, 2, 0, 4, false, true>))
+  ADD("mfma32 fma", 1, (&plf_prot_mfma32_kernel<true, 2>))
+  ADD("mfma32 fma minw1", 1, (&plf_prot_mfma32_kernel<true, 1>))
+  ADD("mfma32 fma minw3", 1, (&plf_prot_mfma32_kernel<true, 3>))
+  ADD("mfma32 fma minw4", 1, (&plf_prot_mfma32_kernel<true, 4>))
   std::vector<uint32_t> ref[2], got(n * 80);
   std::vector<uint8_t> rsc[2], gsc(n);
   int64_t rsum[2] = {0, 0}, gsum = 0;
