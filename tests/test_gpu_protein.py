@@ -65,9 +65,9 @@ def test_protein_exact_matches_oracle(ctx, oracle, dtype, n):
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("n", [1, 17, 64, 100, 4097])
 def test_protein_fma_mode(ctx, oracle, dtype, n):
-    """FMA mode (f64: matrix cores, v_mfma_f64_16x16x4 = k-ordered fma chain;
-    f32: fused VALU) is bit-identical to the oracle's fma() restatement and
-    within 1e-12 (f64) of the unfused loop."""
+    """FMA mode (f64: v_mfma_f64_16x16x4 / 4x4x4, f32: v_mfma_f32_16x16x4 --
+    both k-ordered fma chains) is bit-identical to the oracle's fma()
+    restatement and within 1e-12 (f64) of the unfused loop."""
     x1, x2, EV, left, right, w = gen(n, dtype, 5 + n)
     x3, sc, s = run(ctx, x1, x2, EV, left, right, w, n, fma=True)
     f3, fsc, finc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
@@ -79,6 +79,21 @@ def test_protein_fma_mode(ctx, oracle, dtype, n):
         scale = np.abs(e3).reshape(n, V).max(axis=1, keepdims=True)   # cancellation-aware bound
         err = np.abs(x3 - e3).reshape(n, V) / scale
         assert err.max() <= FMA_RTOL
+
+
+@pytest.mark.parametrize("fma", [False, True])
+def test_protein_f32_many_trips(ctx, oracle, fma):
+    """f32 at 2^16 + 1 sites (every block runs several trips through the tile
+    prefetch, and the last tile is ragged): FMA mode on the matrix cores
+    (plf_prot_mfma32_kernel) bit-identical to the oracle's fmaf restatement,
+    exact mode (plf_prot_lds_kernel<float>) to plf()'s loop; scaler bytes and
+    the weighted sum exact."""
+    n = (1 << 16) + 1
+    x1, x2, EV, left, right, w = gen(n, np.float32, 77)
+    x3, sc, s = run(ctx, x1, x2, EV, left, right, w, n, fma=fma)
+    e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=fma)
+    assert np.array_equal(bits(x3), bits(e3))
+    assert np.array_equal(sc, esc) and s == einc and esc.sum() > 0
 
 
 def test_protein_full_size_256k(ctx, oracle):
