@@ -221,7 +221,7 @@ hipError_t launch_prot_exact64_t(const DnaArgs &a, int max_blocks, hipStream_t s
                                  const double *tipvec) {
   static int cache = 0;
   // 10-row groups + tile prefetch (tools/tune_prot.hip, profiles/r02_tune_protein_exact_rows.log)
-  auto kernel = &dev::plf_prot_lds_kernel<double, false, kSum, 2, kTips, 10>;
+  auto kernel = &dev::plf_prot_lds_kernel<double, false, kSum, 2, kTips, 10, true, false, true>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV,

@@ -391,7 +391,8 @@ __device__ __forceinline__ void pin_chains(T (&u)[R]) {
 // fetched into registers while the previous phase computes (the FMA kernel's
 // schedule): x2 during phase 1, the next trip's first dense child during
 // phases 2 and 3.
-template <typename T, bool kFma, bool kSum, int kTips, int kRows, bool kPf, bool kPack>
+template <typename T, bool kFma, bool kSum, int kTips, int kRows, bool kPf, bool kPack,
+          bool kE3S = false>
 __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T *__restrict__ x2,
                                               T *__restrict__ x3, const T *__restrict__ EV,
                                               const T *__restrict__ left, const T *__restrict__ right,
@@ -588,6 +589,23 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
             for (int j = 0; j < PV; j++) ring[(k + 2) % 3][j] = G[o + (S / E) * (k + 2) + j];
           }
           const V *e = ring[k % 3];
+          if constexpr (kE3S && !kPacked && !kFma) {
+            // tuning (kE3S): EV row k straight from global memory at a
+            // wave-uniform address -- scalar loads, SGPR operands -- instead
+            // of LDS broadcasts (one row ahead: the opaque offset)
+            int so = 0;
+            asm volatile("" : "+s"(so) : "v"(tok));
+            const T *er = EV + so + k * S + h * kPh3;
+            T pr[kPh3];
+#pragma unroll
+            for (int j = 0; j < kPh3; j++) pr[j] = U[k] * er[j];
+            pin_chains(pr);
+#pragma unroll
+            for (int j = 0; j < kPh3; j++) v[j] += pr[j];
+            pin_chains(v);
+            tok = v[kPh3 - 1];
+            continue;
+          }
           if constexpr (kPacked) {
             const f32x2 uv = {(float)U[k], (float)U[k]};
             if constexpr (kFma) {
@@ -660,21 +678,24 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
 // kPack (f32): chain pairs on v_pk_* -- faster in FMA mode (one v_pk_fma_f32
 // per two multiply-adds), slower in exact mode at 4-row groups
 // (tools/tune_prot32.hip, profiles/r02_tune_protein_f32.log).
+// kE3S (exact mode): phase 3's EV rows by scalar loads (SGPR operands) instead of
+// LDS broadcasts: 145.8 vs 148.8 us at 2^18 f64 (profiles/r02_tune_protein_exact_rows.log).
 template <typename T, bool kFma, bool kSum, int kMinWaves, int kTips, int kRows, bool kPf = true,
-          bool kPack = kFma>
+          bool kPack = kFma, bool kE3S = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_lds_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
                     const T *__restrict__ EV, const T *__restrict__ left, const T *__restrict__ right,
                     const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
                     unsigned long long *ws, int64_t *scaler_sum, const T *__restrict__ tipvec = nullptr) {
-  prot_lds_body<T, kFma, kSum, kTips, kRows, kPf, kPack>(x1, x2, x3, EV, left, right, wgt, scaler, n,
-                                                          ws, scaler_sum, tipvec);
+  prot_lds_body<T, kFma, kSum, kTips, kRows, kPf, kPack, kE3S>(x1, x2, x3, EV, left, right, wgt,
+                                                                scaler, n, ws, scaler_sum, tipvec);
 }
 
 // The round-1 EXACT f64 form, kept for same-process comparisons
 // (tools/tune_prot.hip): one chain per row k, the row streamed one ahead.
 // kRows > 0 runs the product body (plf_prot_lds_kernel) instead.
-template <bool kSum, int kMinWaves = 2, int kTips = 0, int kRows = 0, bool kPf = false>
+template <bool kSum, int kMinWaves = 2, int kTips = 0, int kRows = 0, bool kPf = false,
+          bool kE3S = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                           double *__restrict__ x3, const double *__restrict__ EV,
@@ -683,8 +704,8 @@ plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restric
                           unsigned long long *ws, int64_t *scaler_sum,
                           const double *__restrict__ tipvec = nullptr) {
   if constexpr (kRows > 0) {
-    prot_lds_body<double, false, kSum, kTips, kRows, kPf, false>(x1, x2, x3, EV, left, right, wgt,
-                                                                 scaler, n, ws, scaler_sum, tipvec);
+    prot_lds_body<double, false, kSum, kTips, kRows, kPf, false, kE3S>(
+        x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum, tipvec);
     return;
   } else {
   constexpr int S = 20;

@@ -182,8 +182,7 @@ int main(int argc, char **argv) {
   ADD_K("exact-lds rows=10", (&plf_prot_exact_f64_kernel<true, 2, 0, 10>), 64)
   ADD_K("exact-lds rows=4 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 4, true>), 64)
   ADD_K("exact-lds rows=10 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true>), 64)
-  ADD_K("exact-sgpr rows=4 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 4, true, true>), 64)
-  ADD_K("exact-sgpr rows=10 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true>), 64)
+  ADD_K("exact-lds rows=10 prefetch EV-sgpr", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true>), 64)
   ADD_K("mfma ablate: no matrix cores", (&plf_prot_mfma_kernel<true, 2, true, 1>), 64)
   ADD_K("mfma ablate: no HBM traffic", (&plf_prot_mfma_kernel<true, 2, true, 2>), 64)
   ADD_K("mfma 16x16x4 only (padded rows)", (&plf_prot_mfma_kernel<true, 2, true, 0, false>), 64)
