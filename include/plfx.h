@@ -136,7 +136,9 @@ int plfx_plf_dev_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *
  * [cat][k][l] (S*S per category), EV[k][l] (S*S).  flags: PLFX_EXACT keeps
  * plf()'s separate multiply/add and operation order (bit-identical to the
  * double/float instantiation of the reference loop); PLFX_FMA fuses each
- * multiply-add (one rounding per term, within 1e-12 relative; protein only,
+ * multiply-add (one rounding per term, within 1e-12 relative in f64; protein
+ * only, on the matrix cores -- v_mfma_f64_16x16x4 / v_mfma_f32_16x16x4 are
+ * k-ordered fma chains, so the result is bit-identical to a fused VALU loop;
  * DNA is always exact). */
 #define PLFX_EXACT 0
 #define PLFX_FMA 1
@@ -240,7 +242,7 @@ int plfx_plf_tips_dev(plfx_ctx *ctx, int dtype, const uint8_t *tip1, const void 
                       int64_t *scaler_sum, const void *tipvec, void *stream);
 
 /* plfx_plf_tips_dev for states 4 or 20 and flags as plfx_plf_dev_gen
- * (PLFX_FMA: protein f64 nodes on the matrix cores; DNA is always exact). */
+ * (PLFX_FMA: protein nodes on the f64 / f32 matrix cores; DNA is always exact). */
 int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const uint8_t *tip1,
                           const void *x1, const uint8_t *tip2, const void *x2, void *x3,
                           const void *EV, int64_t n, const void *left, const void *right,
@@ -255,8 +257,8 @@ int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const
  * six-level subtrees over dense leaves, three-level subtrees and level pairs
  * fused where possible (bit-identical results; env PLFX_FUSE=2 no six-level
  * passes, 1 pairs only, 0 none).  states 4 or 20; flags as
- * plfx_plf_dev_gen (PLFX_FMA: protein nodes on the f64 matrix cores; DNA is
- * always exact).  plfx_traverse == flags PLFX_EXACT, no tips, no tipvec. */
+ * plfx_plf_dev_gen (PLFX_FMA: protein nodes on the f64 / f32 matrix cores;
+ * DNA is always exact).  plfx_traverse == flags PLFX_EXACT, no tips, no tipvec. */
 int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const plfx_trav_op *ops,
                        int nops, void *const *clv, const uint8_t *const *tips, int nslots,
                        const void *pmats,
