@@ -114,6 +114,69 @@ cat_v(const float *__restrict__ x1, const float *__restrict__ x2, float *__restr
   block_ticket_sum(acc, ws, scaler_sum);
 }
 
+// roll: a rolling prefetch at step granularity -- right after step u of this
+// trip is computed and stored, step u of the wave's next trip is loaded into
+// the same registers, so loads stay in flight through the compute without a
+// second register set.  The trip count of every wave is fixed by the grid
+// (harness: full trips only), the last trip is peeled so no load sits in a
+// branch.
+template <int U>
+__global__ void __launch_bounds__(256, 1)
+cat_roll(const float *__restrict__ x1, const float *__restrict__ x2, float *__restrict__ x3,
+         const float *__restrict__ EV, const float *__restrict__ left, const float *__restrict__ right,
+         const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+         int64_t *scaler_sum) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 3, q = lane >> 2, nib = lane & 60;
+  const float m = Num<float>::minlik();
+  long long acc = 0;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  int64_t base = wave * 16 * U;
+  const int64_t T = base < n ? (n - base + stride - 1) / stride : 0;  // trips of this wave
+  float a[U][4], b[U][4];
+  int w[U];
+  auto ld = [&](int u, int64_t bs) {
+    const int64_t site = bs + u * 16 + q;
+    Num<float>::load4<true>(x1 + site * 16 + c * 4, a[u]);
+    Num<float>::load4<true>(x2 + site * 16 + c * 4, b[u]);
+    w[u] = wgt_at(wgt, site, ws);
+  };
+  if (T > 0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) ld(u, base);
+  }
+  float PL[16], PR[16], E[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) { PL[i] = left[c * 16 + i]; PR[i] = right[c * 16 + i]; E[i] = EV[i]; }
+  auto step = [&](int u, int64_t bs) {
+    const int64_t site = bs + u * 16 + q;
+    float o[4];
+    site_cat<float>(a[u], b[u], PL, PR, E, o);
+    const bool small = (Num<float>::abs(o[0]) < m) && (Num<float>::abs(o[1]) < m) &&
+                       (Num<float>::abs(o[2]) < m) && (Num<float>::abs(o[3]) < m);
+    const unsigned long long mask = __ballot(small);
+    const bool sc = ((mask >> nib) & 0xFull) == 0xFull;
+#pragma unroll
+    for (int l = 0; l < 4; l++) { const float s = o[l] * Num<float>::two32(); o[l] = sc ? s : o[l]; }
+    Num<float>::store4_nt(x3 + site * 16 + c * 4, o);
+    if (c == 0 && scaler) scaler[site] = (uint8_t)sc;
+    acc += (c == 0 && sc) ? (long long)w[u] : 0ll;
+  };
+  for (int64_t t = 0; t + 1 < T; t++, base += stride) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      step(u, base);
+      ld(u, base + stride);
+    }
+  }
+  if (T > 0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) step(u, base);
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
 __global__ void fill(float *p, int64_t n, uint64_t seed, float scale4) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
@@ -164,14 +227,14 @@ int main(int argc, char **argv) {
                          s.wgt, s.sc, n, ws, s.sum); }, {}});                                      \
   }
   ADD("csrc cat U=4 grid 2/CU (product)", (&plf_dna_kernel<float, 4, true, true, 1>), 256, 2)
+  ADD("roll U=4 2/CU", (&cat_roll<4>), 256, 2)
+  ADD("roll U=4 3/CU", (&cat_roll<4>), 256, 3)
+  ADD("roll U=2 4/CU", (&cat_roll<2>), 128, 4)
+  ADD("roll U=8 1/CU", (&cat_roll<8>), 512, 1)
+  ADD("roll U=8 2/CU", (&cat_roll<8>), 512, 2)
   ADD("peel U=4 2/CU", (&cat_v<4, true, false>), 256, 2)
   ADD("plain U=4 2/CU (harness form of csrc)", (&cat_v<4, false, false>), 256, 2)
-  ADD("group U=4 2/CU", (&cat_v<4, false, true>), 256, 2)
-  ADD("peel+group U=4 2/CU", (&cat_v<4, true, true>), 256, 2)
   ADD("peel+group U=4 4/CU", (&cat_v<4, true, true>), 256, 4)
-  ADD("peel U=2 4/CU", (&cat_v<2, true, false>), 128, 4)
-  ADD("peel+group U=2 4/CU", (&cat_v<2, true, true>), 128, 4)
-  ADD("peel U=8 1/CU", (&cat_v<8, true, false>), 512, 1)
   ADD("csrc cat U=4 nosum 2/CU", (&plf_dna_kernel<float, 4, false, true, 1>), 256, 2)
   {
     const size_t bytes = n * 64;
