@@ -179,12 +179,14 @@ hipError_t launch_lnl_t(const T *x, int64_t n, const double *catw, const double 
 template <typename T, bool kFma, bool kSum, int kTips>
 hipError_t launch_prot_t(const DnaArgs &a, int max_blocks, hipStream_t s, const T *tipvec) {
   static_assert(sizeof(T) == 4, "f32 protein; f64 runs launch_prot_mfma_t / launch_prot_exact64_t");
-  // f32: FMA mode on the matrix cores (v_mfma_f32_16x16x4_f32 = fmaf chain),
-  // exact mode on the LDS-matrix kernel (4-row groups, tile prefetch)
+  // f32: FMA mode on the matrix cores (v_mfma_f32_16x16x4_f32 = fmaf chain;
+  // rows 16..19 of the products and the back-transform on 4x4x1_16b, kQ = 2:
+  // 52.4 -> 46.5 us at 2^18, profiles/r02_tune_protein_f32_q.log), exact mode
+  // on the LDS-matrix kernel (4-row groups, tile prefetch)
   // (tools/tune_prot32.hip, profiles/r02_tune_protein_f32.log)
   if constexpr (kFma) {
     static int cache = 0;
-    auto kernel = &dev::plf_prot_mfma32_kernel<kSum, 3, kTips>;
+    auto kernel = &dev::plf_prot_mfma32_kernel<kSum, 3, kTips, 2>;
     const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
     hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
                        (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,

@@ -1179,9 +1179,43 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
 // Per 16-site sub-tile and category: 20 + 10 MFMAs of 32 cycles (960 cycles;
 // f32 has no 4x4x4 form for rows 16..19).  Tiles as the f64 kernel (prefetch:
 // x2 during phase 1, the next trip's first dense child during phase 2).
+//
+// kQ >= 1: rows 16..19 of both child products on v_mfma_f32_4x4x1_16b_f32
+// instead of a zero-padded 16x16x4 tile.  Its maps (probed on the MI355X,
+// tools/probes/mfma_f32_4x4x1.hip: block b = lane/4, A lane l = A_b[l%4][0],
+// B lane l = B_b[0][l%4], D lane l reg r = D_b[r][l%4]; 20 chained K = 1 steps
+// are bit for bit a k-ordered fmaf chain) give, with A = P[16 + l%4][col] and
+// B = x[site l][col], lane l = the trip's site l holding U[16..19] of its own
+// site after 20 steps (14 cycles each) for all 64 sites at once -- 280 cycles
+// per product and trip instead of 640.  One 4x4 transpose of (lane group x
+// register) by v_permlane32_swap + v_permlane16_swap then hands lane group g
+// the k = 16 + g row of every sub-tile, the back-transform's B fragment of
+// k-step 4.  kQ = 2: the back-transform's states 16..19 the same way (B =
+// p[k][site l] for all 20 k: the rows 0..15 brought to lane l by four more
+// transposes), so a lane writes states 16..19 of its site as one 16-B row.
 typedef float f32x4m __attribute__((ext_vector_type(4)));
 
-template <bool kSum, int kMinWaves = 2, int kTips = 0>
+// 4x4 transpose of (lane group g = lane >> 4) x (register r) on 32-bit values:
+// afterwards v[r] of group g holds what v[g] of group r held.  (Unsigned
+// values; convert with __float_as_uint / __uint_as_float: __builtin_bit_cast of
+// a vector element, e.g. a builtin's pair result p[1], reads element 0 with
+// this compiler.)
+__device__ __forceinline__ void transpose_groups44(unsigned (&v)[4]) {
+#pragma unroll
+  for (int r = 0; r < 2; r++) {  // off-diagonal 2x2 blocks: groups 2,3 of v[r] <-> groups 0,1 of v[r+2]
+    const auto p = __builtin_amdgcn_permlane32_swap(v[r], v[r + 2], false, false);
+    v[r] = p[0];
+    v[r + 2] = p[1];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r += 2) {  // inside each block: odd groups of v[r] <-> even groups of v[r+1]
+    const auto p = __builtin_amdgcn_permlane16_swap(v[r], v[r + 1], false, false);
+    v[r] = p[0];
+    v[r + 1] = p[1];
+  }
+}
+
+template <bool kSum, int kMinWaves = 2, int kTips = 0, int kQ = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x2,
                        float *__restrict__ x3, const float *__restrict__ EV,
@@ -1209,11 +1243,27 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
     for (int st = 0; st < 5; st++) {
       const int i = lo16, col = 4 * st + g;
       const int k = 16 * mt + 4 * (i & 3) + (i >> 2);  // pi: accumulators = back-transform B fragments
-      AL[mt][st] = k < S ? left[c * S * S + k * S + col] : 0.f;   // P_L[k][l]
-      AR[mt][st] = k < S ? right[c * S * S + k * S + col] : 0.f;
+      AL[mt][st] = (k < S && !(kQ && mt)) ? left[c * S * S + k * S + col] : 0.f;   // P_L[k][l]
+      AR[mt][st] = (k < S && !(kQ && mt)) ? right[c * S * S + k * S + col] : 0.f;
       const int lrow = 16 * mt + i;  // EV^T[l][k]: natural rows
-      AE[mt][st] = lrow < S ? EV[col * S + lrow] : 0.f;
+      AE[mt][st] = (lrow < S && !(kQ == 2 && mt)) ? EV[col * S + lrow] : 0.f;
     }
+  // kQ: A operands of the 4x4x1 chains in LDS (registers would cost 40-60
+  // VGPRs and the third block per CU): qm[0|1][cat][i][col] = P_L|P_R[16+i][col],
+  // qm[2][0][i][k] = EV[k][16+i]; lane l reads row i = l%4 (4 distinct 16-B
+  // addresses per 16 lanes, 20 banks apart: no conflicts)
+  __shared__ float qm[kQ ? 3 : 1][kQ ? 4 : 1][4][kQ ? S : 1];
+  if constexpr (kQ) {
+    for (int e = threadIdx.x; e < 4 * 4 * S; e += kBlock) {
+      const int cc = e / (4 * S), i = (e / S) & 3, j = e % S;
+      qm[0][cc][i][j] = T1 ? 0.f : left[cc * S * S + (16 + i) * S + j];
+      qm[1][cc][i][j] = T2 ? 0.f : right[cc * S * S + (16 + i) * S + j];
+      if (cc == 0) qm[2][0][i][j] = EV[j * S + 16 + i];
+    }
+    __syncthreads();
+  }
+  const float *QL = &qm[0][kQ ? c : 0][lane & 3][0], *QR = &qm[kQ ? 1 : 0][kQ ? c : 0][lane & 3][0];
+  const float *QE = &qm[kQ ? 2 : 0][0][lane & 3][0];
   const float m = Num<float>::minlik();
   __shared__ float tabs[(T1 ? 1 : 0) + (T2 ? 1 : 0) + (T1 ? 0 : 1)][T1 ? 4 * kProtCodes * 20 : 1];
   if constexpr (T1) build_prot_tip_table<float, true>(left, tipvec, tabs[0]);
@@ -1231,8 +1281,11 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
   const float *td = reinterpret_cast<const float *>(tile);
   float *tw = reinterpret_cast<float *>(tile);
   long long acc = 0;
-  // one child's product U^T for the 4 sub-tiles from the LDS tile (mul: into P)
-  auto product = [&](const float (&A)[2][5], f32x4 (&P)[4][2], bool mul) {
+  // one child's product U^T for the 4 sub-tiles from the LDS tile (mul: into P);
+  // kQ: rows 16..19 of the lane's own site into Q (4x4x1 chain, k ascending)
+  auto product = [&](const float (&A)[2][5], const float *QA, f32x4 (&P)[4][2], f32x4 &Q, bool mul) {
+    f32x4 q = {0.f, 0.f, 0.f, 0.f};
+    const float *xs = td + lane * kRow + c * S;  // the lane's own site row
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       const float *xr = td + (16 * t + lo16) * kRow + c * S + g;
@@ -1240,22 +1293,45 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
 #pragma unroll
       for (int st = 0; st < 5; st++) bv[st] = xr[4 * st];
 #pragma unroll
-      for (int mt = 0; mt < 2; mt++) {
+      for (int mt = 0; mt < (kQ ? 1 : 2); mt++) {
         f32x4 u = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int st = 0; st < 5; st++) u = __builtin_amdgcn_mfma_f32_16x16x4f32(A[mt][st], bv[st], u, 0, 0, 0);
         P[t][mt] = mul ? P[t][mt] * u : u;  // prod[k] = umpL[k] * umpR[k]
       }
+      if constexpr (kQ) {  // four of the 20 K = 1 steps per sub-tile, interleaved
+        const f32x4 xv = *reinterpret_cast<const f32x4 *>(xs + 4 * t);
+        const f32x4 av = *reinterpret_cast<const f32x4 *>(QA + 4 * t);
+#pragma unroll
+        for (int j = 0; j < 4; j++) q = __builtin_amdgcn_mfma_f32_4x4x1f32(av[j], xv[j], q, 0, 0, 0);
+      }
+    }
+    if constexpr (kQ) {
+      const f32x4 xv = *reinterpret_cast<const f32x4 *>(xs + 16);
+      const f32x4 av = *reinterpret_cast<const f32x4 *>(QA + 16);
+#pragma unroll
+      for (int j = 0; j < 4; j++) q = __builtin_amdgcn_mfma_f32_4x4x1f32(av[j], xv[j], q, 0, 0, 0);
+      Q = mul ? Q * q : q;
     }
   };
   for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
     f32x4 P[4][2];
+    f32x4 Q = {0.f, 0.f, 0.f, 0.f};  // kQ: U[16..19] (then p[16..19]) of site `lane`
+    if constexpr (kQ)  // rows 16..19 live in Q: the padded tiles stay zero (and unused)
+#pragma unroll
+      for (int t = 0; t < 4; t++) P[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int64_t sq = base + lane < n ? base + lane : n - 1;
     const int code1 = T1 ? prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) : 0;
     const int code2 = T2 ? prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) : 0;
+    // kQ: a tip child's U[16..19] of the lane's own site from its table row
+    auto tip_q = [&](const float *tab, int code_lane) -> f32x4 {
+      const float *r = tab + c * kProtCodes * 20 + code_lane * 20 + 16;
+      return f32x4{r[0], r[1], r[2], r[3]};
+    };
     if constexpr (T1) {
 #pragma unroll
       for (int t = 0; t < 4; t++) tip_u(tabs[0], code1, t, P[t][0], P[t][1]);
+      if constexpr (kQ) Q = tip_q(tabs[0], code1);
     } else {
       tile_put<float>(tile, pf);
       __syncthreads();
@@ -1265,7 +1341,7 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
       } else {
         tile_fetch<float>(x2, base, n, pf);
       }
-      product(AL, P, false);
+      product(AL, QL, P, Q, false);
       __syncthreads();
     }
     if constexpr (T2) {
@@ -1276,35 +1352,68 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
         P[t][0] = P[t][0] * u0;
         P[t][1] = P[t][1] * u1;
       }
+      if constexpr (kQ) Q = Q * tip_q(tabs[1], code2);
     } else {
       tile_put<float>(tile, pf);
       __syncthreads();
       if (base + stride < n) tile_fetch<float>(T1 ? x2 : x1, base + stride, n, pf);
-      product(AR, P, true);
+      product(AR, QR, P, Q, true);
       __syncthreads();  // every wave is done reading x2: the tile takes X3 now
     }
-    // back-transform: B fragment of k-step s = P[t][s >> 2][s & 3]
+    // kQ: lane group g gets p[16 + g] of sub-tile t's site lo16 as Qt[t]
+    // (__float_as_uint: __builtin_bit_cast of a vector element reads element 0
+    // with this compiler)
+    unsigned Qt[4] = {__float_as_uint(Q[0]), __float_as_uint(Q[1]), __float_as_uint(Q[2]),
+                      __float_as_uint(Q[3])};
+    if constexpr (kQ) transpose_groups44(Qt);
+    // kQ == 2: p[k][site lane] for k = 0..15 (four transposes of the P rows)
+    unsigned pk[kQ == 2 ? 16 : 1];
+    if constexpr (kQ == 2) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        unsigned v[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) v[t] = __float_as_uint(P[t][0][r]);
+        transpose_groups44(v);  // lane (t, lo16) reg g' = p[4r + g'][site 16t + lo16]
+#pragma unroll
+        for (int gg = 0; gg < 4; gg++) pk[4 * r + gg] = v[gg];
+      }
+    }
+    // back-transform: B fragment of k-step s = P[t][s >> 2][s & 3] (kQ: k-step 4 = Qt[t])
     unsigned long long mine = 0;
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       f32x4 X0 = {0.f, 0.f, 0.f, 0.f}, X1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int st = 0; st < 5; st++) {
-        const float b = P[t][st >> 2][st & 3];
+        const float b = (kQ && st == 4) ? __uint_as_float(Qt[t]) : P[t][st >> 2][st & 3];
         X0 = __builtin_amdgcn_mfma_f32_16x16x4f32(AE[0][st], b, X0, 0, 0, 0);
-        X1 = __builtin_amdgcn_mfma_f32_16x16x4f32(AE[1][st], b, X1, 0, 0, 0);
+        if constexpr (kQ != 2) X1 = __builtin_amdgcn_mfma_f32_16x16x4f32(AE[1][st], b, X1, 0, 0, 0);
       }
       // lane group g holds states 4g..4g+3 (X0) and, for g = 0, 16..19 (X1)
       bool small = (__builtin_fabsf(X0[0]) < m) && (__builtin_fabsf(X0[1]) < m) &&
                    (__builtin_fabsf(X0[2]) < m) && (__builtin_fabsf(X0[3]) < m);
-      if (g == 0)
+      if (kQ != 2 && g == 0)
         small = small && (__builtin_fabsf(X1[0]) < m) && (__builtin_fabsf(X1[1]) < m) &&
                 (__builtin_fabsf(X1[2]) < m) && (__builtin_fabsf(X1[3]) < m);
       const unsigned long long b = __ballot(small);
       mine |= (b & (b >> 16) & (b >> 32) & (b >> 48) & 0xFFFFull) << (16 * t);
       float *w = tw + (16 * t + lo16) * kRow + c * S;
       *reinterpret_cast<f32x4 *>(w + 4 * g) = X0;
-      if (g == 0) *reinterpret_cast<f32x4 *>(w + 16) = X1;
+      if (kQ != 2 && g == 0) *reinterpret_cast<f32x4 *>(w + 16) = X1;
+    }
+    if constexpr (kQ == 2) {  // states 16..19 of site `lane`: 20 K = 1 steps, k ascending
+      f32x4 X1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 20; k++) {
+        const float a = reinterpret_cast<const f32x4 *>(QE)[k >> 2][k & 3];
+        const float b = k < 16 ? __uint_as_float(pk[k & 15]) : Q[k & 3];
+        X1 = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, X1, 0, 0, 0);
+      }
+      const bool small = (__builtin_fabsf(X1[0]) < m) && (__builtin_fabsf(X1[1]) < m) &&
+                         (__builtin_fabsf(X1[2]) < m) && (__builtin_fabsf(X1[3]) < m);
+      mine &= __ballot(small);
+      *reinterpret_cast<f32x4 *>(tw + lane * kRow + c * S + 16) = X1;
     }
     if (lane == 0) small_mask[c] = mine;
     __syncthreads();

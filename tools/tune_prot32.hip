@@ -38,7 +38,7 @@ struct Set { float *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
 
 int main(int argc, char **argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : (1 << 18);
-  const int R = 4, reps = argc > 2 ? atoi(argv[2]) : 40, rounds = 3;
+  const int R = 4, reps = argc > 2 ? atoi(argv[2]) : 40, rounds = 5;
   hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
   const int CUs = prop.multiProcessorCount;
   std::vector<Set> sets(R);
@@ -68,6 +68,8 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
                          s.wgt, s.sc, n, ws, s.sum, nullptr); }, {}});                              \
   }
+  const bool q = argc > 3 && atoi(argv[3]) == 1;  // round-2 kQ session: FMA kernels only
+  if (!q) {
   ADD("readlane exact (r01 product)", 0, (&plf_prot_kernel<float, false, true>))
   ADD("readlane fma (r01 product)", 1, (&plf_prot_kernel<float, true, true>))
   ADD("lds exact rows=4", 0, (&plf_prot_lds_kernel<float, false, true, 2, 0, 4, true, false>))
@@ -83,6 +85,18 @@ int main(int argc, char **argv) {
   ADD("mfma32 fma minw1", 1, (&plf_prot_mfma32_kernel<true, 1>))
   ADD("mfma32 fma minw3", 1, (&plf_prot_mfma32_kernel<true, 3>))
   ADD("mfma32 fma minw4", 1, (&plf_prot_mfma32_kernel<true, 4>))
+  } else {
+  // rows 16..19 on v_mfma_f32_4x4x1_16b (kQ = 1: the products; 2: also the
+  // back-transform), against the readlane FMA kernel (the check) and the product
+  ADD("readlane fma (r01, the check)", 1, (&plf_prot_kernel<float, true, true>))
+  ADD("mfma32 fma minw3 (product)", 1, (&plf_prot_mfma32_kernel<true, 3>))
+  ADD("mfma32 fma minw3 kQ=1", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 1>))
+  ADD("mfma32 fma minw3 kQ=2", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2>))
+  ADD("mfma32 fma minw2 kQ=1", 1, (&plf_prot_mfma32_kernel<true, 2, 0, 1>))
+  ADD("mfma32 fma minw2 kQ=2", 1, (&plf_prot_mfma32_kernel<true, 2, 0, 2>))
+  ADD("mfma32 fma minw4 kQ=2", 1, (&plf_prot_mfma32_kernel<true, 4, 0, 2>))
+  ADD("mfma32 fma minw3 (product, again)", 1, (&plf_prot_mfma32_kernel<true, 3>))
+  }
   std::vector<uint32_t> ref[2], got(n * 80);
   std::vector<uint8_t> rsc[2], gsc(n);
   int64_t rsum[2] = {0, 0}, gsum = 0;
@@ -101,6 +115,7 @@ int main(int argc, char **argv) {
            bad == 0 && gsum == rsum[v.mode] ? "bit-exact" : "DIFFERS", (long long)bad, (long long)gsum);
   }
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int i = 0; i < 300; i++) vs[1].run(sets[i % R]);  // past the first launches' transient
   for (int round = 0; round < rounds; round++)
     for (auto &v : vs) {
       for (int i = 0; i < 3; i++) v.run(sets[i % R]);
