@@ -896,9 +896,17 @@ __device__ __forceinline__ void swap_rows16(double &v, double &w) {
 // compiler pairs the k-steps 32 B apart into ds_read2_b64, which banks mod 32
 // in 16-lane groups (sites lo16 and lo16+8 collide: 2-way) and takes 8 LDS
 // cycles instead of 2 x 2.
+// kSwz (with kPrefetch, kX3 = 2): the two doubles of every 16-B chunk of the
+// tile rows of sites 8..15 of each 16-site group are stored swapped (double
+// index d -> d ^ 1 in those rows).  The paired B reads keep their ds_read2_b64
+// (the pair's 32-B offset is unchanged by the swap) but sites lo16 and lo16+8
+// now start 8 B apart, so the 16 lanes of a read2 group cover all 32 banks
+// once; the rows-16..19 ds_write_b64 of X3 becomes conflict-free the same way.
+// The b128 tile writes and the store pass move whole chunks and swap the two
+// halves back with a select (tools/lds_banks.py, swizzle rows).
 template <bool kSum, int kMinWaves = 2, bool kPrefetch = true, int kAblate = 0, bool kMix4 = true,
           int kTips = 0, int kX3 = 0, bool kEarly = false, bool kFirstX2 = false,
-          bool kSplitB = false>
+          bool kSplitB = false, bool kSwz = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                      double *__restrict__ x3, const double *__restrict__ EV,
@@ -957,6 +965,22 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   const double *td = reinterpret_cast<const double *>(tile);
   double *tw = reinterpret_cast<double *>(tile);
   long long acc = 0;
+  static_assert(!kSwz || (kPrefetch && kX3 == 2), "kSwz: the prefetch path with kX3 = 2");
+  const int sw = kSwz ? (lo16 >> 3) & 1 : 0;  // this lane's rows are swizzled
+  auto swap2 = [](f64x2 v, bool on) { return on ? f64x2{v.y, v.x} : v; };
+  // a prefetched child tile into LDS (kSwz: halves of the swizzled rows swapped)
+  auto put = [&](const f64x2 (&v)[PT::kChunks / kBlock]) {
+    if constexpr (kSwz) {
+#pragma unroll
+      for (int i = 0; i < PT::kChunks / kBlock; i++) {
+        const int j = threadIdx.x + i * kBlock;
+        const int s_ = j / PT::kChunksPerSite, q = j - s_ * PT::kChunksPerSite;
+        tile[s_ * PT::kStride + q] = swap2(v[i], (s_ >> 3) & 1);
+      }
+    } else {
+      tile_put<double>(tile, v);
+    }
+  };
   // the five B-fragment values of sub-tile row xr (kSplitB: each read from its
   // own laundered LDS address, so no two are paired into a ds_read2_b64)
   auto bfrag = [&](const double *xr, double (&bv)[5]) {
@@ -984,7 +1008,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
 #pragma unroll
       for (int t = 0; t < 4; t++) tip_u(tabs[0], code1, t, P[t][0], P[t][1]);
     } else if constexpr (kPrefetch) {
-      tile_put<double>(tile, pf);
+      put(pf);
       __syncthreads();
       if constexpr (kFirst && kX2Early) {
 #pragma unroll
@@ -1000,7 +1024,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         double bv[5];
-        bfrag(td + (16 * t + lo16) * kRow + c * S + g, bv);
+        bfrag(td + (16 * t + lo16) * kRow + c * S + (g ^ sw), bv);
 #pragma unroll
         for (int mt = 0; mt < 2; mt++) {
           f64x4 u = {0.0, 0.0, 0.0, 0.0};
@@ -1025,7 +1049,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       }
     } else {
     if constexpr (kPrefetch) {
-      tile_put<double>(tile, pf);
+      put(pf);
       __syncthreads();
       // next trip's first dense child: x1, or x2 when x1 is a tip
       if (kAblate != 2 && base + stride < n) tile_fetch<double>(T1 ? x2 : x1, base + stride, n, pf);
@@ -1036,7 +1060,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       double bv[5];
-      bfrag(td + (16 * t + lo16) * kRow + c * S + g, bv);
+      bfrag(td + (16 * t + lo16) * kRow + c * S + (g ^ sw), bv);
 #pragma unroll
       for (int mt = 0; mt < 2; mt++) {
         f64x4 u = {0.0, 0.0, 0.0, 0.0};
@@ -1076,9 +1100,9 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       mine |= (b & (b >> 16) & (b >> 32) & (b >> 48) & 0xFFFFull) << (16 * t);
       double *w = tw + (16 * t + lo16) * kRow + c * S;
       if constexpr (kX3 == 2) {
-        *reinterpret_cast<f64x2 *>(w + 4 * g) = f64x2{X0[0], X0[1]};
-        *reinterpret_cast<f64x2 *>(w + 4 * g + 2) = f64x2{X0[2], X0[3]};
-        w[16 + g] = X1[0];
+        *reinterpret_cast<f64x2 *>(w + 4 * g) = swap2(f64x2{X0[0], X0[1]}, sw);
+        *reinterpret_cast<f64x2 *>(w + 4 * g + 2) = swap2(f64x2{X0[2], X0[3]}, sw);
+        w[16 + (g ^ sw)] = X1[0];
       } else if constexpr (kX3 == 3) {
         // kX3 == 2, and states 16..19 as 16-B pairs: after swap_rows16(X1,
         // copy) the lanes of even rows hold (16 + g, 17 + g)
@@ -1129,6 +1153,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
         const int j = threadIdx.x + i * kBlock;
         const int sl = j / PT::kChunksPerSite, q = j - sl * PT::kChunksPerSite;
         v[i] = tile[sl * PT::kStride + q];
+        if constexpr (kSwz) v[i] = swap2(v[i], (sl >> 3) & 1);
         if ((all >> sl) & 1ull) v[i] = v[i] * Num<double>::two32();
       }
       if (kAblate == 2) {

@@ -200,6 +200,12 @@ int main(int argc, char **argv) {
   ADD_K("mfma v3 permX3+early+splitB", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, true>), 64)
   ADD_K("mfma v3 permX3b128+early", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 3, true, false, false>), 64)
   ADD_K("mfma v3 permX3b128+early+splitB", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 3, true, false, true>), 64)
+  // round 2: tile rows of sites 8..15 of each 16-site group stored with their
+  // chunk halves swapped (kSwz): the paired B reads and the rows-16..19 X3
+  // writes become conflict-free (tools/lds_banks.py)
+  ADD_K("mfma v5 permX3+early+swz", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, false, true>), 64)
+  ADD_K("mfma v5 permX3+early (product form)", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
+  ADD_K("mfma v5 permX3+early+swz again", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, false, true>), 64)
   ADD_KT("mfma v8 perm late", (&plf_prot_mfma8_kernel<true, true, false, 64>), 64)
   ADD_KT("mfma v4x2 perm late", (&plf_prot_mfma8_kernel<true, true, false, 32>), 32)
   ADD_KT("mfma v4x2 perm early", (&plf_prot_mfma8_kernel<true, true, true, 32>), 32)
