@@ -65,9 +65,10 @@ def test_protein_exact_matches_oracle(ctx, oracle, dtype, n):
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("n", [1, 17, 64, 100, 4097])
 def test_protein_fma_mode(ctx, oracle, dtype, n):
-    """FMA mode (f64: v_mfma_f64_16x16x4 / 4x4x4, f32: v_mfma_f32_16x16x4 --
-    both k-ordered fma chains) is bit-identical to the oracle's fma()
-    restatement and within 1e-12 (f64) of the unfused loop."""
+    """FMA mode (f64: v_mfma_f64_16x16x4 / 4x4x4, f32: v_mfma_f32_16x16x4 with
+    rows 16..19 on 4x4x1_16b and permlane transposes -- all k-ordered fma
+    chains) is bit-identical to the oracle's fma() restatement and within
+    1e-12 (f64) of the unfused loop."""
     x1, x2, EV, left, right, w = gen(n, dtype, 5 + n)
     x3, sc, s = run(ctx, x1, x2, EV, left, right, w, n, fma=True)
     f3, fsc, finc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
