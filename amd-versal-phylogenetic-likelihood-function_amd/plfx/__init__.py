@@ -522,13 +522,15 @@ class Context:
 
         S = states
         for k, t in (("eigen", eigen), ("rates", rates), ("blen", blen)):
-            if t.dtype != torch.float64 or not t.is_contiguous():
+            if t.dtype != torch.float64 or not t.is_contiguous() or not t.is_cuda:
                 raise PlfxError(ERR_INVALID, f"{k} must be a contiguous float64 device tensor")
         if eigen.numel() < S + 2 * S * S:
             raise PlfxError(ERR_INVALID, "eigen too small")
         ncat, nb = rates.numel(), blen.numel()
-        if out.dtype not in (torch.float32, torch.float64) or out.numel() < nb * ncat * S * S:
-            raise PlfxError(ERR_INVALID, "out must hold nbranch*ncat*S*S float values")
+        if (out.dtype not in (torch.float32, torch.float64) or out.numel() < nb * ncat * S * S
+                or not out.is_cuda or not out.is_contiguous()):
+            raise PlfxError(ERR_INVALID, "out must be a contiguous device tensor of nbranch*ncat*S*S "
+                                         "float values")
         self._check(self._L.plfx_pmatrix(
             self.h, F32 if out.dtype == torch.float32 else F64, S, convention,
             C.c_void_p(eigen.data_ptr()), C.c_void_p(rates.data_ptr()), ncat,
@@ -540,13 +542,20 @@ class Context:
         """Root lnL into `out` (float64 device tensor, 1 element); see plfx.h (7)."""
         import torch
 
-        if out.dtype != torch.float64 or out.numel() < 1:
+        if out.dtype != torch.float64 or out.numel() < 1 or not out.is_cuda:
             raise PlfxError(ERR_INVALID, "out must be a float64 device tensor")
-        if x.numel() < 4 * states * n:
-            raise PlfxError(ERR_INVALID, "x too small")
-        for t, k in ((catw, 4), (freq, states)):
-            if t is not None and (t.dtype != torch.float64 or t.numel() < k):
-                raise PlfxError(ERR_INVALID, "catw/freq must be float64 device tensors")
+        if (x.dtype not in (torch.float32, torch.float64) or x.numel() < 4 * states * n
+                or not x.is_cuda or not x.is_contiguous()):
+            raise PlfxError(ERR_INVALID, "x must be a contiguous float device tensor of >= 4*S*n values")
+        for t, k in ((catw, 4), (freq, states), (site_lnl, n)):
+            if t is not None and (t.dtype != torch.float64 or t.numel() < k or not t.is_cuda
+                                  or not t.is_contiguous()):
+                raise PlfxError(ERR_INVALID, "catw/freq/site_lnl must be contiguous float64 device "
+                                             "tensors (4 / S / n values)")
+        _check_aux(n, wgt, None, None)
+        if scaler_sums is not None and (scaler_sums.dtype != torch.int64 or not scaler_sums.is_cuda
+                                        or not scaler_sums.is_contiguous()):
+            raise PlfxError(ERR_INVALID, "scaler_sums must be a contiguous int64 device tensor")
         p = lambda t: C.c_void_p(None if t is None else t.data_ptr())  # noqa: E731
         nsums = 0 if scaler_sums is None else scaler_sums.numel()
         self._check(self._L.plfx_root_lnl(self.h, F32 if x.dtype == torch.float32 else F64, states,
@@ -561,8 +570,7 @@ class Context:
             n = scaler.numel()
         if scaler.dtype != torch.uint8 or out_sum.dtype != torch.int64:
             raise PlfxError(ERR_INVALID, "scaler uint8, out_sum int64")
-        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n):
-            raise PlfxError(ERR_INVALID, "wgt int32 with >= n elements")
+        _check_aux(n, wgt, scaler, out_sum)
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         self._check(self._L.plfx_scaler_sum(self.h, p(scaler), p(wgt), int(n), p(out_sum),
                                             _stream_handle(stream, self.device)))

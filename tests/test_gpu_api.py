@@ -175,3 +175,44 @@ def test_nodes64_full_size_windows(ctx, oracle):
         assert int(nd["scaler"].sum().item()) >= n // 4
     del nodes
     torch.cuda.empty_cache()
+
+
+def test_binding_rejects_host_or_mistyped_tensors(ctx):
+    """The Python binding checks every tensor a kernel would read or write
+    (the C ABI cannot see sizes or devices): host tensors, wrong dtypes and
+    short buffers raise PlfxError before any launch."""
+    import plfx
+    import torch
+
+    n = 64
+    x = torch.zeros(16 * n, dtype=torch.float64, device="cuda")
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    bad_root = [
+        dict(x=x.cpu(), out=out),                                      # host CLV
+        dict(x=x.float()[: 8 * n], out=out),                            # short CLV
+        dict(x=x, out=out.cpu()),                                       # host output
+        dict(x=x, out=out, wgt=torch.ones(n, dtype=torch.int64, device="cuda")),
+        dict(x=x, out=out, scaler_sums=torch.zeros(1, dtype=torch.int32, device="cuda")),
+        dict(x=x, out=out, site_lnl=torch.zeros(n - 1, dtype=torch.float64, device="cuda")),
+        dict(x=x, out=out, freq=torch.full((4,), 0.25, dtype=torch.float64)),
+    ]
+    for kw in bad_root:
+        with pytest.raises(plfx.PlfxError):
+            ctx.root_lnl(kw.pop("x"), n, kw.pop("out"), **kw)
+    sc = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for args in ((sc.cpu(), None, s), (sc, None, s.cpu()), (sc[: n - 1], None, s),
+                 (sc, torch.ones(n, dtype=torch.int32), s)):
+        with pytest.raises(plfx.PlfxError):
+            ctx.scaler_sum(*args, n=n)
+    e = torch.zeros(4 + 32, dtype=torch.float64, device="cuda")
+    r = torch.ones(4, dtype=torch.float64, device="cuda")
+    b = torch.ones(3, dtype=torch.float64, device="cuda")
+    pm = torch.zeros(3 * 4 * 16, dtype=torch.float64, device="cuda")
+    for args in ((e.cpu(), r, b, pm), (e, r, b, pm.cpu()), (e, r.float(), b, pm)):
+        with pytest.raises(plfx.PlfxError):
+            ctx.pmatrix(*args)
+    # the valid forms still run
+    ctx.scaler_sum(sc, None, s, n=n)
+    torch.cuda.synchronize()
+    assert int(s.item()) == 0
