@@ -391,14 +391,22 @@ __device__ __forceinline__ void pin_chains(T (&u)[R]) {
 // fetched into registers while the previous phase computes (the FMA kernel's
 // schedule): x2 during phase 1, the next trip's first dense child during
 // phases 2 and 3.
+// kPS (tuning, exact mode, dense children): phase 1 (bit 0) / phase 2 (bit 1)
+// reads its matrix as SGPR operands by scalar loads from a group-transposed
+// global copy (pl_t / pr_t: [c][k / kRows][l][k % kRows], prot_group_transpose)
+// instead of LDS broadcasts, one column ahead; a null copy keeps the LDS path.
+// Bit-identical; within the run-to-run spread of the LDS form on two boxes
+// (profiles/r02_tune_protein_exact_sgpr.log), so the product keeps the LDS form.
 template <typename T, bool kFma, bool kSum, int kTips, int kRows, bool kPf, bool kPack,
-          bool kE3S = false>
+          bool kE3S = false, int kPS = 0>
 __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T *__restrict__ x2,
                                               T *__restrict__ x3, const T *__restrict__ EV,
                                               const T *__restrict__ left, const T *__restrict__ right,
                                               const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler,
                                               int64_t n, unsigned long long *ws, int64_t *scaler_sum,
-                                              const T *__restrict__ tipvec) {
+                                              const T *__restrict__ tipvec,
+                                              const T *__restrict__ pl_t = nullptr,
+                                              const T *__restrict__ pr_t = nullptr) {
   constexpr int S = 20;
   constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
   using PT = ProtTile<T>;
@@ -442,10 +450,45 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
   long long acc = 0;
   __syncthreads();
   // phases 1/2: M = the category's group-transposed matrix, x = the child's 20
-  // values; fn(k, sum_l x[l] * M[k][l]) for every k
-  auto gphase = [&](const V *M, const T (&x)[S], auto &&fn) {
+  // values; fn(k, sum_l x[l] * M[k][l]) for every k.  gsrc (kPS): the same
+  // layout in global memory, read by scalar loads (SGPR operands)
+  auto gphase = [&](const V *M, const T (&x)[S], auto &&fn, const T *gsrc = nullptr) {
     int o = 0;
     T tok = T(0);
+    if constexpr (kPS != 0 && !kFma && !kPacked) {
+      if (gsrc) {
+#pragma unroll
+        for (int gk = 0; gk < S / kRows; gk++) {
+          const T *gp = gsrc + gk * S * kRows;
+          int so = 0;
+          asm volatile("" : "+s"(so) : "v"(tok));
+          T cur[kRows], nxt[kRows], u[kRows];
+#pragma unroll
+          for (int j = 0; j < kRows; j++) cur[j] = gp[so + j];
+#pragma unroll
+          for (int l = 0; l < S; l++) {
+            asm volatile("" : "+s"(so) : "v"(tok));  // column l+1's loads after column l-1's chains
+            if (l + 1 < S) {
+#pragma unroll
+              for (int j = 0; j < kRows; j++) nxt[j] = gp[so + (l + 1) * kRows + j];
+            }
+            T pr[kRows];
+#pragma unroll
+            for (int j = 0; j < kRows; j++) pr[j] = x[l] * cur[j];
+            pin_chains(pr);
+#pragma unroll
+            for (int j = 0; j < kRows; j++) u[j] = l == 0 ? pr[j] : u[j] + pr[j];
+            pin_chains(u);
+            tok = u[kRows - 1];
+#pragma unroll
+            for (int j = 0; j < kRows; j++) cur[j] = nxt[j];
+          }
+#pragma unroll
+          for (int j = 0; j < kRows; j++) fn(gk * kRows + j, u[j]);
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int gk = 0; gk < S / kRows; gk++) {
       const V *G = M + gk * S * RV;
@@ -548,7 +591,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
       stage(x1, T2 ? x1 : x2, T2 ? base + stride : base);
       row_read<T>(tile, lane, c, a);
       __syncthreads();
-      gphase(mL, a, [&](int k, T u) { U[k] = u; });
+      gphase(mL, a, [&](int k, T u) { U[k] = u; }, ((kPS & 1) && pl_t) ? pl_t + c * S * S : nullptr);
     }
     if constexpr (T2) {
       const T *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
@@ -559,7 +602,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
       stage(x2, FD, base + stride);  // next: the next trip's first dense child
       row_read<T>(tile, lane, c, b);
       __syncthreads();
-      gphase(mR, b, [&](int k, T u) { U[k] = U[k] * u; });
+      gphase(mR, b, [&](int k, T u) { U[k] = U[k] * u; }, ((kPS & 2) && pr_t) ? pr_t + c * S * S : nullptr);
     }
     // phase 3: O[l] = sum_k U[k] * EV[k][l] from +0.0, kPh3 chains per pass
     T O[S];
@@ -691,21 +734,50 @@ plf_prot_lds_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__res
                                                                 scaler, n, ws, scaler_sum, tipvec);
 }
 
+// Tuning form of the exact f64 kernel with phase 2's matrix as SGPR operands
+// (kPS = 2; not launched by the product): plf_prot_lds_kernel plus pr_t, the
+// group-transposed P_R made by prot_group_transpose on the same stream.
+template <bool kSum, int kMinWaves, int kTips>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_exact64_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                        double *__restrict__ x3, const double *__restrict__ EV,
+                        const double *__restrict__ left, const double *__restrict__ right,
+                        const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                        unsigned long long *ws, int64_t *scaler_sum, const double *__restrict__ tipvec,
+                        const double *__restrict__ pr_t) {
+  prot_lds_body<double, false, kSum, kTips, 10, true, false, true, 2>(
+      x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum, tipvec, nullptr, pr_t);
+}
+
+// The group-transposed copy of a 4-category S = 20 matrix for kPS:
+// Pt[c][k / kRows][l][k % kRows] = P[c][k][l] (one block; stream-ordered before
+// the kernel that reads it).
+template <typename T, int kRows>
+__global__ void __launch_bounds__(kBlock) prot_group_transpose(const T *__restrict__ P, T *__restrict__ Pt) {
+  constexpr int S = 20;
+  for (int i = threadIdx.x; i < 4 * S * S; i += kBlock) {
+    const int cc = i / (S * S), r = i - cc * S * S, k = r / S, l = r - k * S;
+    Pt[cc * S * S + (k / kRows) * (S * kRows) + l * kRows + (k % kRows)] = P[i];
+  }
+}
+
 // The round-1 EXACT f64 form, kept for same-process comparisons
 // (tools/tune_prot.hip): one chain per row k, the row streamed one ahead.
 // kRows > 0 runs the product body (plf_prot_lds_kernel) instead.
 template <bool kSum, int kMinWaves = 2, int kTips = 0, int kRows = 0, bool kPf = false,
-          bool kE3S = false>
+          bool kE3S = false, int kPS = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_exact_f64_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                           double *__restrict__ x3, const double *__restrict__ EV,
                           const double *__restrict__ left, const double *__restrict__ right,
                           const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
                           unsigned long long *ws, int64_t *scaler_sum,
-                          const double *__restrict__ tipvec = nullptr) {
+                          const double *__restrict__ tipvec = nullptr,
+                          const double *__restrict__ pl_t = nullptr,
+                          const double *__restrict__ pr_t = nullptr) {
   if constexpr (kRows > 0) {
-    prot_lds_body<double, false, kSum, kTips, kRows, kPf, false, kE3S>(
-        x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum, tipvec);
+    prot_lds_body<double, false, kSum, kTips, kRows, kPf, false, kE3S, kPS>(
+        x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum, tipvec, pl_t, pr_t);
     return;
   } else {
   constexpr int S = 20;

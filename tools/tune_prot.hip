@@ -117,6 +117,23 @@ int main(int argc, char **argv) {
     fill<<<2048, 256>>>(s.x2, n * 80, 20 + r, 1.0, 80);
     std::vector<int> ones(n, 1); CK(hipMemcpy(s.wgt, ones.data(), n * 4, hipMemcpyHostToDevice));
   }
+  // group-transposed copies of P_L / P_R for the kPS variants: [c][k/10][l][k%10]
+  double *Lt, *Rt, *Rt2;
+  CK(hipMalloc(&Lt, 1600 * 8)); CK(hipMalloc(&Rt, 1600 * 8)); CK(hipMalloc(&Rt2, 1600 * 8));
+  {
+    std::vector<double> hl(1600), hr(1600), tl(1600), tr(1600);
+    CK(hipMemcpy(hl.data(), L, 1600 * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hr.data(), Rm, 1600 * 8, hipMemcpyDeviceToHost));
+    for (int c = 0; c < 4; c++)
+      for (int k = 0; k < 20; k++)
+        for (int l = 0; l < 20; l++) {
+          const int d = c * 400 + (k / 10) * 200 + l * 10 + (k % 10);
+          tl[d] = hl[c * 400 + k * 20 + l];
+          tr[d] = hr[c * 400 + k * 20 + l];
+        }
+    CK(hipMemcpy(Lt, tl.data(), 1600 * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(Rt, tr.data(), 1600 * 8, hipMemcpyHostToDevice));
+  }
   double *ref; uint8_t *refsc; int64_t *refsum;
   CK(hipMalloc(&ref, n * 640)); CK(hipMalloc(&refsc, n)); CK(hipMalloc(&refsum, 8));
   CK(hipDeviceSynchronize());
@@ -174,15 +191,29 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3((TS) * 8), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm, \
                            s.wgt, s.sc, n, ws, s.sum); }, {}, true});                              \
   }
+#define ADD_KX(NAME, KERNEL, PS)                                                                   \
+  {                                                                                                \
+    auto k = KERNEL;                                                                               \
+    const int o = occ((const void *)k);                                                            \
+    const int64_t grid = std::min<int64_t>((n + 63) / 64, (int64_t)o * CUs);                       \
+    char nm[200]; snprintf(nm, sizeof nm, "%s occ=%d/CU grid=%lld", NAME, o, (long long)grid);      \
+    const double *pl = (PS & 1) ? Lt : nullptr, *pr = (PS & 2) ? Rt : nullptr;                     \
+    const bool tr = (PS & 4) != 0;  /* the copy made by prot_group_transpose in every run */       \
+    if (!only || strstr(nm, only) || strstr(nm, "product"))                                        \
+      vs.push_back({nm, [=](const Set &s) {                                                        \
+        if (tr) hipLaunchKernelGGL((prot_group_transpose<double, 10>), dim3(1), dim3(256), 0, 0, Rm, Rt2); \
+        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,  \
+                           s.wgt, s.sc, n, ws, s.sum, nullptr, pl, tr ? Rt2 : pr); }, {}, true});  \
+  }
   ADD_K("product exact", (&plf_prot_kernel<double, false, true>), 64)
   ADD_K("product fma-mfma", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
-  ADD_K("product exact-lds (NS=1)", (&plf_prot_exact_f64_kernel<true>), 64)
-  ADD_K("exact-lds rows=2", (&plf_prot_exact_f64_kernel<true, 2, 0, 2>), 64)
-  ADD_K("exact-lds rows=4", (&plf_prot_exact_f64_kernel<true, 2, 0, 4>), 64)
-  ADD_K("exact-lds rows=10", (&plf_prot_exact_f64_kernel<true, 2, 0, 10>), 64)
-  ADD_K("exact-lds rows=4 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 4, true>), 64)
-  ADD_K("exact-lds rows=10 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true>), 64)
-  ADD_K("exact-lds rows=10 prefetch EV-sgpr", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true>), 64)
+  ADD_KX("product exact-lds (NS=1)", (&plf_prot_exact_f64_kernel<true>), 0)
+  ADD_KX("exact-lds rows=2", (&plf_prot_exact_f64_kernel<true, 2, 0, 2>), 0)
+  ADD_KX("exact-lds rows=4", (&plf_prot_exact_f64_kernel<true, 2, 0, 4>), 0)
+  ADD_KX("exact-lds rows=10", (&plf_prot_exact_f64_kernel<true, 2, 0, 10>), 0)
+  ADD_KX("exact-lds rows=4 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 4, true>), 0)
+  ADD_KX("exact-lds rows=10 prefetch", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true>), 0)
+  ADD_KX("exact-lds rows=10 prefetch EV-sgpr", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true>), 0)
   ADD_K("mfma ablate: no matrix cores", (&plf_prot_mfma_kernel<true, 2, true, 1>), 64)
   ADD_K("mfma ablate: no HBM traffic", (&plf_prot_mfma_kernel<true, 2, true, 2>), 64)
   ADD_K("mfma 16x16x4 only (padded rows)", (&plf_prot_mfma_kernel<true, 2, true, 0, false>), 64)
@@ -206,6 +237,14 @@ int main(int argc, char **argv) {
   ADD_K("mfma v5 permX3+early+swz", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, false, true>), 64)
   ADD_K("mfma v5 permX3+early (product form)", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
   ADD_K("mfma v5 permX3+early+swz again", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, false, true>), 64)
+  // round 2: phase 1 / 2 matrices as SGPR operands by scalar loads (kPS)
+  ADD_KX("exact v6 E3S (product form)", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true>), 0)
+  ADD_KX("exact v6 E3S + P1 sgpr", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true, 1>), 1)
+  ADD_KX("exact v6 E3S + P2 sgpr", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true, 2>), 2)
+  ADD_KX("exact v6 E3S + P1 P2 sgpr", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true, 3>), 3)
+  ADD_KX("exact v6 E3S + P2 sgpr + transpose launch", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true, 2>), 6)
+  ADD_KX("exact v6 E3S + P2 sgpr + transpose launch again", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true, 2>), 6)
+  ADD_KX("exact v6 E3S (product form) again", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true>), 0)
   ADD_KT("mfma v8 perm late", (&plf_prot_mfma8_kernel<true, true, false, 64>), 64)
   ADD_KT("mfma v4x2 perm late", (&plf_prot_mfma8_kernel<true, true, false, 32>), 32)
   ADD_KT("mfma v4x2 perm early", (&plf_prot_mfma8_kernel<true, true, true, 32>), 32)
