@@ -976,9 +976,13 @@ __device__ __forceinline__ void swap_rows16(double &v, double &w) {
 // once; the rows-16..19 ds_write_b64 of X3 becomes conflict-free the same way.
 // The b128 tile writes and the store pass move whole chunks and swap the two
 // halves back with a select (tools/lds_banks.py, swizzle rows).
+// kSpread (tuning, with kPrefetch): the next child tile's ten 16-B loads per
+// thread go out in four parts, part t right after sub-tile t's B-fragment
+// reads, instead of all at the start of the phase (fewer requests in flight
+// at once: the stream probes' V = 1..2 regime).
 template <bool kSum, int kMinWaves = 2, bool kPrefetch = true, int kAblate = 0, bool kMix4 = true,
           int kTips = 0, int kX3 = 0, bool kEarly = false, bool kFirstX2 = false,
-          bool kSplitB = false, bool kSwz = false>
+          bool kSplitB = false, bool kSwz = false, bool kSpread = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                      double *__restrict__ x3, const double *__restrict__ EV,
@@ -1068,6 +1072,27 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       }
     }
   };
+  // kSpread: part `part` (of 4) of a tile fetch into pf; z is an opaque zero
+  // tied to the sub-tile's B reads, so the part cannot be hoisted above them
+  auto fetch_part = [&](const double *src, int64_t b, int part, int z) {
+    constexpr int K = PT::kChunks / kBlock;
+    const f64x2 *sp = reinterpret_cast<const f64x2 *>(src + b * 80) + z;
+    const int i0 = part * K / 4, i1 = (part + 1) * K / 4;
+    if (b + 64 <= n) {
+#pragma unroll
+      for (int i = 0; i < K; i++)
+        if (i >= i0 && i < i1) pf[i] = __builtin_nontemporal_load(sp + threadIdx.x + i * kBlock);
+    } else {
+      const int64_t lim = (n - b) * PT::kChunksPerSite;
+#pragma unroll
+      for (int i = 0; i < K; i++) {
+        if (i < i0 || i >= i1) continue;
+        const int j = threadIdx.x + i * kBlock;
+        pf[i] = f64x2{0.0, 0.0};
+        if (j < lim) pf[i] = __builtin_nontemporal_load(sp + j);
+      }
+    }
+  };
   if constexpr (!kEarly && kPrefetch && kAblate != 2 && !T2)  // the first dense child's first tile
     if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
   auto trip = [&](const int64_t base, auto first_tag) {
@@ -1085,18 +1110,24 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       if constexpr (kFirst && kX2Early) {
 #pragma unroll
         for (int i = 0; i < PT::kChunks / kBlock; i++) pf[i] = pf2[i];
-      } else if constexpr (kAblate != 2) {
+      } else if constexpr (kAblate != 2 && !kSpread) {
         tile_fetch<double>(x2, base, n, pf);
       }
     } else {
       tile_load<double>(x1, base, n, tile);
       __syncthreads();
     }
+    constexpr bool kSp1 = kSpread && kPrefetch && kAblate != 2 && !(kFirst && kX2Early);
     if constexpr (!T1) {
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         double bv[5];
         bfrag(td + (16 * t + lo16) * kRow + c * S + (g ^ sw), bv);
+        if constexpr (kSp1) {
+          int z = 0;
+          asm volatile("" : "+v"(z) : "v"(bv[0]));
+          fetch_part(x2, base, t, z);
+        }
 #pragma unroll
         for (int mt = 0; mt < 2; mt++) {
           f64x4 u = {0.0, 0.0, 0.0, 0.0};
@@ -1124,15 +1155,23 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       put(pf);
       __syncthreads();
       // next trip's first dense child: x1, or x2 when x1 is a tip
-      if (kAblate != 2 && base + stride < n) tile_fetch<double>(T1 ? x2 : x1, base + stride, n, pf);
+      if (!kSpread && kAblate != 2 && base + stride < n) tile_fetch<double>(T1 ? x2 : x1, base + stride, n, pf);
     } else {
       tile_load<double>(x2, base, n, tile);
       __syncthreads();
     }
+    const bool sp2 = kSpread && kPrefetch && kAblate != 2 && base + stride < n;
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       double bv[5];
       bfrag(td + (16 * t + lo16) * kRow + c * S + (g ^ sw), bv);
+      if constexpr (kSpread) {
+        if (sp2) {
+          int z = 0;
+          asm volatile("" : "+v"(z) : "v"(bv[0]));
+          fetch_part(T1 ? x2 : x1, base + stride, t, z);
+        }
+      }
 #pragma unroll
       for (int mt = 0; mt < 2; mt++) {
         f64x4 u = {0.0, 0.0, 0.0, 0.0};

@@ -237,6 +237,11 @@ int main(int argc, char **argv) {
   ADD_K("mfma v5 permX3+early+swz", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, false, true>), 64)
   ADD_K("mfma v5 permX3+early (product form)", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
   ADD_K("mfma v5 permX3+early+swz again", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, false, true>), 64)
+  // round 2: the next tile's loads spread over the phase's sub-tiles (kSpread)
+  ADD_K("mfma v7 permX3+early (product form)", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
+  ADD_K("mfma v7 permX3+early+spread", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, false, false, true>), 64)
+  ADD_K("mfma v7 permX3+early (product form) again", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true>), 64)
+  ADD_K("mfma v7 permX3+early+spread again", (&plf_prot_mfma_kernel<true, 2, true, 0, true, 0, 2, true, false, false, false, true>), 64)
   // round 2: phase 1 / 2 matrices as SGPR operands by scalar loads (kPS)
   ADD_KX("exact v6 E3S (product form)", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true>), 0)
   ADD_KX("exact v6 E3S + P1 sgpr", (&plf_prot_exact_f64_kernel<true, 2, 0, 10, true, true, 1>), 1)
