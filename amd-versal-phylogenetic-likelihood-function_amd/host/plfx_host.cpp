@@ -41,6 +41,8 @@
 #include <string>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "../../include/plfx.h"
 #include "../csrc/testbench.hpp"
 
@@ -229,6 +231,7 @@ int run(const Opts &o) {
     auto ms_since = [&](std::chrono::steady_clock::time_point a) {
       return std::chrono::duration<double, std::milli>(a - t0).count();
     };
+    roctxRangePush("plfx_host roundtrip (sw_emu)");  // the reference's XRT user range, host_mem.cpp:273,395
     for (uint32_t i = 0; i < o.calls; i++) {
       for (uint32_t k = 0; k < P; k++) {
         const uint64_t nk = tb.alignments_per_instance(k), off = tb.instance_site_offset(k);
@@ -244,6 +247,7 @@ int run(const Opts &o) {
       for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
       inc[i] = s;
     }
+    roctxRangePop();
     wall_ms = ms_since(std::chrono::steady_clock::now());
   } else {
     plfx_ctx *ctx = nullptr;
@@ -270,8 +274,14 @@ int run(const Opts &o) {
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipDeviceSynchronize());
     auto t0 = std::chrono::steady_clock::now();
+    // host-side ranges for rocprofv3 --marker-trace: the whole run (the
+    // reference's XRT user range "roundtrip_exec_time", host_mem.cpp:273,395)
+    // and each plf call's enqueue + wait; the H2D / kernel / D2H regions
+    // themselves are the events below and the kernel trace
+    roctxRangePush("plfx_host roundtrip");
     HIPCHK(hipEventRecord(e0, st[0]));
     for (uint32_t i = 0; i < o.calls; i++) {
+      roctxRangePush("plf call (all instances)");
       for (uint32_t k = 0; k < P; k++) {
         const uint64_t nk = tb.alignments_per_instance(k);
         const uint64_t off = tb.instance_site_offset(k);
@@ -292,7 +302,9 @@ int run(const Opts &o) {
       long long s = 0;  // host_mem.cpp:385-388
       for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
       inc[i] = s;
+      roctxRangePop();
     }
+    roctxRangePop();
     wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (size_t q = 0; q < reg.size(); q++) {
       float a, b, c, d;
@@ -322,7 +334,9 @@ int run(const Opts &o) {
     std::vector<long long> cinc(o.calls);
     for (uint32_t i = 0; i < o.calls; i++) {
       auto a = std::chrono::steady_clock::now();
+      roctxRangePush("reference plf() (CPU)");
       cpu_plf<T>(xl.data(), xr.data(), cpu.data(), ev, o.sites, bl, br, wgt.data(), cinc[i]);
+      roctxRangePop();
       ref_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
       for (uint64_t j = 0; j < elems && errors < 20; j++) {
         if (std::memcmp(&cpu[j], &result[i][j], sizeof(T)) != 0) {  // bit patterns, stricter than !=
