@@ -136,6 +136,33 @@ def test_protein_fma_full_size_256k(ctx, oracle):
     assert (np.abs(got - e3).reshape(n, V) / scale).max() <= 1e-12
 
 
+def test_protein_f32_fma_full_size_256k(ctx, oracle):
+    """The f32 protein FMA kernel (matrix cores, rows 16..19 on the 4x4x1 form
+    with permlane transposes) at configs[4]'s size, 2^18 sites: bit-exact
+    against the oracle's fmaf restatement, scaler bytes and sum included."""
+    import torch
+
+    S, CAT, n = 20, 4, 1 << 18
+    V = S * CAT
+    rng = np.random.default_rng(2027)
+    x1 = rng.random(V * n).astype(np.float32)
+    x1.reshape(n, V)[1::4] *= np.float32(1e-14)
+    x2 = rng.random(V * n).astype(np.float32)
+    left = rng.random(CAT * S * S).astype(np.float32)
+    right = rng.random(CAT * S * S).astype(np.float32)
+    EV = (rng.random(S * S) - 0.25).astype(np.float32)
+    w = rng.integers(0, 4, n).astype(np.int32)
+    t = [dev(a) for a in (x1, x2, EV, left, right, w)]
+    x3 = torch.empty(V * n, dtype=torch.float32, device="cuda")
+    sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    ctx.plf_dev_gen(t[0], t[1], x3, t[2], t[3], t[4], S, t[5], sc, s, n=n, fma=True)
+    torch.cuda.synchronize()
+    f3, fsc, finc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
+    assert np.array_equal(bits(x3.cpu().numpy()), bits(f3))
+    assert np.array_equal(sc.cpu().numpy(), fsc) and int(s.item()) == finc and fsc.sum() > 0
+
+
 def test_nodes64_full_size_windows(ctx, oracle):
     """configs[3]'s per-GPU shard as the bench times it: 64 independent nodes
     x 2^20 f64 sites in two 32-node batched launches.  A 4096-site window of
