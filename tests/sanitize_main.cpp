@@ -137,8 +137,8 @@ int main() {
   EXPECT(plfx_shard(512, 8, 7, &o, &c) == 0 && o == 448 && c == 64, "shard 512 nodes over 8");
   // sw_emu over windows, layouts, PLIO kinds, ragged instance splits, f32 and f64
   const uint64_t sites[] = {1, 7, 64, 1000, 1024, 4099};
-  const uint32_t insts[] = {1, 3, 4};
-  const uint32_t windows[] = {1024, 8192, 16288};
+  const uint32_t insts[] = {1, 3, 4, 9};
+  const uint32_t windows[] = {32, 96, 1024, 8192, 16288};
   uint32_t seed = 20250117;
   for (uint64_t n : sites)
     for (uint32_t p : insts) {
