@@ -6,7 +6,7 @@
 // timed over rotating buffer sets in one process.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
-//     -I amd-versal-phylogenetic-likelihood-function_amd/csrc tools/tune_prot32.hip -o build/tune_prot32
+//     -I amd-versal-phylogenetic-likelihood-function_amd/csrc -I tools tools/tune_prot32.hip -o build/tune_prot32
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "plf_prot.hpp"
+#include "prot_pair32.hpp"
 
 using namespace plfx::dev;
 
@@ -96,6 +97,15 @@ int main(int argc, char **argv) {
   ADD("mfma32 fma minw2 kQ=2", 1, (&plf_prot_mfma32_kernel<true, 2, 0, 2>))
   ADD("mfma32 fma minw4 kQ=2", 1, (&plf_prot_mfma32_kernel<true, 4, 0, 2>))
   ADD("mfma32 fma minw3 (product, again)", 1, (&plf_prot_mfma32_kernel<true, 3>))
+  }
+  if (argc > 3 && atoi(argv[3]) == 2) {  // round-2 pair session: exact, two sites per lane
+    vs.clear();
+    ADD("readlane exact (r01, the check)", 0, (&plf_prot_kernel<float, false, true>))
+    ADD("lds exact rows=4 (product)", 0, (&plf_prot_lds_kernel<float, false, true, 2, 0, 4, true, false>))
+    ADD("pair32 exact minw2", 0, (&plf_prot_pair32_kernel<true, 2>))
+    ADD("pair32 exact minw1", 0, (&plf_prot_pair32_kernel<true, 1>))
+    ADD("lds exact rows=4 (product, again)", 0, (&plf_prot_lds_kernel<float, false, true, 2, 0, 4, true, false>))
+    ADD("pair32 exact minw2 again", 0, (&plf_prot_pair32_kernel<true, 2>))
   }
   std::vector<uint32_t> ref[2], got(n * 80);
   std::vector<uint8_t> rsc[2], gsc(n);
