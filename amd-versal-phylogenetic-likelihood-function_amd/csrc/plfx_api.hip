@@ -15,6 +15,7 @@
 #include <new>
 #include <string>
 #include <functional>
+#include <mutex>
 #include <vector>
 
 #include "../../include/plfx.h"
@@ -51,6 +52,9 @@ struct plfx_ctx {
   hipStream_t d2h_stream = nullptr;
   hipEvent_t chunk_done[kHostChunksMax] = {};
   std::string err;
+  // calls on one context from several host threads are serialised (recursive:
+  // entry points call each other, e.g. instance_run_host -> instance_run)
+  mutable std::recursive_mutex mu;
 };
 
 namespace {
@@ -71,8 +75,9 @@ struct DeviceGuard {
   DeviceGuard &operator=(const DeviceGuard &) = delete;
 };
 
-#define PLFX_BIND(ctx)                 \
-  if (!(ctx)) return PLFX_ERR_INVALID; \
+#define PLFX_BIND(ctx)                                              \
+  if (!(ctx)) return PLFX_ERR_INVALID;                              \
+  std::lock_guard<std::recursive_mutex> plfx_lock_((ctx)->mu);      \
   DeviceGuard plfx_guard_((ctx)->device)
 
 constexpr size_t kWsRegions = std::max({(size_t)plfx::kMaxBatch, (size_t)7 * plfx::kMaxSeptets,
@@ -863,6 +868,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
 
 int plfx_traverse_schedule(const plfx_ctx *ctx, int *counts, int ncounts) {
   if (!ctx || (ncounts > 0 && !counts)) return 0;
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   const int m = std::min(ncounts, PLFX_SCHED_COUNTS);
   for (int i = 0; i < m; i++) counts[i] = ctx->sched[i];
   return m < 0 ? 0 : m;

@@ -41,8 +41,12 @@
  * context's own non-blocking stream).  Device pointers must come from the same HIP
  * device as the context; CLV pointers must be 16-byte aligned.  Every entry
  * point binds the context's device for its duration and restores the
- * caller's current device on return.  A context may be used from one host
- * thread at a time; distinct contexts are independent.
+ * caller's current device on return.  Calls on one context from several host
+ * threads are serialised by the context (one lock per context, held for the
+ * call: host entry points block other threads' calls for their duration;
+ * device entry points only for the launch); distinct contexts are independent.
+ * plfx_last_error() reports the last failure on the context, whichever thread
+ * made it.
  *
  * Streams and the scaler-sum workspace.  Sum-producing launches (scaler_sum
  * outputs, plfx_scaler_sum, plfx_root_lnl) reduce across thread blocks through

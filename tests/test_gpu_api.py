@@ -54,6 +54,59 @@ def test_sums_on_two_streams_concurrently(ctx, oracle):
     assert np.all(got[0] == got[0][0]) and np.all(got[1] == got[1][0])  # deterministic
 
 
+def test_one_context_from_several_host_threads(ctx, oracle):
+    """plfx.h: calls on one context from several host threads are serialised by
+    the context.  Four Python threads (ctypes drops the GIL for each call), each
+    on its own stream, issue node updates with scaler sums and root lnLs on the
+    SAME context at once: every sum exact, every CLV bit-exact, lnL identical."""
+    import threading
+
+    import torch
+
+    n = 1 << 18
+    d = oracle.gen_hostmem(n, np.float64, 43)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right")}
+    nt, reps = 4, 16
+    ws = [dev(np.full(n, i + 1, np.int32)) for i in range(nt)]
+    outs = [torch.empty_like(t["x1"]) for _ in range(nt)]
+    sums = torch.zeros(nt, reps, dtype=torch.int64, device="cuda")
+    lnl = torch.zeros(nt, reps, dtype=torch.float64, device="cuda")
+    streams = [torch.cuda.Stream() for _ in range(nt)]
+    torch.cuda.synchronize()
+    errs = []
+    go = threading.Barrier(nt)
+
+    def worker(i):
+        try:
+            go.wait()
+            for r in range(reps):
+                ctx.plf_dev(t["x1"], t["x2"], outs[i], t["EV"], t["left"], t["right"], ws[i], None,
+                            sums[i, r:r + 1], stream=streams[i])
+                ctx.root_lnl(outs[i], n, lnl[i, r:r + 1], wgt=ws[i], scaler_sums=sums[i, r:r + 1],
+                             stream=streams[i])
+            streams[i].synchronize()
+        except Exception as e:  # reported on the main thread
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(nt)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=60)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    n_sc = n // 4
+    for i in range(nt):
+        assert sums[i].tolist() == [(i + 1) * n_sc] * reps
+    e3, _, _ = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], threads=16)
+    for o in outs:
+        assert np.array_equal(bits(o.cpu().numpy()), bits(e3))
+    got = lnl.cpu().numpy()
+    for i in range(nt):
+        assert np.all(got[i] == got[i][0])
+    assert np.allclose(got[1], 2 * got[0], rtol=1e-12)  # weights 2 vs 1: lnL doubles
+
+
 def test_graph_capture_needs_a_warm_stream(ctx, oracle):
     """A stream's first sum-producing call may not be inside a capture (its
     workspace is allocated then): rejected with PlfxError.  After one call the
