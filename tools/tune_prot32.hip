@@ -107,6 +107,29 @@ int main(int argc, char **argv) {
     ADD("lds exact rows=4 (product, again)", 0, (&plf_prot_lds_kernel<float, false, true, 2, 0, 4, true, false>))
     ADD("pair32 exact minw2 again", 0, (&plf_prot_pair32_kernel<true, 2>))
   }
+  if (argc > 3 && atoi(argv[3]) == 3) {  // round-2 grid session: the product kernel at fixed grids
+    vs.clear();
+#define ADDG(NAME, MODE, KERNEL, GRID)                                                             \
+  {                                                                                                \
+    auto k = KERNEL;                                                                               \
+    const int64_t grid = std::min<int64_t>((n + 63) / 64, (int64_t)(GRID));                        \
+    char nm[200]; snprintf(nm, sizeof nm, "%s grid=%lld trips<=%lld", NAME, (long long)grid,       \
+                           (long long)(((n + 63) / 64 + grid - 1) / grid));                         \
+    vs.push_back({nm, MODE, [=](const Set &s) {                                                    \
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm,    \
+                         s.wgt, s.sc, n, ws, s.sum, nullptr); }, {}});                              \
+  }
+    const int64_t tiles = (n + 63) / 64, res = 3LL * CUs;
+    const int64_t trips = (tiles + res - 1) / res, bal = (tiles + trips - 1) / trips;
+    auto kp = &plf_prot_mfma32_kernel<true, 3, 0, 2>;
+    ADDG("readlane fma (r01, the check)", 1, (&plf_prot_kernel<float, true, true>), 2LL * CUs)
+    ADDG("product, resident 3/CU", 1, kp, res)
+    ADDG("product, balanced trips", 1, kp, bal)
+    ADDG("product, 2/CU", 1, kp, 2LL * CUs)
+    ADDG("product, balanced+1 trip", 1, kp, (tiles + trips) / (trips + 1))
+    ADDG("product, resident 3/CU again", 1, kp, res)
+    ADDG("product, balanced trips again", 1, kp, bal)
+  }
   std::vector<uint32_t> ref[2], got(n * 80);
   std::vector<uint8_t> rsc[2], gsc(n);
   int64_t rsum[2] = {0, 0}, gsum = 0;
