@@ -1351,7 +1351,11 @@ __device__ __forceinline__ void transpose_groups44(unsigned (&v)[4]) {
   }
 }
 
-template <bool kSum, int kMinWaves = 2, int kTips = 0, int kQ = 0>
+// kAblate (tuning only, tools/tune_prot32.hip): 1 = every MFMA replaced by one
+// VALU multiply-add (no matrix cores), 2 = no HBM loads or stores.
+// kRing (tuning only): two child tiles in flight (x2 of this trip and x1 of the
+// next during phase 1, x1 and x2 of the next trip during phase 2).
+template <bool kSum, int kMinWaves = 2, int kTips = 0, int kQ = 0, int kAblate = 0, bool kRing = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x2,
                        float *__restrict__ x3, const float *__restrict__ EV,
@@ -1368,10 +1372,16 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
   const int lane = threadIdx.x & 63;
   const int lo16 = lane & 15, g = lane >> 4;
   const int64_t stride = (int64_t)gridDim.x * 64;
+  static_assert(!kRing || (kTips == 0 && kAblate != 2), "kRing: dense children");
   f32x4 pf[K];
+  f32x4 pf2[kRing ? K : 1];
   // the first dense child's first tile, before the matrix fragments
-  if constexpr (!(T1 && T2))
+  if constexpr (kAblate == 2)
+    for (auto &q : pf) q = f32x4{1.f, 1.f, 1.f, 1.f};
+  if constexpr (!(T1 && T2) && kAblate != 2)
     if ((int64_t)blockIdx.x * 64 < n) tile_fetch<float>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
+  if constexpr (kRing)
+    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<float>(x2, (int64_t)blockIdx.x * 64, n, pf2);
   float AL[2][5], AR[2][5], AE[2][5];
 #pragma unroll
   for (int mt = 0; mt < 2; mt++)
@@ -1432,21 +1442,30 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
       for (int mt = 0; mt < (kQ ? 1 : 2); mt++) {
         f32x4 u = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int st = 0; st < 5; st++) u = __builtin_amdgcn_mfma_f32_16x16x4f32(A[mt][st], bv[st], u, 0, 0, 0);
+        for (int st = 0; st < 5; st++) {
+          if constexpr (kAblate == 1) u[st & 3] += bv[st] * A[mt][st];
+          else u = __builtin_amdgcn_mfma_f32_16x16x4f32(A[mt][st], bv[st], u, 0, 0, 0);
+        }
         P[t][mt] = mul ? P[t][mt] * u : u;  // prod[k] = umpL[k] * umpR[k]
       }
       if constexpr (kQ) {  // four of the 20 K = 1 steps per sub-tile, interleaved
         const f32x4 xv = *reinterpret_cast<const f32x4 *>(xs + 4 * t);
         const f32x4 av = *reinterpret_cast<const f32x4 *>(QA + 4 * t);
 #pragma unroll
-        for (int j = 0; j < 4; j++) q = __builtin_amdgcn_mfma_f32_4x4x1f32(av[j], xv[j], q, 0, 0, 0);
+        for (int j = 0; j < 4; j++) {
+          if constexpr (kAblate == 1) q[j] += av[j] * xv[j];
+          else q = __builtin_amdgcn_mfma_f32_4x4x1f32(av[j], xv[j], q, 0, 0, 0);
+        }
       }
     }
     if constexpr (kQ) {
       const f32x4 xv = *reinterpret_cast<const f32x4 *>(xs + 16);
       const f32x4 av = *reinterpret_cast<const f32x4 *>(QA + 16);
 #pragma unroll
-      for (int j = 0; j < 4; j++) q = __builtin_amdgcn_mfma_f32_4x4x1f32(av[j], xv[j], q, 0, 0, 0);
+      for (int j = 0; j < 4; j++) {
+        if constexpr (kAblate == 1) q[j] += av[j] * xv[j];
+        else q = __builtin_amdgcn_mfma_f32_4x4x1f32(av[j], xv[j], q, 0, 0, 0);
+      }
       Q = mul ? Q * q : q;
     }
   };
@@ -1473,8 +1492,10 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
       __syncthreads();
       // next: this trip's x2, or the next trip's x1 when x2 is a tip
       if constexpr (T2) {
+        if (kAblate != 2 && base + stride < n) tile_fetch<float>(x1, base + stride, n, pf);
+      } else if constexpr (kRing) {
         if (base + stride < n) tile_fetch<float>(x1, base + stride, n, pf);
-      } else {
+      } else if constexpr (kAblate != 2) {
         tile_fetch<float>(x2, base, n, pf);
       }
       product(AL, QL, P, Q, false);
@@ -1490,9 +1511,15 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
       }
       if constexpr (kQ) Q = Q * tip_q(tabs[1], code2);
     } else {
-      tile_put<float>(tile, pf);
-      __syncthreads();
-      if (base + stride < n) tile_fetch<float>(T1 ? x2 : x1, base + stride, n, pf);
+      if constexpr (kRing) {
+        tile_put<float>(tile, pf2);
+        __syncthreads();
+        if (base + stride < n) tile_fetch<float>(x2, base + stride, n, pf2);
+      } else {
+        tile_put<float>(tile, pf);
+        __syncthreads();
+        if (kAblate != 2 && base + stride < n) tile_fetch<float>(T1 ? x2 : x1, base + stride, n, pf);
+      }
       product(AR, QR, P, Q, true);
       __syncthreads();  // every wave is done reading x2: the tile takes X3 now
     }
@@ -1523,6 +1550,11 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
 #pragma unroll
       for (int st = 0; st < 5; st++) {
         const float b = (kQ && st == 4) ? __uint_as_float(Qt[t]) : P[t][st >> 2][st & 3];
+        if constexpr (kAblate == 1) {
+          X0[st & 3] += AE[0][st] * b;
+          if constexpr (kQ != 2) X1[st & 3] += AE[1][st] * b;
+          continue;
+        }
         X0 = __builtin_amdgcn_mfma_f32_16x16x4f32(AE[0][st], b, X0, 0, 0, 0);
         if constexpr (kQ != 2) X1 = __builtin_amdgcn_mfma_f32_16x16x4f32(AE[1][st], b, X1, 0, 0, 0);
       }
@@ -1544,7 +1576,8 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
       for (int k = 0; k < 20; k++) {
         const float a = reinterpret_cast<const f32x4 *>(QE)[k >> 2][k & 3];
         const float b = k < 16 ? __uint_as_float(pk[k & 15]) : Q[k & 3];
-        X1 = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, X1, 0, 0, 0);
+        if constexpr (kAblate == 1) X1[k & 3] += a * b;
+        else X1 = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, X1, 0, 0, 0);
       }
       const bool small = (__builtin_fabsf(X1[0]) < m) && (__builtin_fabsf(X1[1]) < m) &&
                          (__builtin_fabsf(X1[2]) < m) && (__builtin_fabsf(X1[3]) < m);
@@ -1573,7 +1606,12 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
         v[i] = tile[sl * PT::kStride + q];
         if ((all >> sl) & 1ull) v[i] = v[i] * Num<float>::two32();
       }
-      if (base + 64 <= n) {
+      if (kAblate == 2) {
+        f32x4 t = v[0];
+#pragma unroll
+        for (int i = 1; i < K; i++) t += v[i];
+        if (t.x == -1.25f) dst[threadIdx.x] = t;  // keeps the LDS reads alive
+      } else if (base + 64 <= n) {
 #pragma unroll
         for (int i = 0; i < K; i++) __builtin_nontemporal_store(v[i], dst + threadIdx.x + i * kBlock);
       } else {

@@ -130,6 +130,24 @@ int main(int argc, char **argv) {
     ADDG("product, resident 3/CU again", 1, kp, res)
     ADDG("product, balanced trips again", 1, kp, bal)
   }
+  if (argc > 3 && atoi(argv[3]) == 4) {  // round-2 ablation session (the ablated forms DIFFER by design)
+    vs.clear();
+    ADD("readlane fma (r01, the check)", 1, (&plf_prot_kernel<float, true, true>))
+    ADD("product", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2>))
+    ADD("product ablate: no matrix cores", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 1>))
+    ADD("product ablate: no HBM", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 2>))
+    ADD("product again", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2>))
+  }
+  if (argc > 3 && atoi(argv[3]) == 5) {  // round-2 ring session: two tiles in flight per block
+    vs.clear();
+    ADD("readlane fma (r01, the check)", 1, (&plf_prot_kernel<float, true, true>))
+    ADD("product", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2>))
+    ADD("ring minw3", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 0, true>))
+    ADD("ring minw2", 1, (&plf_prot_mfma32_kernel<true, 2, 0, 2, 0, true>))
+    ADD("product again", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2>))
+    ADD("ring minw3 again", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 0, true>))
+    ADD("ring minw2 again", 1, (&plf_prot_mfma32_kernel<true, 2, 0, 2, 0, true>))
+  }
   std::vector<uint32_t> ref[2], got(n * 80);
   std::vector<uint8_t> rsc[2], gsc(n);
   int64_t rsum[2] = {0, 0}, gsum = 0;
