@@ -399,7 +399,15 @@ int plfx_ctx_destroy(plfx_ctx *ctx) {
   return PLFX_OK;
 }
 
-const char *plfx_last_error(const plfx_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+// A copy taken under the context's lock, so another thread's failure cannot
+// free the string under the caller; valid until this thread's next call.
+const char *plfx_last_error(const plfx_ctx *ctx) {
+  if (!ctx) return "null context";
+  thread_local std::string copy;
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  copy = ctx->err;
+  return copy.c_str();
+}
 
 void *plfx_ctx_stream(plfx_ctx *ctx) { return ctx ? reinterpret_cast<void *>(ctx->stream) : nullptr; }
 

@@ -46,7 +46,8 @@
  * call: host entry points block other threads' calls for their duration;
  * device entry points only for the launch); distinct contexts are independent.
  * plfx_last_error() reports the last failure on the context, whichever thread
- * made it.
+ * made it; the string is the calling thread's copy, valid until that thread
+ * calls plfx_last_error() again.
  *
  * Streams and the scaler-sum workspace.  Sum-producing launches (scaler_sum
  * outputs, plfx_scaler_sum, plfx_root_lnl) reduce across thread blocks through
