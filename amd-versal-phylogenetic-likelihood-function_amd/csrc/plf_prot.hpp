@@ -1352,7 +1352,9 @@ __device__ __forceinline__ void transpose_groups44(unsigned (&v)[4]) {
 }
 
 // kAblate (tuning only, tools/tune_prot32.hip): 1 = every MFMA replaced by one
-// VALU multiply-add (no matrix cores), 2 = no HBM loads or stores.
+// VALU multiply-add (no matrix cores), 2 = no HBM loads or stores, 3 = the
+// tile data movement alone (x2's tile goes back out as x3: no products, no
+// back-transform).
 // kRing (tuning only): two child tiles in flight (x2 of this trip and x1 of the
 // next during phase 1, x1 and x2 of the next trip during phase 2).
 template <bool kSum, int kMinWaves = 2, int kTips = 0, int kQ = 0, int kAblate = 0, bool kRing = false>
@@ -1430,6 +1432,7 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
   // one child's product U^T for the 4 sub-tiles from the LDS tile (mul: into P);
   // kQ: rows 16..19 of the lane's own site into Q (4x4x1 chain, k ascending)
   auto product = [&](const float (&A)[2][5], const float *QA, f32x4 (&P)[4][2], f32x4 &Q, bool mul) {
+    if constexpr (kAblate == 3) return;
     f32x4 q = {0.f, 0.f, 0.f, 0.f};
     const float *xs = td + lane * kRow + c * S;  // the lane's own site row
 #pragma unroll
@@ -1546,6 +1549,7 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
     unsigned long long mine = 0;
 #pragma unroll
     for (int t = 0; t < 4; t++) {
+      if constexpr (kAblate == 3) break;
       f32x4 X0 = {0.f, 0.f, 0.f, 0.f}, X1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int st = 0; st < 5; st++) {
@@ -1570,7 +1574,7 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
       *reinterpret_cast<f32x4 *>(w + 4 * g) = X0;
       if (kQ != 2 && g == 0) *reinterpret_cast<f32x4 *>(w + 16) = X1;
     }
-    if constexpr (kQ == 2) {  // states 16..19 of site `lane`: 20 K = 1 steps, k ascending
+    if constexpr (kQ == 2 && kAblate != 3) {  // states 16..19 of site `lane`: 20 K = 1 steps, k ascending
       f32x4 X1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < 20; k++) {

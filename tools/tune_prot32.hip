@@ -136,6 +136,8 @@ int main(int argc, char **argv) {
     ADD("product", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2>))
     ADD("product ablate: no matrix cores", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 1>))
     ADD("product ablate: no HBM", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 2>))
+    ADD("product ablate: tile movement only", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 3>))
+    ADD("product ablate: tile movement only, 4/CU", 1, (&plf_prot_mfma32_kernel<true, 4, 0, 2, 3>))
     ADD("product again", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2>))
   }
   if (argc > 3 && atoi(argv[3]) == 5) {  // round-2 ring session: two tiles in flight per block
