@@ -1355,9 +1355,11 @@ __device__ __forceinline__ void transpose_groups44(unsigned (&v)[4]) {
 // VALU multiply-add (no matrix cores), 2 = no HBM loads or stores, 3 = the
 // tile data movement alone (x2's tile goes back out as x3: no products, no
 // back-transform).
-// kRing (tuning only): two child tiles in flight (x2 of this trip and x1 of the
-// next during phase 1, x1 and x2 of the next trip during phase 2).
-template <bool kSum, int kMinWaves = 2, int kTips = 0, int kQ = 0, int kAblate = 0, bool kRing = false>
+// kRing (tuning only): 1 = two child tiles in flight (x2 of this trip and x1 of
+// the next during phase 1, x1 and x2 of the next trip during phase 2); 2 = both
+// children staged together in two LDS tiles, the next trip's two in flight
+// through both products.
+template <bool kSum, int kMinWaves = 2, int kTips = 0, int kQ = 0, int kAblate = 0, int kRing = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x2,
                        float *__restrict__ x3, const float *__restrict__ EV,
@@ -1425,19 +1427,22 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
     u1 = f32x4{r[16 + g], 0.f, 0.f, 0.f};
   };
   __shared__ f32x4 tile[64 * PT::kStride];
+  __shared__ f32x4 tile2[kRing == 2 ? 64 * PT::kStride : 1];
+  const float *td2 = reinterpret_cast<const float *>(tile2);
   __shared__ unsigned long long small_mask[kWavesPerBlock];
   const float *td = reinterpret_cast<const float *>(tile);
   float *tw = reinterpret_cast<float *>(tile);
   long long acc = 0;
   // one child's product U^T for the 4 sub-tiles from the LDS tile (mul: into P);
   // kQ: rows 16..19 of the lane's own site into Q (4x4x1 chain, k ascending)
-  auto product = [&](const float (&A)[2][5], const float *QA, f32x4 (&P)[4][2], f32x4 &Q, bool mul) {
+  auto product = [&](const float (&A)[2][5], const float *QA, f32x4 (&P)[4][2], f32x4 &Q, bool mul,
+                     const float *tb) {
     if constexpr (kAblate == 3) return;
     f32x4 q = {0.f, 0.f, 0.f, 0.f};
-    const float *xs = td + lane * kRow + c * S;  // the lane's own site row
+    const float *xs = tb + lane * kRow + c * S;  // the lane's own site row
 #pragma unroll
     for (int t = 0; t < 4; t++) {
-      const float *xr = td + (16 * t + lo16) * kRow + c * S + g;
+      const float *xr = tb + (16 * t + lo16) * kRow + c * S + g;
       float bv[5];
 #pragma unroll
       for (int st = 0; st < 5; st++) bv[st] = xr[4 * st];
@@ -1486,7 +1491,18 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
       const float *r = tab + c * kProtCodes * 20 + code_lane * 20 + 16;
       return f32x4{r[0], r[1], r[2], r[3]};
     };
-    if constexpr (T1) {
+    if constexpr (kRing == 2) {  // both children staged together
+      tile_put<float>(tile, pf);
+      tile_put<float>(tile2, pf2);
+      __syncthreads();
+      if (base + stride < n) {
+        tile_fetch<float>(x1, base + stride, n, pf);
+        tile_fetch<float>(x2, base + stride, n, pf2);
+      }
+      product(AL, QL, P, Q, false, td);
+      product(AR, QR, P, Q, true, td2);
+      __syncthreads();
+    } else if constexpr (T1) {
 #pragma unroll
       for (int t = 0; t < 4; t++) tip_u(tabs[0], code1, t, P[t][0], P[t][1]);
       if constexpr (kQ) Q = tip_q(tabs[0], code1);
@@ -1501,10 +1517,11 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
       } else if constexpr (kAblate != 2) {
         tile_fetch<float>(x2, base, n, pf);
       }
-      product(AL, QL, P, Q, false);
+      product(AL, QL, P, Q, false, td);
       __syncthreads();
     }
-    if constexpr (T2) {
+    if constexpr (kRing == 2) {
+    } else if constexpr (T2) {
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         f32x4 u0, u1;
@@ -1523,7 +1540,7 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
         __syncthreads();
         if (kAblate != 2 && base + stride < n) tile_fetch<float>(T1 ? x2 : x1, base + stride, n, pf);
       }
-      product(AR, QR, P, Q, true);
+      product(AR, QR, P, Q, true, td);
       __syncthreads();  // every wave is done reading x2: the tile takes X3 now
     }
     // kQ: lane group g gets p[16 + g] of sub-tile t's site lo16 as Qt[t]

@@ -150,6 +150,16 @@ int main(int argc, char **argv) {
     ADD("ring minw3 again", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 0, true>))
     ADD("ring minw2 again", 1, (&plf_prot_mfma32_kernel<true, 2, 0, 2, 0, true>))
   }
+  if (argc > 3 && atoi(argv[3]) == 6) {  // round-2 session: both children staged together
+    vs.clear();
+    ADD("readlane fma (r01, the check)", 1, (&plf_prot_kernel<float, true, true>))
+    ADD("product", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2>))
+    ADD("both minw3", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 0, 2>))
+    ADD("both minw2", 1, (&plf_prot_mfma32_kernel<true, 2, 0, 2, 0, 2>))
+    ADD("product again", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2>))
+    ADD("both minw3 again", 1, (&plf_prot_mfma32_kernel<true, 3, 0, 2, 0, 2>))
+    ADD("both minw2 again", 1, (&plf_prot_mfma32_kernel<true, 2, 0, 2, 0, 2>))
+  }
   std::vector<uint32_t> ref[2], got(n * 80);
   std::vector<uint8_t> rsc[2], gsc(n);
   int64_t rsum[2] = {0, 0}, gsum = 0;
