@@ -107,6 +107,41 @@ def test_one_context_from_several_host_threads(ctx, oracle):
     assert np.allclose(got[1], 2 * got[0], rtol=1e-12)  # weights 2 vs 1: lnL doubles
 
 
+def test_host_entry_from_several_threads(ctx, oracle):
+    """The synchronous plf() entry stages through ONE device buffer per context:
+    four threads calling it on the same context at once (different inputs) must
+    each get exactly their own reference result (the per-context lock)."""
+    import threading
+
+    n = 200_003
+    ins = [oracle.gen_hostmem(n, np.float64, 60 + i) for i in range(4)]
+    want = [oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], threads=4) for d in ins]
+    outs = [np.empty_like(d["x1"]) for d in ins]
+    incs = [None] * 4
+    errs = []
+    go = threading.Barrier(4)
+
+    def worker(i):
+        try:
+            d = ins[i]
+            go.wait()
+            for _ in range(3):
+                incs[i] = ctx.plf(d["x1"], d["x2"], outs[i], d["EV"], n, d["left"], d["right"], None)
+        except Exception as e:  # reported on the main thread
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errs, errs
+    for i in range(4):
+        e3, _, inc = want[i]
+        assert np.array_equal(bits(outs[i]), bits(e3))
+        assert incs[i] == inc
+
+
 def test_graph_capture_needs_a_warm_stream(ctx, oracle):
     """A stream's first sum-producing call may not be inside a capture (its
     workspace is allocated then): rejected with PlfxError.  After one call the
