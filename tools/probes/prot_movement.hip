@@ -12,6 +12,7 @@
 // Each form is checked against x1 + x2 elementwise.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/prot_movement.hip -o build/prot_movement
+//   (-DPROBE_CHUNKS=40: the f64 record, 640 B)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -26,7 +27,10 @@
   } while (0)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kChunks = 20;  // 16-B chunks per site record (80 floats)
+#ifndef PROBE_CHUNKS
+#define PROBE_CHUNKS 20
+#endif
+constexpr int kChunks = PROBE_CHUNKS;  // 16-B chunks per site record: 20 (f32, 80 floats) or 40 (f64)
 
 __global__ void fill(float *p, int64_t n, unsigned seed) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -38,28 +42,28 @@ __global__ void __launch_bounds__(256) mv_block(const f32x4 *__restrict__ x1, co
                                                 f32x4 *__restrict__ x3, int64_t tiles) {
   __shared__ f32x4 t1[64 * (kChunks + 1)], t2[64 * (kChunks + 1)];
   for (int64_t b = blockIdx.x; b < tiles; b += gridDim.x) {
-    f32x4 a[5], c[5];
+    f32x4 a[kChunks / 4], c[kChunks / 4];
 #pragma unroll
-    for (int i = 0; i < 5; i++) a[i] = __builtin_nontemporal_load(x1 + b * 1280 + threadIdx.x + 256 * i);
+    for (int i = 0; i < kChunks / 4; i++) a[i] = __builtin_nontemporal_load(x1 + b * (64 * kChunks) + threadIdx.x + 256 * i);
 #pragma unroll
-    for (int i = 0; i < 5; i++) c[i] = __builtin_nontemporal_load(x2 + b * 1280 + threadIdx.x + 256 * i);
+    for (int i = 0; i < kChunks / 4; i++) c[i] = __builtin_nontemporal_load(x2 + b * (64 * kChunks) + threadIdx.x + 256 * i);
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
+    for (int i = 0; i < kChunks / 4; i++) {
       const int j = threadIdx.x + 256 * i, s = j / kChunks, q = j % kChunks;
       t1[s * (kChunks + 1) + q] = a[i];
       t2[s * (kChunks + 1) + q] = c[i];
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 5; i++) {  // read back in another thread's order (site-major rows)
+    for (int i = 0; i < kChunks / 4; i++) {  // read back in another thread's order (site-major rows)
       const int j = threadIdx.x + 256 * i, s = j % 64, q = j / 64;
       t1[s * (kChunks + 1) + q] = t1[s * (kChunks + 1) + q] + t2[s * (kChunks + 1) + q];
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
+    for (int i = 0; i < kChunks / 4; i++) {
       const int j = threadIdx.x + 256 * i, s = j / kChunks, q = j % kChunks;
-      __builtin_nontemporal_store(t1[s * (kChunks + 1) + q], x3 + b * 1280 + j);
+      __builtin_nontemporal_store(t1[s * (kChunks + 1) + q], x3 + b * (64 * kChunks) + j);
     }
     __syncthreads();
   }
@@ -75,43 +79,43 @@ __global__ void __launch_bounds__(64 * kWaves) mv_wave(const f32x4 *__restrict__
   f32x4 *r1 = reg[w][0], *r2 = reg[w][1];
   const int64_t stride = (int64_t)gridDim.x * kWaves;
   int64_t s0 = (int64_t)blockIdx.x * kWaves + w;
-  f32x4 a[5], c[5];
+  f32x4 a[kChunks / 4], c[kChunks / 4];
   if (s0 < subs) {
 #pragma unroll
-    for (int i = 0; i < 5; i++) a[i] = __builtin_nontemporal_load(x1 + s0 * 320 + lane + 64 * i);
+    for (int i = 0; i < kChunks / 4; i++) a[i] = __builtin_nontemporal_load(x1 + s0 * (16 * kChunks) + lane + 64 * i);
 #pragma unroll
-    for (int i = 0; i < 5; i++) c[i] = __builtin_nontemporal_load(x2 + s0 * 320 + lane + 64 * i);
+    for (int i = 0; i < kChunks / 4; i++) c[i] = __builtin_nontemporal_load(x2 + s0 * (16 * kChunks) + lane + 64 * i);
   }
   for (int64_t s = s0; s < subs; s += stride) {
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
+    for (int i = 0; i < kChunks / 4; i++) {
       const int j = lane + 64 * i, st = j / kChunks, q = j % kChunks;
       r1[st * (kChunks + 1) + q] = a[i];
       r2[st * (kChunks + 1) + q] = c[i];
     }
     if (s + stride < subs) {
 #pragma unroll
-      for (int i = 0; i < 5; i++) a[i] = __builtin_nontemporal_load(x1 + (s + stride) * 320 + lane + 64 * i);
+      for (int i = 0; i < kChunks / 4; i++) a[i] = __builtin_nontemporal_load(x1 + (s + stride) * (16 * kChunks) + lane + 64 * i);
 #pragma unroll
-      for (int i = 0; i < 5; i++) c[i] = __builtin_nontemporal_load(x2 + (s + stride) * 320 + lane + 64 * i);
+      for (int i = 0; i < kChunks / 4; i++) c[i] = __builtin_nontemporal_load(x2 + (s + stride) * (16 * kChunks) + lane + 64 * i);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
+    for (int i = 0; i < kChunks / 4; i++) {
       const int j = lane + 64 * i, st = j % 16, q = j / 16;
       r1[st * (kChunks + 1) + q] = r1[st * (kChunks + 1) + q] + r2[st * (kChunks + 1) + q];
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    f32x4 o[5];
+    f32x4 o[kChunks / 4];
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
+    for (int i = 0; i < kChunks / 4; i++) {
       const int j = lane + 64 * i, st = j / kChunks, q = j % kChunks;
       o[i] = r1[st * (kChunks + 1) + q];
     }
 #pragma unroll
-    for (int i = 0; i < 5; i++) __builtin_nontemporal_store(o[i], x3 + s * 320 + lane + 64 * i);
+    for (int i = 0; i < kChunks / 4; i++) __builtin_nontemporal_store(o[i], x3 + s * (16 * kChunks) + lane + 64 * i);
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -180,11 +184,11 @@ int main(int argc, char **argv) {
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       v.us.push_back(ms * 1000.f / reps);
     }
-  printf("n=%lld sites, 960 B/site moved, %d reps x %d rounds, %d buffer sets\n", (long long)n, reps, rounds, R);
+  printf("n=%lld sites, %d B/site moved, %d reps x %d rounds, %d buffer sets\n", (long long)n, 48 * kChunks, reps, rounds, R);
   for (auto &v : vs) {
     std::sort(v.us.begin(), v.us.end());
     const double t = v.us[v.us.size() / 2] * 1e-6;
-    printf("%-45s median %8.2f us  %5.1f%% of 8 TB/s\n", v.name, v.us[v.us.size() / 2], 100.0 * 960.0 * n / t / 8e12);
+    printf("%-45s median %8.2f us  %5.1f%% of 8 TB/s\n", v.name, v.us[v.us.size() / 2], 100.0 * 48.0 * kChunks * n / t / 8e12);
   }
   return 0;
 }
