@@ -69,6 +69,44 @@ __global__ void __launch_bounds__(256) mv_block(const f32x4 *__restrict__ x1, co
   }
 }
 
+// block form with x3 stored straight from registers in the f32 MFMA kernel's
+// output layout (wave = category c; sub-tile t: lane (lo16, g) holds chunk
+// 5c + g of site 16t + lo16; then lane l holds chunk 5c + 4 of site l): 64-B
+// pieces at a 320-B stride instead of whole coalesced records (f32 only)
+#if PROBE_CHUNKS == 20
+__global__ void __launch_bounds__(256) mv_block_scatter(const f32x4 *__restrict__ x1, const f32x4 *__restrict__ x2,
+                                                        f32x4 *__restrict__ x3, int64_t tiles) {
+  __shared__ f32x4 t1[64 * (kChunks + 1)], t2[64 * (kChunks + 1)];
+  const int c = threadIdx.x >> 6, lane = threadIdx.x & 63, lo16 = lane & 15, g = lane >> 4;
+  for (int64_t b = blockIdx.x; b < tiles; b += gridDim.x) {
+    f32x4 a[5], d[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) a[i] = __builtin_nontemporal_load(x1 + b * 1280 + threadIdx.x + 256 * i);
+#pragma unroll
+    for (int i = 0; i < 5; i++) d[i] = __builtin_nontemporal_load(x2 + b * 1280 + threadIdx.x + 256 * i);
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const int j = threadIdx.x + 256 * i, s = j / kChunks, q = j % kChunks;
+      t1[s * (kChunks + 1) + q] = a[i];
+      t2[s * (kChunks + 1) + q] = d[i];
+    }
+    __syncthreads();
+    f32x4 o[5];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int s = 16 * t + lo16, q = 5 * c + g;
+      o[t] = t1[s * (kChunks + 1) + q] + t2[s * (kChunks + 1) + q];
+    }
+    o[4] = t1[lane * (kChunks + 1) + 5 * c + 4] + t2[lane * (kChunks + 1) + 5 * c + 4];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+      __builtin_nontemporal_store(o[t], x3 + b * 1280 + (16 * t + lo16) * kChunks + 5 * c + g);
+    __builtin_nontemporal_store(o[4], x3 + b * 1280 + lane * kChunks + 5 * c + 4);
+  }
+}
+#endif
+
 // wave form: 16 sites x 20 chunks = 320 chunks per child, 5 per lane; a private
 // LDS region per wave, the next sub-tile's loads issued before this one's LDS work
 template <int kWaves>
@@ -151,6 +189,10 @@ int main(int argc, char **argv) {
                 [](const Set &s, int g) { mv_wave<4><<<g, 256>>>(s.x1, s.x2, s.x3, 0); }, {}});
   vs.push_back({"wave x4, 3 blocks/CU", 3 * CUs, 256,
                 [](const Set &s, int g) { mv_wave<4><<<g, 256>>>(s.x1, s.x2, s.x3, 0); }, {}});
+#if PROBE_CHUNKS == 20
+    vs.push_back({"block, x3 scattered from registers (MFMA layout)", occ((const void *)mv_block_scatter, 256) * CUs, 256,
+                  [](const Set &s, int g) { mv_block_scatter<<<g, 256>>>(s.x1, s.x2, s.x3, 0); }, {}});
+#endif
   vs.push_back({"stream (registers)", 2 * CUs, 256,
                 [](const Set &s, int g) { mv_stream<<<g, 256>>>(s.x1, s.x2, s.x3, 0); }, {}});
   // the lambdas cannot capture n: pass it through a global
@@ -158,7 +200,10 @@ int main(int argc, char **argv) {
   gN = n;
   vs[0].run = [](const Set &s, int g) { mv_block<<<g, 256>>>(s.x1, s.x2, s.x3, gN / 64); };
   for (int i = 1; i <= 3; i++) vs[i].run = [](const Set &s, int g) { mv_wave<4><<<g, 256>>>(s.x1, s.x2, s.x3, gN / 16); };
-  vs[4].run = [](const Set &s, int g) { mv_stream<<<g, 256>>>(s.x1, s.x2, s.x3, gN * kChunks); };
+#if PROBE_CHUNKS == 20
+  vs[4].run = [](const Set &s, int g) { mv_block_scatter<<<g, 256>>>(s.x1, s.x2, s.x3, gN / 64); };
+#endif
+  vs.back().run = [](const Set &s, int g) { mv_stream<<<g, 256>>>(s.x1, s.x2, s.x3, gN * kChunks); };
   std::vector<float> h1(chunks * 4), h2(chunks * 4), h3(chunks * 4);
   CK(hipMemcpy(h1.data(), sets[0].x1, chunks * 16, hipMemcpyDeviceToHost));
   CK(hipMemcpy(h2.data(), sets[0].x2, chunks * 16, hipMemcpyDeviceToHost));
