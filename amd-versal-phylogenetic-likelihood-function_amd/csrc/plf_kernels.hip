@@ -186,14 +186,14 @@ hipError_t launch_prot_t(const DnaArgs &a, int max_blocks, hipStream_t s, const 
   // (tools/tune_prot32.hip, profiles/r02_tune_protein_f32.log)
   if constexpr (kFma) {
     static int cache = 0;
-    auto kernel = &dev::plf_prot_mfma32_kernel<kSum, 3, kTips, 2>;
+    auto kernel = &dev::plf_prot_mfma32_kernel<kSum, 3, kTips>;
     const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
     hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
                        (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,
                        (const T *)a.right, a.wgt, a.scaler, a.n, a.ws, a.scaler_sum, tipvec);
   } else {
     static int cache = 0;
-    auto kernel = &dev::plf_prot_lds_kernel<T, kFma, kSum, 2, kTips, 4>;
+    auto kernel = &dev::plf_prot_lds_kernel<T, kSum, 2, kTips, 4, false>;
     const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
     hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
                        (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,
@@ -209,7 +209,7 @@ hipError_t launch_prot_mfma_t(const DnaArgs &a, int max_blocks, hipStream_t s,
   // X3 to LDS through permuted back-transform rows (kX3 = 2: conflict-free
   // b128 writes; 90.2 vs 91.2 us at 2^18, 342 vs 345 at 2^20, tools/tune_prot.hip,
   // profiles/r02_tune_protein_v3.log); first tile's loads before the matrix fragments
-  auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, true, 0, true, kTips, 2, true>;
+  auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, kTips>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV,
@@ -223,7 +223,7 @@ hipError_t launch_prot_exact64_t(const DnaArgs &a, int max_blocks, hipStream_t s
                                  const double *tipvec) {
   static int cache = 0;
   // 10-row groups + tile prefetch (tools/tune_prot.hip, profiles/r02_tune_protein_exact_rows.log)
-  auto kernel = &dev::plf_prot_lds_kernel<double, false, kSum, 2, kTips, 10, true, false, true>;
+  auto kernel = &dev::plf_prot_lds_kernel<double, kSum, 2, kTips, 10, true>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV,
@@ -289,7 +289,7 @@ hipError_t launch_septets_t(const dev::SeptetBatch &b, int count, const double *
   static int cache = 0;
   // next-trip prefetch for dense leaves only: with coded leaves the pass is
   // write-bound and the prefetch registers cost 4-4.5 % (r01_ab_fused_tips.log)
-  auto kernel = &dev::plf_dna_f64_septet_kernel<kSum, 1, kNtl64, kTips, true, kSeptetU, kTips == 0>;
+  auto kernel = &dev::plf_dna_f64_septet_kernel<kSum, 1, kNtl64, kTips, kSeptetU, kTips == 0>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 8 * kSeptetU, count,
                             max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt,

@@ -15,7 +15,7 @@
 #include <string>
 #include <vector>
 
-#include "plf_dna.hpp"
+#include "plf_dna_tune.hpp"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 

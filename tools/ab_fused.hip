@@ -87,27 +87,27 @@ int main(int argc, char **argv) {
   }
   const double kSep = 15 * 128 + 4, kTri = 7 * 128 + 4;
   // tip kinds: the leaves are read as one code byte (g[] then points at CLV data, read as bytes)
-  ADD("A septet tips=1 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 1, true, 2, true>), sa, 8, 4 * 128 + 4 + 4 + 7 * 128)
-  ADD("A septet tips=1 U=2 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 1, true, 2, false>), sa, 8, 4 * 128 + 4 + 4 + 7 * 128)
-  ADD("A septet tips=2 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, true, 2, true>), sa, 8, 8 + 4 + 7 * 128)
-  ADD("A septet tips=2 U=2 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, true, 2, false>), sa, 8, 8 + 4 + 7 * 128)
-  ADD("A septet tips=2 U=4 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, true, 4, false>), sa, 8, 8 + 4 + 7 * 128)
-  ADD("A septet tips=2 U=4pf x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, true, 4, true>), sa, 8, 8 + 4 + 7 * 128)
-  ADD("A septet tips=2 U=1pf x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, true, 1, true>), sa, 8, 8 + 4 + 7 * 128)
-  ADD("A septet tips=2 minw2 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 2, true, 2, true, 2, true>), sa, 8, 8 + 4 + 7 * 128)
+  ADD("A septet tips=1 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 1, 2, true>), sa, 8, 4 * 128 + 4 + 4 + 7 * 128)
+  ADD("A septet tips=1 U=2 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 1, 2, false>), sa, 8, 4 * 128 + 4 + 4 + 7 * 128)
+  ADD("A septet tips=2 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, 2, true>), sa, 8, 8 + 4 + 7 * 128)
+  ADD("A septet tips=2 U=2 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, 2, false>), sa, 8, 8 + 4 + 7 * 128)
+  ADD("A septet tips=2 U=4 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, 4, false>), sa, 8, 8 + 4 + 7 * 128)
+  ADD("A septet tips=2 U=4pf x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, 4, true>), sa, 8, 8 + 4 + 7 * 128)
+  ADD("A septet tips=2 U=1pf x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 2, 1, true>), sa, 8, 8 + 4 + 7 * 128)
+  ADD("A septet tips=2 minw2 x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 2, true, 2, 2, true>), sa, 8, 8 + 4 + 7 * 128)
   ADD("A triple tips=2 x10", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 2, 1>), ta, 10, 4 + 4 + 3 * 128)
   ADD("A triple tips=1 U=2 x10", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 1, 2>), ta, 10, 2 * 128 + 4 + 4 + 3 * 128)
   ADD("A triple tips=1 U=1 x10", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 1, 1>), ta, 10, 2 * 128 + 4 + 4 + 3 * 128)
   ADD("A triple tips=2 U=2 x10", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 2, 2>), ta, 10, 4 + 4 + 3 * 128)
-  ADD("A septet U=2 pf  x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, true>), sa, 8, kSep)
+  ADD("A septet U=2 pf  x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, 2, true>), sa, 8, kSep)
   ADD("B septet U=2 pf  x8", (&plfx::dev_b::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, true>), sb, 8, kSep)
-  ADD("A septet U=2     x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, false>), sa, 8, kSep)
+  ADD("A septet U=2     x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, 2, false>), sa, 8, kSep)
   ADD("B septet U=2     x8", (&plfx::dev_b::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, false>), sb, 8, kSep)
-  ADD("A septet U=4     x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 4, false>), sa, 8, kSep)
-  ADD("A septet U=2 pf  x1", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, true>), sa, 1, kSep)
+  ADD("A septet U=4     x8", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, 4, false>), sa, 8, kSep)
+  ADD("A septet U=2 pf  x1", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, 2, true>), sa, 1, kSep)
   ADD("B septet U=2 pf  x1", (&plfx::dev_b::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, true>), sb, 1, kSep)
-  ADD("A septet U=2     x1", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 2, false>), sa, 1, kSep)
-  ADD("A septet U=1     x1", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, true, 1, false>), sa, 1, kSep)
+  ADD("A septet U=2     x1", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, 2, false>), sa, 1, kSep)
+  ADD("A septet U=1     x1", (&plfx::dev::plf_dna_f64_septet_kernel<true, 1, true, 0, 1, false>), sa, 1, kSep)
   ADD("A triple x10", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 0, 1>), ta, 10, kTri)
   ADD("B triple x10", (&plfx::dev_b::plf_dna_f64_triple_kernel<true, 1, true, 0, 1>), tb, 10, kTri)
   ADD("A triple x4", (&plfx::dev::plf_dna_f64_triple_kernel<true, 1, true, 0, 1>), ta, 4, kTri)

@@ -1,5 +1,6 @@
 // ab_prot.hip -- interleaved A/B of the protein f64 FMA (matrix-core) kernel
-// (tuning only): A = csrc/plf_prot.hpp, B = B_HEADER (another copy next to its
+// (tuning only): A = tools/plf_prot_tune.hpp (the round-2 product form and its
+// knobs), B = B_HEADER (another copy next to its
 // own plf_dna.hpp, under plfx::dev_b); 2^18 sites, rotating buffer sets.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
@@ -13,7 +14,7 @@
 #include <string>
 #include <vector>
 
-#include "plf_prot.hpp"
+#include "plf_prot_tune.hpp"
 #define dev dev_b
 #include B_HEADER
 #undef dev
@@ -63,15 +64,12 @@ int main(int argc, char **argv) {
   }
   ADD("A mfma (csrc)", (&plfx::dev::plf_prot_mfma_kernel<true>))
   ADD("B mfma (" B_HEADER ")", (&plfx::dev_b::plf_prot_mfma_kernel<true>))
-  ADD("A exact (csrc)", (&plfx::dev::plf_prot_exact_f64_kernel<true>))
   ADD("A mfma tip/inner (codes in x1)", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 0, true, 1>))
   ADD("B mfma tip/inner (codes in x1)", (&plfx::dev_b::plf_prot_mfma_kernel<true, 2, true, 0, true, 1>))
-  ADD("A exact tip/inner", (&plfx::dev::plf_prot_exact_f64_kernel<true, 2, 1>))
   ADD("A mfma tip/inner ablate: no MFMA", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 1, true, 1>))
   ADD("A mfma tip/inner ablate: no HBM", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 2, true, 1>))
   ADD("A mfma ablate: no MFMA", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 1, true, 0>))
   ADD("A mfma ablate: no HBM", (&plfx::dev::plf_prot_mfma_kernel<true, 2, true, 2, true, 0>))
-  ADD("B exact (" B_HEADER ")", (&plfx::dev_b::plf_prot_exact_f64_kernel<true>))
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int r = 0; r < rounds; r++)
     for (auto &v : vs) {

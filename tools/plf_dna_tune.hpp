@@ -1,5 +1,11 @@
-// plf_dna.hpp -- device code of the fused DNA PLF kernels (instantiated by
-// plf_kernels.hip; the tuning harnesses in tools/ include it too).
+// plf_dna_tune.hpp -- TUNING COPY (not product code): csrc/plf_dna.hpp as it
+// stood at the end of round 2, with the measured-and-not-adopted kDefer knob
+// and block_ticket_sum_flush and the septet kernel's kLds knob, for
+// tools/ab_defer.hip and tools/tune_septet.hip.  Include it INSTEAD of
+// csrc/plf_dna.hpp (same names, same namespace).
+//
+// plf_dna.hpp -- device code of the fused DNA PLF kernel (shared by
+// plf_kernels.hip and the tuning harness tools/tune_plf.hip).
 //
 // Semantics: app/src/plf.cpp:19-65 (+ s2mm scaler byte,
 // hls/src/s2mm_memDNAwindowComb.cpp:70-97, and the weighted scaler sum,
@@ -121,6 +127,44 @@ __device__ inline void block_ticket_sum(long long v, unsigned long long *wsu, in
 #pragma unroll
   for (int i = 0; i < kWavesPerBlock; i++) tot += part[i];
   ticket_publish(tot, wsu, out);
+}
+
+// block_ticket_sum with the block's last stores issued between the ticket's
+// atomic and the wait for its result: `flush` (run by every thread) stores the
+// outputs a kernel held back from its final trip.  A returned atomic waits for
+// every earlier vector-memory operation of its wave (one vmcnt on CDNA), so
+// issued after the final stores the ticket's two round trips queue behind the
+// store acknowledgements; issued first they overlap them.
+template <typename F>
+__device__ inline void block_ticket_sum_flush(long long v, unsigned long long *wsu, int64_t *out,
+                                              F &&flush) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __shared__ long long partf[kWavesPerBlock];
+  if ((threadIdx.x & 63) == 0) partf[threadIdx.x >> 6] = v;
+  __syncthreads();
+  long long *ws = reinterpret_cast<long long *>(wsu);
+  const long long G = gridDim.x;
+  const long long slot = blockIdx.x % kSlots;
+  long long tot = 0, old = 0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < kWavesPerBlock; i++) tot += partf[i];
+    old = __hip_atomic_fetch_add(ws + slot * 16, kTick + tot, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+  }
+  flush();
+  if (threadIdx.x != 0) return;
+  const long long nslots = G < kSlots ? G : kSlots;
+  const long long arrivals = (G - slot + kSlots - 1) / kSlots;
+  if (decode_count(old) != arrivals - 1) return;
+  const long long slot_sum = old + kTick + tot - arrivals * kTick;
+  __hip_atomic_store(ws + slot * 16, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long told = __hip_atomic_fetch_add(ws + kSlots * 16, kTick + slot_sum, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+  if (decode_count(told) != nslots - 1) return;
+  if (out) *out = (int64_t)(told + kTick + slot_sum - nslots * kTick);
+  __hip_atomic_store(ws + kSlots * 16, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Three independent sums (consecutive kWsWords regions of ws), published by
@@ -257,8 +301,11 @@ __device__ __forceinline__ void site_cat_tips(const T (&a)[4], const T (&b)[4], 
 
 // Knobs: U = 16-site wave steps per loop trip (bytes in flight per lane =
 // 2*U*4*sizeof(T)); NT = non-temporal CLV loads; kSum = produce the weighted
-// scaler sum; kMinWaves = __launch_bounds__ occupancy hint (waves per SIMD).
-template <typename T, int U, bool kSum, bool NT, bool T1 = false, bool T2 = false>
+// scaler sum; kMinWaves = __launch_bounds__ occupancy hint (waves per SIMD);
+// kDefer = a wave's final full trip keeps its outputs in registers and stores
+// them after the block's scaler-sum ticket is issued (block_ticket_sum_flush).
+template <typename T, int U, bool kSum, bool NT, bool T1 = false, bool T2 = false,
+          bool kDefer = false>
 __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *__restrict__ x2,
                                              T *__restrict__ x3, const T *__restrict__ EV,
                                              const T *__restrict__ left, const T *__restrict__ right,
@@ -292,6 +339,10 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
   const int64_t nfull = n - (16 * U - 1);  // base < nfull  <=>  whole step in range
 
   int64_t base = wave * 16 * U;
+  constexpr bool kHold = kDefer && kSum;
+  T held[kHold ? U : 1][4];  // kDefer: the final full trip's outputs
+  bool heldsc[kHold ? U : 1];
+  int64_t heldbase = -1;
   // full steps: no bounds checks, every load of the step issued up front
   for (; base < nfull; base += stride) {
     T a[U][4], b[U][4];
@@ -305,6 +356,8 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
       else Num<T>::template load4<NT>(x2 + site * 16 + c * 4, b[u]);
       if (kSum) w[u] = wgt_at(wgt, site, ws);
     }
+    // the wave's last trip (no further full step, no tail): held back
+    const bool hold = kHold && base + stride >= n;
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int64_t site = base + u * 16 + q;
@@ -323,12 +376,20 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
         const T s = o[l] * Num<T>::two32();  // exact: power-of-two scaling
         o[l] = sc ? s : o[l];
       }
-      Num<T>::store4_nt(x3 + site * 16 + c * 4, o);
-      if (c == 0) {
-        if (scaler) scaler[site] = (uint8_t)sc;
+      if (hold) {
+        const int uu = kHold ? u : 0;
+#pragma unroll
+        for (int l = 0; l < 4; l++) held[uu][l] = o[l];
+        heldsc[uu] = sc;
+      } else {
+        Num<T>::store4_nt(x3 + site * 16 + c * 4, o);
+        if (c == 0) {
+          if (scaler) scaler[site] = (uint8_t)sc;
+        }
       }
       if (kSum) acc += (c == 0 && sc) ? (long long)w[u] : 0ll;
     }
+    if (hold) heldbase = base;
   }
   // tail (at most one partial step per wave)
   if (base < n) {
@@ -367,17 +428,30 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
       }
     }
   }
-  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+  if constexpr (kHold) {
+    block_ticket_sum_flush(acc, ws, scaler_sum, [&] {
+      if (heldbase < 0) return;
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t site = heldbase + u * 16 + q;
+        Num<T>::store4_nt(x3 + site * 16 + c * 4, held[u]);
+        if (c == 0 && scaler) scaler[site] = (uint8_t)heldsc[u];
+      }
+    });
+  } else if constexpr (kSum) {
+    block_ticket_sum(acc, ws, scaler_sum);
+  }
 }
 
-template <typename T, int U, bool kSum, bool NT, int kMinWaves>
+template <typename T, int U, bool kSum, bool NT, int kMinWaves, bool kDefer = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
                const T *__restrict__ EV, const T *__restrict__ left,
                const T *__restrict__ right, const int32_t *__restrict__ wgt,
                uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
                int64_t *scaler_sum) {
-  dna_cat_body<T, U, kSum, NT>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum);
+  dna_cat_body<T, U, kSum, NT, false, false, kDefer>(x1, x2, x3, EV, left, right, wgt, scaler, n,
+                                                      ws, scaler_sum);
 }
 
 // f64 DNA kernel, lane-pair mapping: every wave memory instruction touches one
@@ -397,7 +471,8 @@ __device__ __forceinline__ f64x2 ld16(const f64x2 *p) {
 
 // T1/T2: child 1/2 is a tip (one state code per site, see build_tip_table);
 // its lane pair reads ump[2h], ump[2h+1] as one 16-B LDS row slice.
-template <int U, bool kSum, bool NTL, bool T1 = false, bool T2 = false>
+// kDefer: as dna_cat_body's (final full trip's stores after the ticket).
+template <int U, bool kSum, bool NTL, bool T1 = false, bool T2 = false, bool kDefer = false>
 __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
                                               const double *__restrict__ x2,
                                               double *__restrict__ x3,
@@ -440,9 +515,14 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
   const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
   const int64_t nfull = n - (16 * U - 1);
 
-  // one 8-site block: loads are done by the caller
+  constexpr bool kHold = kDefer && kSum;
+  f64x2 held[kHold ? U : 1][2];  // kDefer: the final full trip's outputs
+  bool heldsc[kHold ? U : 1][2];
+  int64_t heldbase = -1;
+  // one 8-site block: loads are done by the caller; keep != nullptr holds the
+  // output (and *keepsc the scale flag) instead of storing it
   auto body = [&](const f64x2 a, const f64x2 b, int k1, int k2, int64_t site0, bool valid,
-                  int w) {
+                  int w, f64x2 *keep = nullptr, bool *keepsc = nullptr) {
     double u1[2], u2[2];
     if constexpr (T1) {
       const f64x2 r = *reinterpret_cast<const f64x2 *>(tab1 + trow + 4 * k1);
@@ -493,8 +573,13 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
     }
     if (valid) {
       f64x2 ov = {o[0], o[1]};
-      __builtin_nontemporal_store(ov, reinterpret_cast<f64x2 *>(x3 + site0 * 16) + lane);
-      if ((lane & 7) == 0 && scaler) scaler[site0 + g] = (uint8_t)sc;
+      if (keep) {
+        *keep = ov;
+        *keepsc = sc;
+      } else {
+        __builtin_nontemporal_store(ov, reinterpret_cast<f64x2 *>(x3 + site0 * 16) + lane);
+        if ((lane & 7) == 0 && scaler) scaler[site0 + g] = (uint8_t)sc;
+      }
       if ((lane & 7) == 0) {
         if (kSum && sc) acc += w;
       }
@@ -516,12 +601,18 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
         else b[u][j] = ld16<NTL>(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
         if (kSum) w[u][j] = wgt ? wgt[site0 + g] : 1;  // (wgt_at measured 1.6 % slower here)
       }
+    // the wave's last trip (no further full step, no tail): held back
+    const bool hold = kHold && base + stride >= n;
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
-      for (int j = 0; j < 2; j++)
+      for (int j = 0; j < 2; j++) {
+        const int uu = kHold ? u : 0;
         body(T1 ? f64x2{} : a[u][j], T2 ? f64x2{} : b[u][j], T1 ? k1[u][j] : 0,
-             T2 ? k2[u][j] : 0, base + u * 16 + j * 8, true, kSum ? w[u][j] : 0);
+             T2 ? k2[u][j] : 0, base + u * 16 + j * 8, true, kSum ? w[u][j] : 0,
+             hold ? &held[uu][j] : nullptr, hold ? &heldsc[uu][j] : nullptr);
+      }
+    if (hold) heldbase = base;
   }
   if (base < n) {  // tail: at most one partial step per wave
 #pragma unroll
@@ -542,17 +633,32 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
         body(a, b, k1, k2, site0, valid, w);
       }
   }
-  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+  if constexpr (kHold) {
+    block_ticket_sum_flush(acc, ws, scaler_sum, [&] {
+      if (heldbase < 0) return;
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const int64_t site0 = heldbase + u * 16 + j * 8;
+          __builtin_nontemporal_store(held[u][j], reinterpret_cast<f64x2 *>(x3 + site0 * 16) + lane);
+          if ((lane & 7) == 0 && scaler) scaler[site0 + g] = (uint8_t)heldsc[u][j];
+        }
+    });
+  } else if constexpr (kSum) {
+    block_ticket_sum(acc, ws, scaler_sum);
+  }
 }
 
-template <int U, bool kSum, int kMinWaves, bool NTL = false>
+template <int U, bool kSum, int kMinWaves, bool NTL = false, bool kDefer = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_f64_pair_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                         double *__restrict__ x3, const double *__restrict__ EV,
                         const double *__restrict__ left, const double *__restrict__ right,
                         const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
                         unsigned long long *ws, int64_t *scaler_sum) {
-  dna_pair_body<U, kSum, NTL>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum);
+  dna_pair_body<U, kSum, NTL, false, false, kDefer>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws,
+                                                    scaler_sum);
 }
 
 // Batched inner-node updates: one launch evaluates gridDim.y <= kMaxBatch
@@ -985,12 +1091,13 @@ __device__ inline void block_ticket_sum7(const long long (&v)[7], unsigned long 
   ticket_publish(tot, wsu + (size_t)t * kWsWords, out[t]);
 }
 
-// The matrices are re-read from LDS on every trip (an opaque zero offset
+// kLds: re-read the matrices from LDS on every trip (an opaque zero offset
 // stops the compiler hoisting the 224 loop-invariant values into registers),
 // trading LDS traffic for occupancy.  U: 8-site blocks per trip (one matrix
 // read serves all U).  kPf: issue the next trip's loads before this trip's
 // arithmetic (software pipelining; twice the input registers).
-template <bool kSum, int kMinWaves, bool NTL, int kTips, int U = 1, bool kPf = false>
+template <bool kSum, int kMinWaves, bool NTL, int kTips, bool kLds = true, int U = 1,
+          bool kPf = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
                           const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
@@ -1057,7 +1164,7 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
   if constexpr (kPf) fetch(wave * 8 * U, nxt);
   for (int64_t base = wave * 8 * U; base < n; base += stride) {
     int z = 0;
-    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    if constexpr (kLds) asm volatile("s_mov_b32 %0, 0" : "=s"(z));
     const double *mz = &mats[0][0] + z;
     Trip cur;
     if constexpr (kPf) {  // the next trip's loads stay in flight while this one computes

@@ -1,15 +1,21 @@
 // clock_drift.hip -- probe (not product code): per-launch duration of the
-// protein FMA kernel and of the headline DNA f64 kernel over a long run of
-// back-to-back launches, and the shader clock between launches.  Every K-th
-// launch is followed by a one-wave probe that spins 3 us and reports
-// d(s_memtime) / d(s_memrealtime) x 100 MHz -- the clock the chip holds right
-// after that launch (MI355X_MICROARCH.md, DVFS give-back item 6).
+// protein FMA kernel and of the headline DNA f64 kernel over runs of
+// back-to-back launches that start from an idle GPU, and the shader clock
+// between launches.  Round 3: the round-2 form measured the clock only in a
+// second, already-warm pass; tools/probes/warm_transient.py then showed the
+// slow launches come back after any idle gap (0.3 s is enough), so every pass
+// here starts after `idle_ms` of idle, and the probe pass comes first.  A probe
+// after a launch is one wave that spins 3 us and reports d(s_memtime) /
+// d(s_memrealtime) x 100 MHz -- the clock the chip holds right after that
+// launch (MI355X_MICROARCH.md, DVFS give-back item 6).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //     -I amd-versal-phylogenetic-likelihood-function_amd/csrc tools/probes/clock_drift.hip -o build/clock_drift
-//   build/clock_drift [launches] [probe_every]
+//   build/clock_drift [launches] [probe_every] [idle_ms]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -47,7 +53,8 @@ struct Set { double *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
 
 int main(int argc, char **argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 400;
-  const int K = argc > 2 ? atoi(argv[2]) : 5;
+  const int K = argc > 2 ? atoi(argv[2]) : 1;
+  const int idle_ms = argc > 3 ? atoi(argv[3]) : 2000;
   hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
   const int CUs = prop.multiProcessorCount;
   const int R = 4;
@@ -67,8 +74,8 @@ int main(int argc, char **argv) {
     fill<<<2048, 256>>>(s.x2, vals, 20 + (&s - sets.data()), 1.0, 80);
   }
   CK(hipDeviceSynchronize());
-  auto prot = &plf_prot_mfma_kernel<true, 2, true, 0, true, 0, false, true>;
-  auto dna = &plf_dna_f64_pair_kernel<2, true, 1, true, false>;
+  auto prot = &plf_prot_mfma_kernel<true, 2, 0>;
+  auto dna = &plf_dna_f64_pair_kernel<2, true, 1, true>;
   int op = 0, od = 0;
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&op, prot, kBlock, 0));
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&od, dna, kBlock, 0));
@@ -76,9 +83,12 @@ int main(int argc, char **argv) {
   std::vector<hipEvent_t> ev(2 * N);
   for (auto &evt : ev) CK(hipEventCreate(&evt));
   for (int which = 0; which < 2; which++) {
-    for (int pass = 0; pass < 2; pass++) {  // pass 0: no probes; pass 1: probe every K-th launch
+    // pass 0: after idle, probe every K-th launch; pass 1: straight on, no
+    // probes; pass 2: after idle again, no probes
+    for (int pass = 0; pass < 3; pass++) {
       CK(hipMemset(clk, 0, N * sizeof(float)));
       CK(hipDeviceSynchronize());
+      if (pass != 1) std::this_thread::sleep_for(std::chrono::milliseconds(idle_ms));
       for (int i = 0; i < N; i++) {
         const Set &s = sets[i % R];
         CK(hipEventRecord(ev[2 * i], 0));
@@ -89,7 +99,7 @@ int main(int argc, char **argv) {
           hipLaunchKernelGGL(dna, dim3(gd), dim3(kBlock), 0, 0, s.x1, s.x2, s.x3, EV, L, Rm, (const int32_t *)nullptr,
                              s.sc, nd, ws, s.sum);
         CK(hipEventRecord(ev[2 * i + 1], 0));
-        if (pass == 1 && i % K == K - 1) clk_probe<<<1, 64>>>(clk, i);
+        if (pass == 0 && i % K == K - 1) clk_probe<<<1, 64>>>(clk, i);
       }
       CK(hipDeviceSynchronize());
       CK(hipGetLastError());
@@ -97,9 +107,9 @@ int main(int argc, char **argv) {
       CK(hipMemcpy(mhz.data(), clk, N * sizeof(float), hipMemcpyDeviceToHost));
       for (int i = 0; i < N; i++) { CK(hipEventElapsedTime(&us[i], ev[2 * i], ev[2 * i + 1])); us[i] *= 1000.f; }
       float t0; CK(hipEventElapsedTime(&t0, ev[0], ev[2 * N - 1]));
+      static const char *what[3] = {"after idle, clock probes", "straight on, no probes", "after idle, no probes"};
       printf("%s pass %d (%s): %d launches in %.1f ms; per-launch us in windows of %d:\n",
-             which ? "dna f64 pair 2^20" : "protein fma 2^18", pass, pass ? "clock probes" : "no probes",
-             N, t0, N / 20);
+             which ? "dna f64 pair 2^20" : "protein fma 2^18", pass, what[pass], N, t0, N / 20);
       for (int w = 0; w < 20; w++) {
         std::vector<float> v(us.begin() + w * (N / 20), us.begin() + (w + 1) * (N / 20));
         std::sort(v.begin(), v.end());

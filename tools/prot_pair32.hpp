@@ -5,7 +5,7 @@
 // halving the VALU instructions and LDS broadcasts per site does not pay at two
 // blocks per CU (its 234 VGPRs) against three.
 #pragma once
-#include "plf_prot.hpp"
+#include "plf_prot_tune.hpp"
 
 namespace plfx {
 namespace dev {

@@ -10,7 +10,7 @@
 // instead of four 2-way-conflicted ds_write_b64.  Arithmetic and k order
 // as plf_prot_mfma_kernel (bit-identical results).
 #pragma once
-#include "plf_prot.hpp"
+#include "plf_prot_tune.hpp"
 
 namespace plfx {
 namespace dev {

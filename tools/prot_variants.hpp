@@ -11,7 +11,7 @@
 // kScalar: matrix values come from scalar loads (s_load through the scalar
 // cache) instead of v_readlane broadcasts of lane-distributed registers.
 #pragma once
-#include "plf_prot.hpp"
+#include "plf_prot_tune.hpp"
 
 namespace plfx {
 namespace dev {

@@ -14,7 +14,7 @@
 #include <vector>
 
 #include "plf_dna.hpp"
-#include "plf_prot.hpp"
+#include "plf_prot_tune.hpp"
 
 using namespace plfx::dev;
 
@@ -197,7 +197,7 @@ int main(int argc, char **argv) {
                            occ((const void *)k), (long long)grid, (long long)np);                  \
     vs.push_back({nm, [=](const Set &s) {                                                          \
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, PEV, PL, PR,  \
-                         s.wgt, s.sc, np, ws, s.sum); }, {}});                                     \
+                         s.wgt, s.sc, np, ws, s.sum, (const double *)nullptr); }, {}});           \
   }
   double *PEV, *PL, *PR;
   CK(hipMalloc(&PEV, 400 * 8)); CK(hipMalloc(&PL, 1600 * 8)); CK(hipMalloc(&PR, 1600 * 8));

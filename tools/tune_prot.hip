@@ -14,7 +14,7 @@
 #include <string>
 #include <vector>
 
-#include "plf_prot.hpp"
+#include "plf_prot_tune.hpp"
 #include "prot_variants.hpp"
 #include "prot_v8.hpp"
 

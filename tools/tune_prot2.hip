@@ -22,7 +22,7 @@
 #include <string>
 #include <vector>
 
-#include "plf_prot.hpp"
+#include "plf_prot_tune.hpp"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 

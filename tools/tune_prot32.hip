@@ -16,7 +16,7 @@
 #include <string>
 #include <vector>
 
-#include "plf_prot.hpp"
+#include "plf_prot_tune.hpp"
 #include "prot_pair32.hpp"
 
 using namespace plfx::dev;

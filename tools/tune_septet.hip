@@ -15,7 +15,7 @@
 #include <string>
 #include <vector>
 
-#include "plf_dna.hpp"
+#include "plf_dna_tune.hpp"
 
 using namespace plfx::dev;
 
