@@ -16,6 +16,7 @@
 #include <string>
 #include <functional>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/plfx.h"
@@ -28,14 +29,21 @@ constexpr int kHostChunksMax = 16;
 // block_ticket_sum, plf_lnl.hpp): zero at rest, restored to zero by the last
 // arriving block of every launch.  One per stream, so sum-producing launches
 // on different streams of one context may overlap (plfx.h, "Streams and the
-// scaler-sum workspace").
+// scaler-sum workspace").  hipStreamPerThread is one handle value that names a
+// different stream in every host thread, so its workspaces are keyed by
+// (handle, thread).  Entries come from a pool allocated and zeroed with the
+// context (no allocation on a call path for the first kWsPool streams, so a
+// stream's first use may be inside a graph capture); plfx_ctx_release_stream
+// returns an entry to the pool.
 struct StreamWs {
   hipStream_t stream = nullptr;
+  std::thread::id tid;               // owning thread for hipStreamPerThread, else none
+  bool in_use = false;
   unsigned long long *ws = nullptr;  // kWsRegions x kWsWords u64
   double *lnl_partials = nullptr;    // kLnlMaxGrid doubles
   unsigned long long *lnl_ticket = nullptr;
-  void *block = nullptr;             // the one allocation holding all three
 };
+constexpr int kWsPool = PLFX_WS_POOL;
 
 struct plfx_ctx {
   int device = 0;
@@ -44,6 +52,7 @@ struct plfx_ctx {
   int fuse = 3;  // traverse: 3 six-level subtrees before 2's, 2 three-level subtrees +
                  // level pairs, 1 level pairs, 0 none (PLFX_FUSE)
   std::deque<StreamWs> wss;         // per-stream workspaces (stable addresses)
+  std::vector<void *> ws_blocks;    // their allocations (the pool's, then one per extra entry)
   int sched[PLFX_SCHED_COUNTS] = {};  // schedule of the last traverse
   // grow-only staging for the synchronous host entry points
   void *d_buf = nullptr;
@@ -114,42 +123,72 @@ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // to run on the context's own stream.
 hipStream_t pick(plfx_ctx *, void *stream) { return reinterpret_cast<hipStream_t>(stream); }
 
-// The workspace of stream s, created (zeroed in order on s) on its first use.
-// Not inside a stream capture: the allocation would not be part of the graph.
-StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
+constexpr size_t kWsEntryBytes = kWsBytes + kLnlPartialBytes + kLnlTicketBytes;
+
+// the key thread of a stream handle: the calling thread for hipStreamPerThread
+std::thread::id ws_thread(hipStream_t s) {
+  return s == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
+}
+
+StreamWs *ws_find(plfx_ctx *ctx, hipStream_t s) {
+  const std::thread::id tid = ws_thread(s);
   for (StreamWs &w : ctx->wss)
-    if (w.stream == s) return &w;
+    if (w.in_use && w.stream == s && w.tid == tid) return &w;
+  return nullptr;
+}
+
+void ws_carve(StreamWs &w, void *base) {
+  char *b = static_cast<char *>(base);
+  w.ws = reinterpret_cast<unsigned long long *>(b);
+  w.lnl_partials = reinterpret_cast<double *>(b + kWsBytes);
+  w.lnl_ticket = reinterpret_cast<unsigned long long *>(b + kWsBytes + kLnlPartialBytes);
+}
+
+// The workspace of stream s: its own, else a free pool entry (zero at rest),
+// else a new allocation (zeroed in order on s) -- not inside a stream capture,
+// where the allocation would not be part of the graph.
+StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
+  if (StreamWs *w = ws_find(ctx, s)) return w;
   *rc = PLFX_OK;
+  for (StreamWs &w : ctx->wss)
+    if (!w.in_use) {
+      w.in_use = true;
+      w.stream = s;
+      w.tid = ws_thread(s);
+      return &w;
+    }
   if ((int)ctx->wss.size() >= PLFX_MAX_STREAMS) {
-    *rc = fail(ctx, PLFX_ERR_INVALID, "more than %d streams used with one context", PLFX_MAX_STREAMS);
+    *rc = fail(ctx, PLFX_ERR_INVALID,
+               "more than %d streams in use with one context (release idle ones with "
+               "plfx_ctx_release_stream)", PLFX_MAX_STREAMS);
     return nullptr;
   }
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (s && hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
     *rc = fail(ctx, PLFX_ERR_INVALID,
-               "first call on a stream inside a graph capture: issue one call on the stream "
-               "before capturing (its reduction workspace is allocated then)");
+               "more than %d streams in use and this one is being captured: issue one call on "
+               "the stream before capturing (its reduction workspace is allocated then)", kWsPool);
     return nullptr;
   }
-  StreamWs w;
-  w.stream = s;
-  const size_t bytes = kWsBytes + kLnlPartialBytes + kLnlTicketBytes;
-  hipError_t e = hipMalloc(&w.block, bytes);
+  void *block = nullptr;
+  hipError_t e = hipMalloc(&block, kWsEntryBytes);
   if (e != hipSuccess) {
-    *rc = fail(ctx, PLFX_ERR_NOMEM, "workspace hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    *rc = fail(ctx, PLFX_ERR_NOMEM, "workspace hipMalloc(%zu): %s", kWsEntryBytes, hipGetErrorString(e));
     return nullptr;
   }
-  char *b = static_cast<char *>(w.block);
-  w.ws = reinterpret_cast<unsigned long long *>(b);
-  w.lnl_partials = reinterpret_cast<double *>(b + kWsBytes);
-  w.lnl_ticket = reinterpret_cast<unsigned long long *>(b + kWsBytes + kLnlPartialBytes);
-  e = hipMemsetAsync(w.block, 0, bytes, s);
+  e = hipMemsetAsync(block, 0, kWsEntryBytes, s);
   if (e == hipSuccess && !s) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
-    (void)hipFree(w.block);
+    (void)hipFree(block);
     *rc = hip_fail(ctx, e, "workspace memset");
     return nullptr;
   }
+  ctx->ws_blocks.push_back(block);
+  StreamWs w;
+  w.stream = s;
+  w.tid = ws_thread(s);
+  w.in_use = true;
+  ws_carve(w, block);
   ctx->wss.push_back(w);
   return &ctx->wss.back();
 }
@@ -326,11 +365,21 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
     }
     return PLFX_OK;
   }
-  for (int i = 0; i < count; i += plfx::kMaxBatch) {
-    const int c = std::min(plfx::kMaxBatch, count - i);
-    hipError_t e = plfx::launch_plf_dna_batch(dtype, reinterpret_cast<const plfx::NodeDescH *>(nodes + i),
-                                              c, EV, wgt, n, w->ws, ctx->max_blocks, s, tips,
-                                              tipvec);
+  // More than kMaxBatch nodes: launch j takes nodes j, j + L, j + 2L, ... (L
+  // launches), so every launch mixes nodes from across the caller's list.
+  // Consecutive nodes are usually consecutive allocations, and a launch made of
+  // 32 neighbouring allocations of 128 MiB ran up to 15 % slower than a mixed
+  // one while each of its nodes alone ran at the same speed (nodes512 at N = 1:
+  // launches of 2.09-2.48 ms consecutive, 2.10-2.12 ms interleaved;
+  // tools/probes/nodes_groups.py, nodes_sched.py).
+  const int L = (count + plfx::kMaxBatch - 1) / plfx::kMaxBatch;
+  const plfx::NodeDescH *all = reinterpret_cast<const plfx::NodeDescH *>(nodes);
+  for (int j = 0; j < L; j++) {
+    plfx::NodeDescH sel[plfx::kMaxBatch];
+    int c = 0;
+    for (int i = j; i < count; i += L) sel[c++] = all[i];
+    hipError_t e = plfx::launch_plf_dna_batch(dtype, L == 1 ? all : sel, c, EV, wgt, n, w->ws,
+                                              ctx->max_blocks, s, tips, tipvec);
     if (e != hipSuccess) return hip_fail(ctx, e, "plf batch launch");
     if (launches) ++*launches;
   }
@@ -367,12 +416,25 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
     if (v > 0) ctx->max_blocks = v;
   }
   if (const char *env = std::getenv("PLFX_FUSE")) ctx->fuse = std::atoi(env);
-  int rc = PLFX_OK;
-  if (!ws_for(ctx, ctx->stream, &rc) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
-    for (StreamWs &w : ctx->wss) (void)hipFree(w.block);
+  // the workspace pool: kWsPool entries in one allocation, zeroed before return
+  void *pool = nullptr;
+  if (hipMalloc(&pool, kWsPool * kWsEntryBytes) != hipSuccess) {
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
-    return rc != PLFX_OK ? rc : PLFX_ERR_HIP;
+    return PLFX_ERR_NOMEM;
+  }
+  if (hipMemsetAsync(pool, 0, kWsPool * kWsEntryBytes, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    (void)hipFree(pool);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return PLFX_ERR_HIP;
+  }
+  ctx->ws_blocks.push_back(pool);
+  for (int i = 0; i < kWsPool; i++) {
+    StreamWs w;
+    ws_carve(w, static_cast<char *>(pool) + i * kWsEntryBytes);
+    ctx->wss.push_back(w);
   }
   *out = ctx;
   return PLFX_OK;
@@ -390,9 +452,15 @@ int plfx_ctx_destroy(plfx_ctx *ctx) {
     }
     for (hipEvent_t e : ctx->chunk_done)
       if (e) (void)hipEventDestroy(e);
-    // other streams' workspaces: their last launches must be done before the free
-    (void)hipDeviceSynchronize();
-    for (StreamWs &w : ctx->wss) (void)hipFree(w.block);
+    // other streams' workspaces: their last launches must be done before the
+    // free.  A stream still holding one may already be destroyed (HIP does not
+    // validate handles), so it is never touched here: streams released with
+    // plfx_ctx_release_stream cost nothing, any other holder makes destroy wait
+    // for the device (plfx.h, "Streams and the scaler-sum workspace").
+    bool held = false;
+    for (StreamWs &w : ctx->wss) held |= w.in_use && w.stream != ctx->stream;
+    if (held) (void)hipDeviceSynchronize();
+    for (void *b : ctx->ws_blocks) (void)hipFree(b);
     (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -416,6 +484,20 @@ int plfx_ctx_device(const plfx_ctx *ctx) { return ctx ? ctx->device : -1; }
 int plfx_ctx_synchronize(plfx_ctx *ctx) {
   PLFX_BIND(ctx);
   PLFX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return PLFX_OK;
+}
+
+int plfx_ctx_release_stream(plfx_ctx *ctx, void *stream) {
+  PLFX_BIND(ctx);
+  hipStream_t s = pick(ctx, stream);
+  StreamWs *w = ws_find(ctx, s);
+  if (!w) return PLFX_OK;  // no workspace held: nothing to release
+  // the stream's last sum-producing launch must be done before another stream
+  // may take the entry (it is zero again once that launch has finished)
+  PLFX_HIP(ctx, hipStreamSynchronize(s));
+  w->in_use = false;
+  w->stream = nullptr;
+  w->tid = std::thread::id();
   return PLFX_OK;
 }
 

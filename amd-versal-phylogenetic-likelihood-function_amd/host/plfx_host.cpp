@@ -5,6 +5,7 @@
 //                    [--target hw|sw_emu] [--dtype f32|f64] [--layout comb|sep]
 //                    [--aie window|stream] [--window BYTES] [--seed S]
 //                    [--dump PREFIX] [--no-check] [--quiet]
+//                    [--no-intermediate] [--csv FILE]
 //
 // Mirrors host_mem.cpp:
 //   * argv shape <sites> <calls> <instances> (host_mem.cpp:13-38); the xclbin
@@ -17,9 +18,20 @@
 //   * host_mem input protocol (host_mem.cpp:179-209) with a fixed seed (Q8);
 //   * per-instance packing [EV|P_L|CLV_L], [EV|P_R|CLV_R] / [P_R|CLV_R]
 //     (host_mem.cpp:221-243);
-//   * per call, per instance on its own HIP stream: H2D left || H2D right ->
-//     fused kernel -> D2H CLV || D2H scaler, with the begin/t1/t2/end regions
-//     of timing.h:25-52 taken by HIP events (host_mem.cpp:283-325);
+//   * per call, per instance on two HIP streams joined by events, as the
+//     reference's main/right queues (host_mem.cpp:283-325): H2D left (main)
+//     || H2D right (right) -> fused kernel (main) -> D2H CLV (main) || D2H
+//     scaler (right), with the begin/t1/t2/end regions of timing.h:25-52
+//     taken by HIP events on the main stream;
+//   * --no-intermediate: the reference's NO_INTERMEDIATE_RESULTS build
+//     (host_mem.cpp:327-382,390-392,454-468): per call the instance buffers
+//     are packed inside the timed region ("Prepare input"), all instances run
+//     on main/right/output streams (H2D left || H2D right -> kernel -> D2H
+//     scaler || D2H CLV), and the host scaler reduction is its own region
+//     ("scaling wgt mult"), all on the host clock as the reference's t.elapsed();
+//   * --csv FILE: the per-call timing CSV of write_to_csv (timing.h:153-194):
+//     hm<k>,msasm<k>,mh<k> columns per instance, or preparation,plf,scaling
+//     with --no-intermediate;
 //   * host scaler reduction sum scaler[j]*wgt[j] (host_mem.cpp:384-388);
 //   * the correctness check of host_mem.cpp:403-442: this program's own CPU
 //     plf() (below, plf.cpp:19-65 restated) run plf_calls times and timed,
@@ -70,14 +82,16 @@ struct Opts {
   uint32_t window = 8192;
   uint32_t seed = 20250117u;
   std::string dump;
+  std::string csv;
   bool quiet = false;
+  bool no_intermediate = false;
 };
 
 Opts parse(int argc, char **argv) {
   if (argc < 4)
     die("usage: plfx_host <alignment sites> <plf calls> <parallel instances> [--target hw|sw_emu] "
         "[--dtype f32|f64] [--layout comb|sep] [--aie window|stream] [--window BYTES] [--seed S] "
-        "[--dump PREFIX] [--no-check] [--quiet]");
+        "[--dump PREFIX] [--no-check] [--quiet] [--no-intermediate] [--csv FILE]");
   Opts o;
   try {
     o.sites = std::stoull(argv[1]);
@@ -122,6 +136,10 @@ Opts parse(int argc, char **argv) {
       o.check = false;
     } else if (a == "--quiet") {
       o.quiet = true;
+    } else if (a == "--no-intermediate") {
+      o.no_intermediate = true;
+    } else if (a == "--csv") {
+      o.csv = next();
     } else {
       die("unknown option " + a);
     }
@@ -130,6 +148,7 @@ Opts parse(int argc, char **argv) {
   if (o.aie == plfx::WINDOW && (o.window < 32 || o.window % 32)) die("window must be a multiple of 32 bytes");
   if (o.sw_emu && o.aie == plfx::STREAM && o.layout != plfx::COMBINED)
     die("stream movers exist in the COMBINED layout only");
+  if (o.sw_emu && o.no_intermediate) die("--no-intermediate is a GPU (hw) run mode");
   return o;
 }
 
@@ -219,6 +238,7 @@ int run(const Opts &o) {
   std::vector<std::vector<uint8_t>> scaler(o.calls, std::vector<uint8_t>(o.sites));
   std::vector<long long> inc(o.calls, 0);
   std::vector<Regions> reg((size_t)o.calls * P);  // [call][instance]
+  std::vector<Regions> callreg(o.calls);           // --no-intermediate: [call], host clock
   const int dt = o.f64 ? PLFX_F64 : PLFX_F32;
   double wall_ms = 0;
 
@@ -253,11 +273,14 @@ int run(const Opts &o) {
     plfx_ctx *ctx = nullptr;
     int rc = plfx_ctx_create(0, &ctx);
     if (rc != PLFX_OK) die("plfx_ctx_create failed: " + std::to_string(rc));
-    // per-instance pinned host buffers, device buffers, streams and events
+    // per-instance pinned host buffers, device buffers, the reference's three
+    // queues (main / right / output, host_mem.cpp:123-127) as HIP streams, and
+    // the events that join them
     std::vector<T *> hL(P), hR(P), dL(P), dR(P), dO(P);
     std::vector<uint8_t *> dS(P);
-    std::vector<hipStream_t> st(P);
+    std::vector<hipStream_t> st(P), sr(P), so(P);
     std::vector<hipEvent_t> eb(P * o.calls), e1(P * o.calls), e2(P * o.calls), ee(P * o.calls);
+    std::vector<hipEvent_t> j_up(P), j_run(P), j_dn(P);  // joins: right upload, kernel, side download
     hipEvent_t e0;
     for (uint32_t k = 0; k < P; k++) {
       HIPCHK(hipHostMalloc((void **)&hL[k], tb.instance_elements_left() * es));
@@ -266,14 +289,24 @@ int run(const Opts &o) {
       HIPCHK(hipMalloc((void **)&dR[k], tb.instance_elements_right() * es));
       HIPCHK(hipMalloc((void **)&dO[k], std::max<uint64_t>(tb.instance_elements_out(), 16) * es));
       HIPCHK(hipMalloc((void **)&dS[k], std::max<uint64_t>(n0, 1)));
-      HIPCHK(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
-      tb.pack<T>(k, ev, bl, br, xl.data(), xr.data(), hL[k], hR[k]);
+      for (auto *q : {&st, &sr, &so}) HIPCHK(hipStreamCreateWithFlags(&(*q)[k], hipStreamNonBlocking));
+      for (auto *q : {&j_up, &j_run, &j_dn}) HIPCHK(hipEventCreateWithFlags(&(*q)[k], hipEventDisableTiming));
+      if (!o.no_intermediate) tb.pack<T>(k, ev, bl, br, xl.data(), xr.data(), hL[k], hR[k]);
     }
     for (auto *v : {&eb, &e1, &e2, &ee})
       for (auto &e : *v) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipDeviceSynchronize());
     auto t0 = std::chrono::steady_clock::now();
+    auto ms_since = [&](std::chrono::steady_clock::time_point a) {
+      return std::chrono::duration<double, std::milli>(a - t0).count();
+    };
+    auto run_instance = [&](uint32_t k) {
+      const uint64_t nk = tb.alignments_per_instance(k);
+      rc = plfx_instance_run(ctx, dL[k], dR[k], dO[k], dS[k], (uint32_t)nk,
+                             o.aie == plfx::WINDOW ? o.window : 0, o.layout, dt, st[k]);
+      if (rc != PLFX_OK) die(std::string("plfx_instance_run: ") + plfx_last_error(ctx));
+    };
     // host-side ranges for rocprofv3 --marker-trace: the whole run (the
     // reference's XRT user range "roundtrip_exec_time", host_mem.cpp:273,395)
     // and each plf call's enqueue + wait; the H2D / kernel / D2H regions
@@ -282,42 +315,81 @@ int run(const Opts &o) {
     HIPCHK(hipEventRecord(e0, st[0]));
     for (uint32_t i = 0; i < o.calls; i++) {
       roctxRangePush("plf call (all instances)");
-      for (uint32_t k = 0; k < P; k++) {
-        const uint64_t nk = tb.alignments_per_instance(k);
-        const uint64_t off = tb.instance_site_offset(k);
-        const size_t ev_i = (size_t)i * P + k;
-        HIPCHK(hipEventRecord(eb[ev_i], st[k]));
-        HIPCHK(hipMemcpyAsync(dL[k], hL[k], tb.instance_active_elements_left(k) * es, hipMemcpyHostToDevice, st[k]));
-        HIPCHK(hipMemcpyAsync(dR[k], hR[k], tb.instance_active_elements_right(k) * es, hipMemcpyHostToDevice, st[k]));
-        HIPCHK(hipEventRecord(e1[ev_i], st[k]));
-        rc = plfx_instance_run(ctx, dL[k], dR[k], dO[k], dS[k], (uint32_t)nk,
-                               o.aie == plfx::WINDOW ? o.window : 0, o.layout, dt, st[k]);
-        if (rc != PLFX_OK) die(std::string("plfx_instance_run: ") + plfx_last_error(ctx));
-        HIPCHK(hipEventRecord(e2[ev_i], st[k]));
-        HIPCHK(hipMemcpyAsync(result[i].data() + off * 16, dO[k], nk * 16 * es, hipMemcpyDeviceToHost, st[k]));
-        HIPCHK(hipMemcpyAsync(scaler[i].data() + off, dS[k], nk, hipMemcpyDeviceToHost, st[k]));
-        HIPCHK(hipEventRecord(ee[ev_i], st[k]));
+      if (!o.no_intermediate) {
+        for (uint32_t k = 0; k < P; k++) {
+          const uint64_t nk = tb.alignments_per_instance(k);
+          const uint64_t off = tb.instance_site_offset(k);
+          const size_t ev_i = (size_t)i * P + k;
+          // time: begin; the right stream starts after it (so after the
+          // previous call's kernel and downloads of this instance)
+          HIPCHK(hipEventRecord(eb[ev_i], st[k]));
+          HIPCHK(hipStreamWaitEvent(sr[k], eb[ev_i], 0));
+          HIPCHK(hipMemcpyAsync(dL[k], hL[k], tb.instance_active_elements_left(k) * es, hipMemcpyHostToDevice, st[k]));
+          HIPCHK(hipMemcpyAsync(dR[k], hR[k], tb.instance_active_elements_right(k) * es, hipMemcpyHostToDevice, sr[k]));
+          HIPCHK(hipEventRecord(j_up[k], sr[k]));
+          HIPCHK(hipStreamWaitEvent(st[k], j_up[k], 0));
+          HIPCHK(hipEventRecord(e1[ev_i], st[k]));  // time: t1
+          run_instance(k);
+          HIPCHK(hipEventRecord(e2[ev_i], st[k]));  // time: t2
+          HIPCHK(hipStreamWaitEvent(sr[k], e2[ev_i], 0));
+          HIPCHK(hipMemcpyAsync(result[i].data() + off * 16, dO[k], nk * 16 * es, hipMemcpyDeviceToHost, st[k]));
+          HIPCHK(hipMemcpyAsync(scaler[i].data() + off, dS[k], nk, hipMemcpyDeviceToHost, sr[k]));
+          HIPCHK(hipEventRecord(j_dn[k], sr[k]));
+          HIPCHK(hipStreamWaitEvent(st[k], j_dn[k], 0));
+          HIPCHK(hipEventRecord(ee[ev_i], st[k]));  // time: end
+        }
+        for (uint32_t k = 0; k < P; k++) HIPCHK(hipStreamSynchronize(st[k]));
+        long long s = 0;  // host_mem.cpp:385-388
+        for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
+        inc[i] = s;
+      } else {
+        // NO_INTERMEDIATE_RESULTS (host_mem.cpp:327-392): prepare, run, reduce
+        Regions &r = callreg[i];
+        r.begin = ms_since(std::chrono::steady_clock::now());
+        for (uint32_t k = 0; k < P; k++) tb.pack<T>(k, ev, bl, br, xl.data(), xr.data(), hL[k], hR[k]);
+        r.t1 = ms_since(std::chrono::steady_clock::now());
+        for (uint32_t k = 0; k < P; k++) {
+          const uint64_t nk = tb.alignments_per_instance(k);
+          const uint64_t off = tb.instance_site_offset(k);
+          HIPCHK(hipMemcpyAsync(dL[k], hL[k], tb.instance_active_elements_left(k) * es, hipMemcpyHostToDevice, st[k]));
+          HIPCHK(hipMemcpyAsync(dR[k], hR[k], tb.instance_active_elements_right(k) * es, hipMemcpyHostToDevice, sr[k]));
+          HIPCHK(hipEventRecord(j_up[k], sr[k]));
+          HIPCHK(hipStreamWaitEvent(st[k], j_up[k], 0));
+          run_instance(k);
+          HIPCHK(hipEventRecord(j_run[k], st[k]));
+          HIPCHK(hipStreamWaitEvent(so[k], j_run[k], 0));
+          HIPCHK(hipMemcpyAsync(scaler[i].data() + off, dS[k], nk, hipMemcpyDeviceToHost, st[k]));
+          HIPCHK(hipMemcpyAsync(result[i].data() + off * 16, dO[k], nk * 16 * es, hipMemcpyDeviceToHost, so[k]));
+          HIPCHK(hipEventRecord(j_dn[k], so[k]));
+          HIPCHK(hipStreamWaitEvent(st[k], j_dn[k], 0));
+        }
+        for (uint32_t k = 0; k < P; k++) HIPCHK(hipStreamSynchronize(st[k]));
+        r.t2 = ms_since(std::chrono::steady_clock::now());
+        long long s = 0;  // host_mem.cpp:385-388
+        for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
+        inc[i] = s;
+        r.end = ms_since(std::chrono::steady_clock::now());
       }
-      for (uint32_t k = 0; k < P; k++) HIPCHK(hipStreamSynchronize(st[k]));
-      long long s = 0;  // host_mem.cpp:385-388
-      for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
-      inc[i] = s;
       roctxRangePop();
     }
     roctxRangePop();
-    wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    for (size_t q = 0; q < reg.size(); q++) {
-      float a, b, c, d;
-      HIPCHK(hipEventElapsedTime(&a, e0, eb[q]));
-      HIPCHK(hipEventElapsedTime(&b, e0, e1[q]));
-      HIPCHK(hipEventElapsedTime(&c, e0, e2[q]));
-      HIPCHK(hipEventElapsedTime(&d, e0, ee[q]));
-      reg[q] = Regions{a, b, c, d};
+    wall_ms = ms_since(std::chrono::steady_clock::now());
+    if (!o.no_intermediate) {
+      for (size_t q = 0; q < reg.size(); q++) {
+        float a, b, c, d;
+        HIPCHK(hipEventElapsedTime(&a, e0, eb[q]));
+        HIPCHK(hipEventElapsedTime(&b, e0, e1[q]));
+        HIPCHK(hipEventElapsedTime(&c, e0, e2[q]));
+        HIPCHK(hipEventElapsedTime(&d, e0, ee[q]));
+        reg[q] = Regions{a, b, c, d};
+      }
     }
     for (uint32_t k = 0; k < P; k++) {
+      (void)plfx_ctx_release_stream(ctx, st[k]);  // before the stream is destroyed (plfx.h)
       (void)hipHostFree(hL[k]); (void)hipHostFree(hR[k]);
       (void)hipFree(dL[k]); (void)hipFree(dR[k]); (void)hipFree(dO[k]); (void)hipFree(dS[k]);
-      (void)hipStreamDestroy(st[k]);
+      for (auto *q : {&st, &sr, &so}) (void)hipStreamDestroy((*q)[k]);
+      for (auto *q : {&j_up, &j_run, &j_dn}) (void)hipEventDestroy((*q)[k]);
     }
     for (auto *v : {&eb, &e1, &e2, &ee})
       for (auto &e : *v) (void)hipEventDestroy(e);
@@ -365,8 +437,14 @@ int run(const Opts &o) {
                 ms > 0 ? nbytes / 1e6 / (ms / 1e3) : 0.0, ms > 0 ? nsites / (ms / 1e3) * 1e-6 : 0.0);
   };
   // all instances of a call together: first begin .. last end of each region
+  // (--no-intermediate: the call's host-clock regions)
   double agg_hm = 0, agg_msm = 0, agg_mh = 0;
-  for (uint32_t i = 0; i < o.calls; i++) {
+  for (uint32_t i = 0; i < o.calls && o.no_intermediate; i++) {
+    agg_hm += callreg[i].hm();
+    agg_msm += callreg[i].msm();
+    agg_mh += callreg[i].mh();
+  }
+  for (uint32_t i = 0; i < o.calls && !o.no_intermediate; i++) {
     Regions a{1e300, -1e300, -1e300, -1e300};
     double b0 = 1e300;
     for (uint32_t k = 0; k < P; k++) {
@@ -385,6 +463,14 @@ int run(const Opts &o) {
     std::printf("=====================================================================================================\n");
     std::printf("| Timing region (%-6s)                 | time (ms)  | bandwidth (MB/s) |         bandwidth (MA/s) |\n", target);
     std::printf("=====================================================================================================\n");
+  }
+  if (!o.quiet && o.no_intermediate) {
+    // the NO_INTERMEDIATE_RESULTS table (host_mem.cpp:454-468)
+    row("Prepare input for GPU:", agg_hm, bytes_inst * P * o.calls, total_sites);
+    row("PLF on GPU:", agg_msm, bytes_inst * P * o.calls, total_sites);
+    row("scaling wgt mult:", agg_mh, bytes_inst * P * o.calls, total_sites);
+  }
+  if (!o.quiet && !o.no_intermediate) {
     for (uint32_t k = 0; k < P; k++) {
       const double nk_sites = (double)tb.alignments_per_instance(k) * o.calls;
       double hm = 0, msm = 0, mh = 0, mx = 0, mn = 1e300;
@@ -407,6 +493,8 @@ int run(const Opts &o) {
     row("[all instances] Host to GPU memory:", agg_hm, bytes_inst * P * o.calls, total_sites);
     row("[all instances] GPU PLF kernel:", agg_msm, bytes_inst * P * o.calls, total_sites);
     row("[all instances] GPU memory to host:", agg_mh, bytes_inst * P * o.calls, total_sites);
+  }
+  if (!o.quiet) {
     row("Total execution time:", wall_ms, bytes_inst * P * o.calls, total_sites);
     std::printf("=====================================================================================================\n");
     if (o.check) {
@@ -419,6 +507,29 @@ int run(const Opts &o) {
     for (uint32_t i = 0; i < o.calls; i++) std::printf("scalerIncrement[call %u] = %lld\n", i, inc[i]);
   }
   std::printf("Test result: %s\n", verdict.c_str());
+  if (!o.csv.empty()) {  // write_to_csv (timing.h:153-194), ms per call
+    FILE *f = std::fopen(o.csv.c_str(), "w");
+    if (!f) die("cannot write " + o.csv);
+    if (o.no_intermediate) {
+      std::fprintf(f, "preparation,plf,scaling\n");
+      for (uint32_t i = 0; i < o.calls; i++)
+        std::fprintf(f, "%.6f,%.6f,%.6f\n", callreg[i].hm(), callreg[i].msm(), callreg[i].mh());
+    } else {
+      const char *col[3] = {"hm", "msasm", "mh"};
+      for (int c = 0; c < 3; c++)
+        for (uint32_t k = 0; k < P; k++) std::fprintf(f, "%s%s%u", c || k ? "," : "", col[c], k);
+      std::fprintf(f, "\n");
+      for (uint32_t i = 0; i < o.calls; i++) {
+        for (int c = 0; c < 3; c++)
+          for (uint32_t k = 0; k < P; k++) {
+            const Regions &r = reg[(size_t)i * P + k];
+            std::fprintf(f, "%s%.6f", c || k ? "," : "", c == 0 ? r.hm() : (c == 1 ? r.msm() : r.mh()));
+          }
+        std::fprintf(f, "\n");
+      }
+    }
+    std::fclose(f);
+  }
   if (!o.dump.empty()) {
     for (uint32_t i = 0; i < o.calls; i++) {
       std::string base = o.dump + "_call" + std::to_string(i);

@@ -38,7 +38,7 @@ F32, F64 = 0, 1
 # symbols declared by include/plfx.h (checked by tests/test_abi.py)
 EXPORTS = (
     "plfx_ctx_create", "plfx_ctx_destroy", "plfx_last_error", "plfx_get_version",
-    "plfx_ctx_stream", "plfx_ctx_device", "plfx_ctx_synchronize",
+    "plfx_ctx_stream", "plfx_ctx_device", "plfx_ctx_synchronize", "plfx_ctx_release_stream",
     "plfx_plf_f32", "plfx_plf_f64", "plfx_plf_dev_f32", "plfx_plf_dev_f64",
     "plfx_instance_run", "plfx_instance_run_host", "plfx_scaler_sum",
     "plfx_tb_alignments_per_instance", "plfx_tb_alignments_padding",
@@ -54,6 +54,8 @@ EXPORTS = (
     "plfx_shard", "plfx_gen_hostmem", "plfx_swemu_instance_run", "plfx_traverse_schedule",
 )
 MAX_STREAMS = 64   # PLFX_MAX_STREAMS
+WS_POOL = 8        # PLFX_WS_POOL
+STREAM_PER_THREAD = 2  # hipStreamPerThread
 SCHED_KEYS = ("deep6", "deep5", "deep4", "septets", "triples", "unfused", "launches")
 PMAT_STATE, PMAT_EIGEN = 0, 1
 EXACT, FMA = 0, 1
@@ -108,6 +110,7 @@ def load():
     L.plfx_ctx_stream.restype = vp
     L.plfx_ctx_device.argtypes = [vp]
     L.plfx_ctx_synchronize.argtypes = [vp]
+    L.plfx_ctx_release_stream.argtypes = [vp, vp]
     for s in ("f32", "f64"):
         getattr(L, f"plfx_plf_{s}").argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, C.POINTER(i32)]
         getattr(L, f"plfx_plf_dev_{s}").argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
@@ -191,6 +194,11 @@ class Context:
 
     def synchronize(self):
         self._check(self._L.plfx_ctx_synchronize(self.h))
+
+    def release_stream(self, stream):
+        """Wait for `stream` and return its scaler-sum workspace to the pool
+        (plfx_ctx_release_stream)."""
+        self._check(self._L.plfx_ctx_release_stream(self.h, _stream_handle(stream, self.device)))
 
     def _check(self, rc):
         if rc != OK:

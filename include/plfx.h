@@ -52,13 +52,22 @@
  * Streams and the scaler-sum workspace.  Sum-producing launches (scaler_sum
  * outputs, plfx_scaler_sum, plfx_root_lnl) reduce across thread blocks through
  * a small self-resetting device workspace.  The context keeps ONE workspace
- * PER STREAM (up to PLFX_MAX_STREAMS distinct streams per context, created on
- * a stream's first use), so launches on different streams may run
- * concurrently; launches on one stream are ordered by the stream.  A stream's
- * first sum-producing use must not happen inside hipStreamBeginCapture (the
- * workspace is allocated then): issue one call on it before capturing.  A
- * captured graph keeps the workspace of the stream it was captured on, so its
- * replays must not overlap other work on that stream's workspace.
+ * PER STREAM in use (up to PLFX_MAX_STREAMS at a time), so launches on
+ * different streams may run concurrently; launches on one stream are ordered
+ * by the stream.  hipStreamPerThread names a different stream in every host
+ * thread and gets a workspace per thread.  The first PLFX_WS_POOL streams take
+ * workspaces allocated with the context, so their first use may be inside a
+ * graph capture; a further stream's first sum-producing use allocates (not
+ * inside hipStreamBeginCapture: issue one call on it before capturing).
+ * plfx_ctx_release_stream() waits for a stream and returns its workspace to
+ * the pool -- call it before destroying a stream used with the context, or
+ * when rotating through many streams.  A captured graph keeps the workspace
+ * of the stream it was captured on, so its replays must not overlap other
+ * work on that stream's workspace, and must not outlive the context.
+ * plfx_ctx_destroy() synchronises the context's stream; if any other stream
+ * still holds a workspace it waits for the whole device (hipDeviceSynchronize,
+ * which must not overlap a global-mode capture in another thread), so release
+ * streams first to keep destroy local.
  * The reduction encodes arrival counts next to the sums and needs
  * sum_j |wgt[j]| < 2^40 per launch (the reference's own scalerIncrement is a
  * 32-bit int); the host entry points check this, the device entry points
@@ -78,7 +87,8 @@ extern "C" {
 #endif
 
 #define PLFX_VERSION 10100 /* 1.1.0 */
-#define PLFX_MAX_STREAMS 64 /* distinct streams with a workspace, per context */
+#define PLFX_MAX_STREAMS 64 /* streams holding a workspace at a time, per context */
+#define PLFX_WS_POOL 8      /* workspaces allocated with the context */
 
 typedef enum {
   PLFX_OK = 0,
@@ -110,6 +120,11 @@ void *plfx_ctx_stream(plfx_ctx *ctx);
 int plfx_ctx_device(const plfx_ctx *ctx);
 /* Synchronise the context's stream. */
 int plfx_ctx_synchronize(plfx_ctx *ctx);
+/* Wait for `stream` (hipStream_t; NULL = the null stream; hipStreamPerThread =
+ * the calling thread's) and return its scaler-sum workspace to the context's
+ * pool.  PLFX_OK also when the stream holds none.  (Extension: the reference's
+ * XRT queues are fixed per instance, host_mem.cpp:123-127.) */
+int plfx_ctx_release_stream(plfx_ctx *ctx, void *stream);
 
 /* ---- (1) drop-in for plf(): host arrays, synchronous -------------------- */
 /* Same argument order and meaning as plf() (app/src/plf.h:1-5); `int&` is

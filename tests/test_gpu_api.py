@@ -142,41 +142,170 @@ def test_host_entry_from_several_threads(ctx, oracle):
         assert incs[i] == inc
 
 
-def test_graph_capture_needs_a_warm_stream(ctx, oracle):
-    """A stream's first sum-producing call may not be inside a capture (its
-    workspace is allocated then): rejected with PlfxError.  After one call the
-    stream captures, and replays produce exact sums."""
+def _hip():
+    import ctypes
+
+    import torch  # noqa: F401 -- the HIP runtime torch already loaded
+
+    return ctypes.CDLL("libamdhip64.so")
+
+
+def _new_streams(k):
+    import ctypes
+
+    hip = _hip()
+    out = []
+    for _ in range(k):
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithFlags(ctypes.byref(h), 1) == 0  # hipStreamNonBlocking
+        out.append(h.value)
+    return out
+
+
+def _destroy_streams(hs):
+    import ctypes
+
+    hip = _hip()
+    for h in hs:
+        assert hip.hipStreamDestroy(ctypes.c_void_p(h)) == 0
+
+
+def test_graph_capture_first_use_from_the_pool(oracle):
+    """The first PLFX_WS_POOL streams take workspaces allocated with the
+    context, so a stream's FIRST sum-producing call may be inside a capture;
+    once the pool is used up, a cold stream's first call inside a capture is
+    rejected with PlfxError (its workspace would be allocated then), and a
+    stream warmed outside captures fine.  Replays give exact sums."""
     import plfx
     import torch
 
     n = 70001
     d = oracle.gen_hostmem(n, np.float64, 43)
     t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
-    o3 = torch.empty_like(t["x1"])
-    s = torch.zeros(1, dtype=torch.int64, device="cuda")
-    cold = torch.cuda.Stream()
-    g = torch.cuda.CUDAGraph()
-    with pytest.raises(plfx.PlfxError):
-        with torch.cuda.graph(g, stream=cold):
-            ctx.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s,
-                        stream=cold)
-    warm = torch.cuda.Stream()
-    ctx.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s, stream=warm)
-    torch.cuda.synchronize()
-    g2 = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g2, stream=warm):
-        for _ in range(3):
-            ctx.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s,
-                        stream=warm)
-    s.zero_()
-    o3.zero_()
-    torch.cuda.synchronize()
-    for _ in range(4):
-        g2.replay()
-    torch.cuda.synchronize()
     e3, _, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
-    assert int(s.item()) == einc
-    assert np.array_equal(bits(o3.cpu().numpy()), bits(e3))
+    with plfx.Context(0) as c:
+        o3 = torch.empty_like(t["x1"])
+        s = torch.zeros(1, dtype=torch.int64, device="cuda")
+        cold = torch.cuda.Stream()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cold):  # cold stream, pool entry: fine
+            for _ in range(3):
+                c.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s,
+                          stream=cold)
+        s.zero_()
+        torch.cuda.synchronize()
+        for _ in range(4):
+            g.replay()
+        torch.cuda.synchronize()
+        assert int(s.item()) == einc
+        assert np.array_equal(bits(o3.cpu().numpy()), bits(e3))
+        # use up the pool (`cold` holds one entry)
+        hs = _new_streams(plfx.WS_POOL - 1)
+        sums = torch.zeros(len(hs), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        for i, h in enumerate(hs):
+            c.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None,
+                      sums[i:i + 1], stream=h)
+        torch.cuda.synchronize()
+        late = torch.cuda.Stream()
+        g2 = torch.cuda.CUDAGraph()
+        with pytest.raises(plfx.PlfxError):
+            with torch.cuda.graph(g2, stream=late):
+                c.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s,
+                          stream=late)
+        for h in hs:
+            c.release_stream(h)
+        _destroy_streams(hs)
+        assert sums.tolist() == [einc] * len(hs)
+
+
+def test_per_thread_default_stream_from_threads(oracle):
+    """hipStreamPerThread is ONE handle value naming a different stream in every
+    host thread: each thread gets its own workspace, so four
+    threads issuing sum-producing calls on it at once all get exact sums."""
+    import threading
+
+    import plfx
+    import torch
+
+    n = 1 << 18
+    d = oracle.gen_hostmem(n, np.float64, 47)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right")}
+    nt, reps = 4, 24
+    ws = [dev(np.full(n, i + 1, np.int32)) for i in range(nt)]
+    outs = [torch.empty_like(t["x1"]) for _ in range(nt)]
+    sums = torch.zeros(nt, reps, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    errs = []
+    go = threading.Barrier(nt)
+    with plfx.Context(0) as c:
+        def worker(i):
+            try:
+                go.wait()
+                for r in range(reps):
+                    c.plf_dev(t["x1"], t["x2"], outs[i], t["EV"], t["left"], t["right"], ws[i], None,
+                              sums[i, r:r + 1], stream=plfx.STREAM_PER_THREAD)
+                c.release_stream(plfx.STREAM_PER_THREAD)  # waits for this thread's stream
+            except Exception as e:  # reported on the main thread
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(nt)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=60)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    n_sc = n // 4
+    for i in range(nt):
+        assert sums[i].tolist() == [(i + 1) * n_sc] * reps
+    e3, _, _ = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], threads=16)
+    for o in outs:
+        assert np.array_equal(bits(o.cpu().numpy()), bits(e3))
+
+
+def test_release_stream_recycles_workspaces(oracle):
+    """Streams hold a workspace until plfx_ctx_release_stream: more than
+    PLFX_MAX_STREAMS streams used one after another work when each is released;
+    without releases the (MAX_STREAMS+1)-th is refused until one is released.
+    Destroying the context with streams still holding workspaces waits for
+    the device, so the sums are complete after close()."""
+    import plfx
+    import torch
+
+    n = 4099
+    d = oracle.gen_hostmem(n, np.float64, 48)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    _, _, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+    k = plfx.MAX_STREAMS + 6
+    hs = _new_streams(k)
+    sums = torch.zeros(k, dtype=torch.int64, device="cuda")
+    o3 = torch.empty_like(t["x1"])
+    torch.cuda.synchronize()
+
+    def call(c, i):
+        c.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None,
+                  sums[i:i + 1], stream=hs[i])
+
+    with plfx.Context(0) as c:  # rotate with releases: never more than one held
+        for i in range(k):
+            call(c, i)
+            c.release_stream(hs[i])
+        assert sums.tolist() == [einc] * k
+    sums.zero_()
+    torch.cuda.synchronize()
+    c = plfx.Context(0)
+    held = plfx.MAX_STREAMS
+    for i in range(held):
+        call(c, i)
+    with pytest.raises(plfx.PlfxError) as ei:
+        call(c, held)
+    assert ei.value.code == plfx.ERR_INVALID
+    c.release_stream(hs[0])
+    call(c, held)
+    c.close()  # streams still hold workspaces: destroy waits for the device
+    assert sums[1:held + 1].tolist() == [einc] * held
+    _destroy_streams(hs)
 
 
 def test_context_keeps_callers_device(ctx):

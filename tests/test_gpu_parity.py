@@ -318,17 +318,25 @@ def test_rejects_bad_arguments(ctx):
 
 
 def test_host_driver_end_to_end(oracle, tmp_path):
-    """plfx_host (the host_mem.cpp counterpart): H2D -> kernel -> D2H per
-    instance on streams; dumped CLVs/scalers equal the oracle on the same
-    host_mem-protocol inputs (std::mt19937, same seed)."""
+    """plfx_host (the host_mem.cpp counterpart): H2D left || H2D right ->
+    kernel -> D2H CLV || D2H scaler per instance on two streams joined by
+    events; dumped CLVs/scalers equal the oracle on the same host_mem-protocol
+    inputs (std::mt19937, same seed).  --no-intermediate is the reference's
+    NO_INTERMEDIATE_RESULTS mode (host_mem.cpp:327-392,454-468) and --csv its
+    write_to_csv (timing.h:153-194)."""
     exe = PKG / "build" / "plfx_host"
     assert exe.exists()
-    for dtype, args in ((np.float32, ["--dtype", "f32", "--layout", "comb", "--window", "1024"]),
-                        (np.float64, ["--dtype", "f64", "--layout", "sep", "--window", "8192"])):
+    cases = ((np.float32, ["--dtype", "f32", "--layout", "comb", "--window", "1024"], False),
+             (np.float64, ["--dtype", "f64", "--layout", "sep", "--window", "8192"], False),
+             (np.float64, ["--dtype", "f64", "--layout", "comb", "--window", "8192"], True),
+             (np.float32, ["--dtype", "f32", "--layout", "sep", "--window", "1024"], True))
+    for ci, (dtype, args, noint) in enumerate(cases):
         n, calls, P = 3001, 2, 3
-        pre = str(tmp_path / f"out_{np.dtype(dtype).name}")
-        r = subprocess.run([str(exe), str(n), str(calls), str(P), *args, "--dump", pre],
-                           capture_output=True, text=True, timeout=120)
+        pre = str(tmp_path / f"out{ci}_{np.dtype(dtype).name}")
+        csv = tmp_path / f"t{ci}.csv"
+        extra = ["--no-intermediate"] if noint else []
+        r = subprocess.run([str(exe), str(n), str(calls), str(P), *args, *extra, "--dump", pre,
+                            "--csv", str(csv)], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr
         d = oracle.gen_hostmem(n, dtype, oracle.SEED)
         e3, esc, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
@@ -338,7 +346,20 @@ def test_host_driver_end_to_end(oracle, tmp_path):
             inc = int(open(f"{pre}_call{i}_inc.txt").read())
             assert np.array_equal(bits(got), bits(e3))
             assert np.array_equal(sc, esc) and inc == einc
-        assert "GPU PLF kernel" in r.stdout
+        lines = csv.read_text().strip().split("\n")
+        assert len(lines) == 1 + calls
+        if noint:
+            for row in ("Prepare input for GPU:", "PLF on GPU:", "scaling wgt mult:"):
+                assert row in r.stdout
+            assert "GPU PLF kernel" not in r.stdout
+            assert lines[0] == "preparation,plf,scaling"
+        else:
+            assert "GPU PLF kernel" in r.stdout and "[all instances] Host to GPU memory" in r.stdout
+            assert lines[0].split(",") == ([f"hm{k}" for k in range(P)] + [f"msasm{k}" for k in range(P)]
+                                           + [f"mh{k}" for k in range(P)])
+        for ln in lines[1:]:
+            vals = [float(v) for v in ln.split(",")]
+            assert len(vals) == len(lines[0].split(",")) and all(v >= 0 for v in vals)
         # the driver's own check (host_mem.cpp:403-442): CPU plf() vs the GPU, exact
         assert "Test result: Passed" in r.stdout
         assert "Reference (CPU plf" in r.stdout and "Speed up (excluding transfers)" in r.stdout
