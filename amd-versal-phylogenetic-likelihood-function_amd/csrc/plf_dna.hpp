@@ -1132,8 +1132,15 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
 // site scaled) and is published by the per-region ticket at the end.  Results
 // are bit-identical to 63 separate updates.  (Measured, tools/gpu_deep.sh,
 // profiles/r01_deep.log: 256/512/768-thread blocks, U = 1/2, next-group
-// prefetch; coded leaves expanded in registers ran 20-40 % slower than the
-// three-level passes' tip tables, so the scheduler keeps tips there.)
+// prefetch.)
+// kTips = 2: every leaf is a tip (one uint8 state code per site, see
+// build_tip_table).  The level-1 nodes then read their ump values from
+// per-child LDS tables instead of multiplying: 2 x 2^(D-1) tables of 256
+// doubles (128 KiB at D = 6) built once per block, and only the upper levels'
+// matrices sit in LDS (31 KiB) -- 159.5 KiB of the 160.  (Round 1 expanded the
+// codes in registers instead and ran 20-40 % slower than the three-level
+// passes' tables; with the tables a coded 64-taxon tree reads 64 code bytes
+// and writes 63 CLVs per site in one pass.)
 // Heap-order level offsets of a complete subtree of depth D (level 1 first):
 // node numbers off(l) .. off(l) + 2^(D-1-l) - 1 hold level l+1.
 template <int D>
@@ -1151,22 +1158,40 @@ struct DeepDesc {
   int64_t *ss[63];
 };
 
-template <int D, bool kSum, bool NTL, int U, int kThreads>
+template <int D, bool kSum, bool NTL, int U, int kThreads, int kTips = 0>
 __global__ void __launch_bounds__(kThreads, 1)
 plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
-                        const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
+                        const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
+                        const double *__restrict__ tipvec = nullptr) {
   static_assert(D >= 4 && D <= 6, "depth 4..6");
+  static_assert(kTips == 0 || kTips == 2, "dense leaves or every leaf a tip");
   constexpr int kWaves = kThreads / 64, kNodes = (1 << D) - 1, kGroups = 1 << (D - 3);
+  constexpr bool kT = kTips == 2;
+  constexpr int kLeafOps = 1 << (D - 1);        // level-1 nodes
+  constexpr int kM0 = kT ? kLeafOps : 0;        // first node whose matrices sit in LDS
   const int lane = threadIdx.x & 63;
   const int h = lane & 1, c = (lane >> 1) & 3, g = lane >> 3, sh = lane & 56;
-  __shared__ double mats[kNodes][128];
+  __shared__ double mats[kNodes - kM0][128];
+  __shared__ double tabs[kT ? 2 * kLeafOps : 1][kT ? 256 : 1];  // [2i | 2i+1]: node i's left | right
   __shared__ unsigned long long nacc[kNodes];
-  for (int e = threadIdx.x; e < kNodes * 128; e += kThreads) {
-    const int node = e >> 7, k = e & 127;
-    mats[node][k] = static_cast<const double *>(d.mat[2 * node + (k >> 6)])[k & 63];
+  for (int e = threadIdx.x; e < (kNodes - kM0) * 128; e += kThreads) {
+    const int node = kM0 + (e >> 7), k = e & 127;
+    mats[node - kM0][k] = static_cast<const double *>(d.mat[2 * node + (k >> 6)])[k & 63];
+  }
+  if constexpr (kT) {  // build_tip_table's entries and order, 2^D tables at once
+    for (int e = threadIdx.x; e < 2 * kLeafOps * 256; e += kThreads) {
+      const int t = e >> 8, cc = (e >> 6) & 3, code = (e >> 2) & 15, k = e & 3;
+      const double *P = static_cast<const double *>(d.mat[t]);
+      double v = 0.0;
+#pragma unroll
+      for (int l = 0; l < 4; l++)
+        v += (tipvec ? tipvec[code * 4 + l] : double((code >> l) & 1)) * P[cc * 16 + k * 4 + l];
+      tabs[t][e & 255] = v;
+    }
   }
   if (threadIdx.x < kNodes) nacc[threadIdx.x] = 0;
   __syncthreads();
+  const int trow = c * 64 + 2 * h;  // + 4*code: this lane's slice of a table row
   double E[4][2];
 #pragma unroll
   for (int k = 0; k < 4; k++)
@@ -1188,16 +1213,24 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
       sq[j] = valid[j] ? base + 8 * j + g : n - 1;  // past n: any valid record (unused)
       w[j] = kSum ? wgt_at(wgt, sq[j], ws) : 0;
     }
-    // node `node` of this trip on inputs a, b: output stored, scaler byte and sum
-    auto node_eval = [&](int node, const f64x2 (&a)[U], const f64x2 (&b)[U], f64x2 (&o)[U]) {
+    // node `node` of this trip on inputs a, b (kT level 1: codes ka, kb):
+    // output stored, scaler byte and sum
+    auto node_eval = [&](int node, const f64x2 (&a)[U], const f64x2 (&b)[U], f64x2 (&o)[U],
+                         const int *ka = nullptr, const int *kb = nullptr) {
       PairMats M;
-      pair_mats_lds(mz + 128 * node, c, h, M);
+      const bool tipn = kT && node < kLeafOps;  // compile-time after unrolling
+      if (!tipn) pair_mats_lds(mz + 128 * (node - kM0), c, h, M);
       f64x2 *dst = static_cast<f64x2 *>(d.x[node]);
       uint8_t *scp = d.sc[node];
 #pragma unroll
       for (int j = 0; j < U; j++) {
         bool sc;
-        o[j] = pair_node<false, false>(a[j], b[j], nullptr, nullptr, M, E, valid[j], sh, m, sc);
+        if (tipn)
+          o[j] = pair_node<true, true>(a[j], b[j], &tabs[kT ? 2 * node : 0][trow + 4 * ka[j]],
+                                       &tabs[kT ? 2 * node + 1 : 0][trow + 4 * kb[j]], M, E, valid[j],
+                                       sh, m, sc);
+        else
+          o[j] = pair_node<false, false>(a[j], b[j], nullptr, nullptr, M, E, valid[j], sh, m, sc);
         if (valid[j]) {
           __builtin_nontemporal_store(o[j], dst + (base + 8 * j) * 8 + lane);
           if ((lane & 7) == 0 && scp) scp[base + 8 * j + g] = (uint8_t)sc;
@@ -1218,15 +1251,22 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
 #pragma unroll 1
     for (int q = 0; q < kGroups; q++) {
       f64x2 v[8][U];
+      int k8[8][U];
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        const f64x2 *gp = static_cast<const f64x2 *>(d.g[8 * q + i]);
 #pragma unroll
-        for (int j = 0; j < U; j++) v[i][j] = ld16<NTL>(gp + sq[j] * 8 + (lane & 7));
+        for (int j = 0; j < U; j++) {
+          if constexpr (kT) {
+            k8[i][j] = static_cast<const uint8_t *>(d.g[8 * q + i])[sq[j]] & 15;
+            v[i][j] = f64x2{0.0, 0.0};
+          } else {
+            v[i][j] = ld16<NTL>(static_cast<const f64x2 *>(d.g[8 * q + i]) + sq[j] * 8 + (lane & 7));
+          }
+        }
       }
       f64x2 a1[4][U], a2[2][U], r[U];
 #pragma unroll
-      for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i]);
+      for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i], k8[2 * i], k8[2 * i + 1]);
 #pragma unroll
       for (int i = 0; i < 2; i++) node_eval(deep_off<D>(1) + 2 * q + i, a1[2 * i], a1[2 * i + 1], a2[i]);
       node_eval(deep_off<D>(2) + q, a2[0], a2[1], r);

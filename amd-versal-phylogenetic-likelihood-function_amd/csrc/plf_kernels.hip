@@ -313,13 +313,16 @@ hipError_t launch_septets32_t(const dev::SeptetBatch &b, int count, const float 
 // fused six-level subtrees: 512-thread blocks (one LDS copy of the 63 nodes'
 // matrices per 8 waves), 2 x 8-site blocks per trip, grid = co-resident blocks
 // (tools/gpu_deep.sh, profiles/r01_deep.log)
-template <int D, typename T, bool kSum, int U, int kThreads>
+template <int D, typename T, bool kSum, int U, int kThreads, int kTips = 0>
 hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt, int64_t n,
-                         unsigned long long *ws, int max_blocks, hipStream_t s) {
+                         unsigned long long *ws, int max_blocks, hipStream_t s,
+                         const T *tipvec = nullptr) {
   static int resident = 0;
-  // f64: lane pairs, 8 sites per wave instruction; f32: lane = category, 16
+  // f64: lane pairs, 8 sites per wave instruction; f32: lane = category, 16;
+  // coded leaves (kTips = 2): f64 only
+  static_assert(kTips == 0 || sizeof(T) == 8, "coded-leaf deep pass: f64");
   auto kernel = [] {
-    if constexpr (sizeof(T) == 8) return &dev::plf_dna_f64_deep_kernel<D, kSum, kNtl64, U, kThreads>;
+    if constexpr (sizeof(T) == 8) return &dev::plf_dna_f64_deep_kernel<D, kSum, kNtl64, U, kThreads, kTips>;
     else return &dev::plf_dna_cat_deep_kernel<D, T, kSum, kNt, U, kThreads>;
   }();
   constexpr int kSitesPerWave = sizeof(T) == 8 ? 8 : 16;
@@ -337,7 +340,10 @@ hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt
   const int64_t per_block = (int64_t)(kThreads / 64) * kSitesPerWave * U;
   int64_t gx = (n + per_block - 1) / per_block;
   gx = std::max<int64_t>(1, std::min<int64_t>(gx, max_blocks > 0 ? max_blocks : resident));
-  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kThreads), 0, s, d, EV, wgt, n, ws);
+  if constexpr (sizeof(T) == 8)
+    hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kThreads), 0, s, d, EV, wgt, n, ws, tipvec);
+  else
+    hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kThreads), 0, s, d, EV, wgt, n, ws);
   return hipGetLastError();
 }
 
@@ -346,9 +352,16 @@ hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt
 template <int D>
 hipError_t launch_deep_d(int dtype, bool any_sum, const dev::DeepDesc &d, const void *EV,
                          const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
-                         hipStream_t s) {
+                         hipStream_t s, int tips, const void *tipvec) {
   const double *E64 = (const double *)EV;
   const float *E32 = (const float *)EV;
+  if (tips == 2) {
+    if (dtype != 1) return hipErrorInvalidValue;
+    const double *V = (const double *)tipvec;
+    return any_sum ? launch_deep_t<D, double, true, 2, 512, 2>(d, E64, wgt, n, ws, max_blocks, s, V)
+                   : launch_deep_t<D, double, false, 2, 512, 2>(d, E64, wgt, n, ws, max_blocks, s, V);
+  }
+  if (tips != 0) return hipErrorInvalidValue;
   if (dtype == 1)
     return any_sum ? launch_deep_t<D, double, true, 2, 512>(d, E64, wgt, n, ws, max_blocks, s)
                    : launch_deep_t<D, double, false, 2, 512>(d, E64, wgt, n, ws, max_blocks, s);
@@ -358,16 +371,16 @@ hipError_t launch_deep_d(int dtype, bool any_sum, const dev::DeepDesc &d, const 
 
 hipError_t launch_plf_dna_deep(int dtype, int depth, const DeepDescH *t, const void *EV,
                                const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
-                               hipStream_t s) {
+                               hipStream_t s, int tips, const void *tipvec) {
   if (depth < 4 || depth > 6) return hipErrorInvalidValue;
   dev::DeepDesc d;
   __builtin_memcpy(&d, t, sizeof(d));
   bool any_sum = false;
   for (int q = 0; q < (1 << depth) - 1; q++) any_sum |= t->ss[q] != nullptr;
   switch (depth) {
-    case 4: return launch_deep_d<4>(dtype, any_sum, d, EV, wgt, n, ws, max_blocks, s);
-    case 5: return launch_deep_d<5>(dtype, any_sum, d, EV, wgt, n, ws, max_blocks, s);
-    default: return launch_deep_d<6>(dtype, any_sum, d, EV, wgt, n, ws, max_blocks, s);
+    case 4: return launch_deep_d<4>(dtype, any_sum, d, EV, wgt, n, ws, max_blocks, s, tips, tipvec);
+    case 5: return launch_deep_d<5>(dtype, any_sum, d, EV, wgt, n, ws, max_blocks, s, tips, tipvec);
+    default: return launch_deep_d<6>(dtype, any_sum, d, EV, wgt, n, ws, max_blocks, s, tips, tipvec);
   }
 }
 

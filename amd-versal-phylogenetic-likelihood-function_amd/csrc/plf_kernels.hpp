@@ -90,9 +90,10 @@ hipError_t launch_plf_dna_septets(int dtype, const SeptetDescH *t, int count, co
                                   const int32_t *wgt, int64_t n, unsigned long long *ws,
                                   int max_blocks, hipStream_t s, int tips, const void *tipvec);
 
-// Fused complete subtree of depth 4..6 (plf_dna.hpp DeepDesc: 2^depth dense
-// leaves, 2^depth - 1 nodes in heap order by level), dtype 0 f32 / 1 f64, one
-// per launch, ws >= 2^depth - 1 regions.
+// Fused complete subtree of depth 4..6 (plf_dna.hpp DeepDesc: 2^depth leaves,
+// 2^depth - 1 nodes in heap order by level), dtype 0 f32 / 1 f64, one per
+// launch, ws >= 2^depth - 1 regions.  tips: 0 dense leaves; 2 every leaf a tip
+// (uint8 state codes; f64 only), tipvec as launch_plf_dna_batch's.
 struct DeepDescH {
   const void *g[64];
   void *x[63];
@@ -103,6 +104,6 @@ struct DeepDescH {
 constexpr int kDeepNodes = 63;
 hipError_t launch_plf_dna_deep(int dtype, int depth, const DeepDescH *t, const void *EV,
                                const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
-                               hipStream_t s);
+                               hipStream_t s, int tips = 0, const void *tipvec = nullptr);
 
 }  // namespace plfx

@@ -760,13 +760,14 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   };
   // Fused deep subtrees (DNA, plf_dna.hpp DeepDesc): a complete binary
   // subtree of depth D = 6, 5 or 4 (2^D - 1 ops on consecutive levels
-  // L..L+D-1), every op's own slot free by L (pdep <= L), dense leaves.  Collected per level in heap
+  // L..L+D-1), every op's own slot free by L (pdep <= L), all leaves dense
+  // or (f64) all leaves tips.  Collected per level in heap
   // order (children left to right before parents): the ops of level k are
   // lv[k], and lv[k][i]'s children were written by lv[k-1][2i], lv[k-1][2i+1].
   // Tried before the three-level subtrees.
   struct Deep {
     std::vector<int> ops;  // the 2^D - 1 ops in DeepDesc node order
-    int L, D;
+    int L, D, tips;        // tips: 0 dense leaves, 2 every leaf a tip
   };
   std::vector<Deep> deeps;
   std::function<bool(int, int, int, std::vector<int> *)> complete =
@@ -784,16 +785,22 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         if (level[r] < D - 1 || used[r]) continue;
         std::vector<int> lv[6];
         if (!complete(r, D, level[r] - (D - 1), lv)) continue;
-        bool dense = true;  // coded leaves stay with the three-level passes' tip tables
-        for (int j : lv[0]) dense = dense && !is_tip(ops[j].child1) && !is_tip(ops[j].child2);
+        // every leaf dense, or every leaf a tip (f64: the coded-leaf pass's
+        // tables); mixed leaves stay with the three-level passes
+        bool dense = true, coded = dtype == PLFX_F64;
+        for (int j : lv[0]) {
+          const bool t1 = is_tip(ops[j].child1), t2 = is_tip(ops[j].child2);
+          dense = dense && !t1 && !t2;
+          coded = coded && t1 && t2;
+        }
         // nor may a deep pass take the top of a subtree whose lower levels are
         // still unfused (over coded leaves: the septets below it would become
         // level pairs and move more bytes in all)
         for (int j : lv[0])
           for (int wr : {w1[j], w2[j]})
-            if (wr >= 0 && !used[wr] && level[wr] == level[r] - D) dense = false;
-        if (!dense) continue;
-        Deep t{{}, level[r] - (D - 1), D};
+            if (wr >= 0 && !used[wr] && level[wr] == level[r] - D) dense = coded = false;
+        if (!dense && !coded) continue;
+        Deep t{{}, level[r] - (D - 1), D, coded ? 2 : 0};
         for (int k = 0; k < D; k++) t.ops.insert(t.ops.end(), lv[k].begin(), lv[k].end());
         for (int j : t.ops) used[j] = 1;
         deeps.push_back(std::move(t));
@@ -857,9 +864,9 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         int kq;
         const int rc = check_node(ctx, node_of(j, &kq), kq, n, j);
         if (rc != PLFX_OK) return rc;
-        if (q < leaf_ops) {  // level 1: the (dense) leaves, child1 then child2
-          d.g[2 * q] = clv[o.child1];
-          d.g[2 * q + 1] = clv[o.child2];
+        if (q < leaf_ops) {  // level 1: the leaves (CLVs or tip codes), child1 then child2
+          d.g[2 * q] = t.tips ? (const void *)tips[o.child1] : clv[o.child1];
+          d.g[2 * q + 1] = t.tips ? (const void *)tips[o.child2] : clv[o.child2];
         }
         d.x[q] = clv[o.parent];
         d.mat[2 * q] = pm + (size_t)(2 * o.pmat) * mat * es;
@@ -872,7 +879,8 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
           if (ss) PLFX_HIP(ctx, hipMemsetAsync(ss, 0, sizeof(int64_t), s));
         continue;
       }
-      hipError_t e = plfx::launch_plf_dna_deep(dtype, t.D, &d, EV, wgt, n, ws, ctx->max_blocks, s);
+      hipError_t e = plfx::launch_plf_dna_deep(dtype, t.D, &d, EV, wgt, n, ws, ctx->max_blocks, s,
+                                               t.tips, tipvec);
       if (e != hipSuccess) return hip_fail(ctx, e, "fused deep-subtree launch");
       sched[6]++;
     }

@@ -240,6 +240,16 @@ def test_protein_tip_children(ctx, oracle, dtype, fma, kind, n):
     assert np.array_equal(sc.cpu().numpy(), fsc) and int(s.item()) == finc
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("kind", ["tip1", "tip2", "both"])
+def test_protein_tip_children_many_trips(ctx, oracle, dtype, kind):
+    """The matrix-core (FMA) kernels' tip paths across many trips per block
+    (2^16 + 1 sites: every block loops, and the next trip's dense tile is
+    fetched while the current one is multiplied), bit-identical to
+    the oracle's fused restatement on the expanded CLVs."""
+    test_protein_tip_children(ctx, oracle, dtype, True, kind, (1 << 16) + 1)
+
+
 def test_protein_tip_vector_table(ctx, oracle):
     """A caller tip-vector table (24 x 20, e.g. eigen coordinates or a
     different ambiguity model) replaces the default one."""

@@ -242,12 +242,12 @@ def test_fused_level_pairs_match_unfused(ctx, oracle, tipmode, dtype, monkeypatc
 def test_fused_six_level_subtrees(oracle, tipmode, dtype, monkeypatch):
     """PLFX_FUSE=3 (the default): complete six-level subtrees over dense
     leaves run as one 63-node pass (plf_dna_f64_deep_kernel, f32:
-    plf_dna_cat_deep_kernel).  A 128-taxon
-    balanced tree (two such passes, then the root) with a tail that reuses tips
-    and inner slots, n not a multiple of the trip; with dense tips the deep
-    passes run, with mixed / coded / left-coded tips (or a caller tipvec table)
-    the scheduler keeps the three-level passes: CLVs, scaler bytes and sums
-    bit-identical to the oracle in every case."""
+    plf_dna_cat_deep_kernel), and in f64 also over all-coded leaves (the
+    coded-leaf pass's LDS tip tables).  A 128-taxon balanced tree (two such
+    passes, then the root) with a tail that reuses tips and inner slots, n not
+    a multiple of the trip; with mixed / left-coded tips (or a caller tipvec
+    table over a mix) the scheduler keeps the three-level passes: CLVs, scaler
+    bytes and sums bit-identical to the oracle in every case."""
     import plfx
     import torch
 
@@ -286,8 +286,11 @@ def test_fused_six_level_subtrees(oracle, tipmode, dtype, monkeypatch):
         c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips,
                    tipvec=None if tv is None else dev(tv))
         torch.cuda.synchronize()
+        sched = c.last_schedule()
     finally:
         c.close()
+    deep = tipmode == "dense" or (tipmode == "coded" and dtype == np.float64)
+    assert sched["deep6"] == (2 if deep else 0), sched
     for s_ in range(ntax, nslots):
         assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
     assert np.array_equal(sums.cpu().numpy(), esums)
@@ -295,12 +298,13 @@ def test_fused_six_level_subtrees(oracle, tipmode, dtype, monkeypatch):
         assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
 
 
-@pytest.mark.parametrize("dtype", [np.float64, np.float32])
-@pytest.mark.parametrize("n", [1, 7, 17, 33])
-def test_six_level_pass_tiny_alignments(oracle, n, dtype, monkeypatch):
+@pytest.mark.parametrize("dtype,coded", [(np.float64, False), (np.float32, False), (np.float64, True)])
+@pytest.mark.parametrize("n", [1, 7, 17, 33, 4099])
+def test_six_level_pass_tiny_alignments(oracle, n, dtype, coded, monkeypatch):
     """The 63-node pass on alignments shorter than one trip (one wave
-    active, partial 8/16-site blocks): a 64-taxon balanced dense tree equals
-    the oracle bit for bit, sums included."""
+    active, partial 8/16-site blocks) and past it: a 64-taxon balanced tree
+    (dense leaves, or in f64 all leaves coded) equals the oracle bit for bit,
+    sums included, with nothing written past n."""
     import plfx
     import torch
 
@@ -310,10 +314,14 @@ def test_six_level_pass_tiny_alignments(oracle, n, dtype, monkeypatch):
     nslots, nops = 2 * ntax - 1, ops.shape[0]
     dense = [rng.random(16 * n).astype(dtype) for _ in range(ntax)]
     dense[0][::3] *= 1e-30 if dtype == np.float64 else 1e-20  # some sites scale
+    codes = [oracle.random_tip_codes(rng, n, 0.2) for _ in range(ntax)]
     pm = (rng.random(nops * 128) * 0.3).astype(dtype)
+    if coded:  # tiny P entries on the first tip's matrices: some sites scale
+        pm[:128] *= 1e-30
     EV = (rng.random(16) * 0.3).astype(dtype)
     wgt = rng.integers(1, 5, n).astype(np.int32)
-    host = [d.copy() for d in dense] + [np.zeros(16 * n, dtype) for _ in range(nslots - ntax)]
+    leaves = [oracle.expand_tips(codes[t], dtype) for t in range(ntax)] if coded else dense
+    host = [d.copy() for d in leaves] + [np.zeros(16 * n, dtype) for _ in range(nslots - ntax)]
     esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
     monkeypatch.setenv("PLFX_FUSE", "3")
     c = plfx.Context(0)
@@ -321,10 +329,11 @@ def test_six_level_pass_tiny_alignments(oracle, n, dtype, monkeypatch):
         tt = torch.float64 if dtype == np.float64 else torch.float32
         # oversized buffers with sentinels past n: a tail write would land there
         big = [torch.full((16 * (n + 24),), -1.0, dtype=tt, device="cuda") for _ in range(nslots - ntax)]
-        clv = [dev(d) for d in dense] + [b[:16 * n] for b in big]
+        clv = [None if coded else dev(d) for d in dense] + [b[:16 * n] for b in big]
+        tips = [dev(codes[t]) for t in range(ntax)] + [None] * (nslots - ntax) if coded else None
         sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
         sbig = [torch.full((n + 24,), 7, dtype=torch.uint8, device="cuda") for _ in range(nops)]
-        c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), [x[:n] for x in sbig], sums)
+        c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), [x[:n] for x in sbig], sums, tips=tips)
         torch.cuda.synchronize()
         sched = c.last_schedule()
     finally:
@@ -404,8 +413,11 @@ def test_fused_depth4_depth5_subtrees(oracle, tipmode, dtype, monkeypatch):
         c.close()
     if tipmode == "dense":  # the 16-taxon subtree one depth-4 pass, the 32-taxon one depth-5
         assert sched["deep5"] == 1 and sched["deep4"] == 1, sched
-    else:  # the coded half keeps three-level passes; the dense 16-taxon parts run depth-4
-        assert sched["deep5"] == 0 and sched["deep4"] >= 1 and sched["septets"] >= 1, sched
+    else:  # the mixed 32-taxon subtree splits: its dense half runs depth-4, its coded half
+        # depth-4 too in f64 (coded-leaf pass), three-level passes in f32
+        assert sched["deep5"] == 0 and sched["deep4"] >= (3 if dtype == np.float64 else 1), sched
+        if dtype == np.float32:
+            assert sched["septets"] >= 1, sched
     for s_ in range(ntax, nslots):
         assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
     assert np.array_equal(sums.cpu().numpy(), esums)
