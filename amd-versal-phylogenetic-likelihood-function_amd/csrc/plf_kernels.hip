@@ -358,8 +358,12 @@ hipError_t launch_deep_d(int dtype, bool any_sum, const dev::DeepDesc &d, const 
   if (tips == 2) {
     if (dtype != 1) return hipErrorInvalidValue;
     const double *V = (const double *)tipvec;
-    return any_sum ? launch_deep_t<D, double, true, 2, 512, 2>(d, E64, wgt, n, ws, max_blocks, s, V)
-                   : launch_deep_t<D, double, false, 2, 512, 2>(d, E64, wgt, n, ws, max_blocks, s, V);
+    // coded leaves: 4 x 8-site blocks per trip (every output stream gets 4 KiB
+    // runs per wave and trip; the pass is write-bound): 0.693 -> 0.727 of
+    // peak on tree64 --tips same box, U = 1 0.637; U = 6/8 spill
+    // (profiles/r03_ab_deep_tips_u.log)
+    return any_sum ? launch_deep_t<D, double, true, 4, 512, 2>(d, E64, wgt, n, ws, max_blocks, s, V)
+                   : launch_deep_t<D, double, false, 4, 512, 2>(d, E64, wgt, n, ws, max_blocks, s, V);
   }
   if (tips != 0) return hipErrorInvalidValue;
   if (dtype == 1)
