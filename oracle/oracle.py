@@ -158,6 +158,37 @@ def ref_lib(opt: str = "O0"):
     return _refs[opt]
 
 
+def ref_lib_f64(opt: str = "O0"):
+    """The reference plf()'s double instantiation (oracle/ref_shim_f64.cpp:
+    the unmodified plf.cpp compiled with float spelled double), or None."""
+    key = "f64_" + opt
+    if key not in _refs:
+        p = ORACLE_DIR / "_ref" / f"libplfref_f64_{opt}.so"
+        if not p.exists():
+            _refs[key] = None
+        else:
+            L = C.CDLL(str(p))
+            f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+            L.plfref_plf_f64.argtypes = [f64p, f64p, f64p, f64p, C.c_int, f64p, f64p, _i32p]
+            L.plfref_plf_f64.restype = C.c_int
+            _refs[key] = L
+    return _refs[key]
+
+
+def ref_plf_f64(x1, x2, EV, left, right, wgt, opt="O0"):
+    """(x3, scalerIncrement) from the reference's own loop in double, or None
+    when oracle/_ref holds no f64 build."""
+    L = ref_lib_f64(opt)
+    if L is None:
+        return None
+    c = lambda a: np.ascontiguousarray(a, np.float64)  # noqa: E731
+    a1, a2 = c(x1), c(x2)
+    n = a1.size // 16
+    x3 = np.empty(16 * n, np.float64)
+    inc = L.plfref_plf_f64(a1, a2, x3, c(EV), n, c(left), c(right), np.ascontiguousarray(wgt, np.int32))
+    return x3, int(inc)
+
+
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 

@@ -304,6 +304,33 @@ def test_instance_run_host_buffers(ctx, oracle, dtype, layout, P, W):
     assert int((scal.astype(np.int64) * d["wgt"]).sum()) == einc
 
 
+@pytest.mark.parametrize("n", [1, 4099, (1 << 16) + 3])
+def test_plf_f64_against_reference_double_instantiation(ctx, oracle, n):
+    """The f64 kernels against the REFERENCE's own loop in double (plf.cpp
+    compiled with float spelled double, oracle/_ref/libplfref_f64_O0.so,
+    which travels with the snapshot): the device entry (lane-pair kernel) and
+    the host plf()-shaped entry, bit for bit, scaler sum exact; every 4th site
+    underflows."""
+    import torch
+
+    if oracle.ref_lib_f64("O0") is None:
+        pytest.skip("oracle/_ref has no f64 build")
+    d = oracle.gen_hostmem(n, np.float64, 2024 + n)
+    d["x1"].reshape(-1, 16)[::4] *= 1e-30
+    w = (np.arange(n) % 7 + 1).astype(np.int32)
+    r3, rinc = oracle.ref_plf_f64(d["x1"], d["x2"], d["EV"], d["left"], d["right"], w)
+    t = {k: torch_dev(d[k]) for k in ("x1", "x2", "EV", "left", "right")}
+    x3 = torch.empty_like(t["x1"])
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.plf_dev(t["x1"], t["x2"], x3, t["EV"], t["left"], t["right"], torch_dev(w), None, s)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(x3.cpu().numpy()), bits(r3))
+    assert int(s.item()) == rinc
+    h3 = np.empty_like(d["x1"])
+    inc = ctx.plf(d["x1"], d["x2"], h3, d["EV"], n, d["left"], d["right"], w)
+    assert np.array_equal(bits(h3), bits(r3)) and inc == rinc
+
+
 def test_rejects_bad_arguments(ctx):
     import plfx
     import torch

@@ -103,6 +103,36 @@ def test_reference_binary_live(oracle):
             assert inc == rinc
 
 
+def test_reference_double_instantiation_live(oracle):
+    """Pins the f64 restatement: the reference's own plf() loop compiled in
+    double (oracle/ref_shim_f64.cpp builds the unmodified plf.cpp with float
+    spelled double) equals the oracle's f64 plf() bit for bit, at -O0 and -O3,
+    on host_mem-protocol inputs, on inputs where every 4th site underflows,
+    and on hand-built edge sites (values straddling 2^-32, signed zeros)."""
+    if oracle.ref_lib_f64("O0") is None:
+        pytest.skip("oracle/_ref has no f64 build")
+    rng = np.random.default_rng(5)
+    cases = []
+    for n, seed in ((777, 1), (4096, 99)):
+        d = oracle.gen_hostmem(n, np.float64, seed)
+        cases.append((d, (np.arange(n) % 5 + 1).astype(np.int32)))
+    d = oracle.gen_hostmem(1024, np.float64, 3)
+    d["x1"].reshape(-1, 16)[::4] *= 1e-30
+    d["x2"].reshape(-1, 16)[1::4] *= -1e-25
+    cases.append((d, d["wgt"]))
+    e = oracle.gen_hostmem(64, np.float64, 11)
+    e["x1"].reshape(-1, 16)[:, :] = rng.choice([0.0, -0.0, 2.0 ** -33, 2.0 ** -32, 1e-300, 1.0],
+                                              size=(64, 16))
+    cases.append((e, e["wgt"]))
+    for d, w in cases:
+        x3, sc, inc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], w)
+        assert sc.any() or d["x1"].size != 16 * 1024
+        for opt in ("O0", "O3"):
+            r3, rinc = oracle.ref_plf_f64(d["x1"], d["x2"], d["EV"], d["left"], d["right"], w, opt)
+            assert np.array_equal(bits(x3), bits(r3)), opt
+            assert inc == rinc
+
+
 def test_double_and_generic_agree(oracle):
     d = oracle.gen_hostmem(513, np.float64, 7)
     x3, sc, inc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
