@@ -1296,22 +1296,42 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
 // The same six-level pass in the lane = category mapping (f32; any T): lane =
 // (site q, category c), 16 sites per wave and block of U; a lane reads its
 // category's 32 matrix values per node from the LDS copy (31.5 KB f32).
-template <int D, typename T, bool kSum, bool NT, int U, int kThreads>
+// kTips = 2: every leaf a tip, as the f64 pass (2^D per-child tables of 256
+// values, 64 KiB f32 at D = 6, beside the upper levels' 15.5 KiB of matrices).
+template <int D, typename T, bool kSum, bool NT, int U, int kThreads, int kTips = 0>
 __global__ void __launch_bounds__(kThreads, 1)
 plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
-                        const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
+                        const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
+                        const T *__restrict__ tipvec = nullptr) {
   static_assert(D >= 4 && D <= 6, "depth 4..6");
+  static_assert(kTips == 0 || kTips == 2, "dense leaves or every leaf a tip");
   constexpr int kWaves = kThreads / 64, kNodes = (1 << D) - 1, kGroups = 1 << (D - 3);
+  constexpr bool kT = kTips == 2;
+  constexpr int kLeafOps = 1 << (D - 1);  // level-1 nodes
+  constexpr int kM0 = kT ? kLeafOps : 0;  // first node whose matrices sit in LDS
   const int lane = threadIdx.x & 63;
   const int c = lane & 3, qs = lane >> 2, nib = lane & 60;
-  __shared__ T mats[kNodes * 128];  // node i: left [c][16] | right [c][16]
+  __shared__ T mats[(kNodes - kM0) * 128];  // node i: left [c][16] | right [c][16]
+  __shared__ T tabs[kT ? 2 * kLeafOps : 1][kT ? 256 : 1];  // [2i | 2i+1]: node i's left | right
   __shared__ unsigned long long nacc[kNodes];
-  for (int e = threadIdx.x; e < kNodes * 128; e += kThreads) {
-    const int node = e >> 7, k = e & 127;
+  for (int e = threadIdx.x; e < (kNodes - kM0) * 128; e += kThreads) {
+    const int node = kM0 + (e >> 7), k = e & 127;
     mats[e] = static_cast<const T *>(d.mat[2 * node + (k >> 6)])[k & 63];
+  }
+  if constexpr (kT) {  // build_tip_table's entries and order, 2^D tables at once
+    for (int e = threadIdx.x; e < 2 * kLeafOps * 256; e += kThreads) {
+      const int t = e >> 8, cc = (e >> 6) & 3, code = (e >> 2) & 15, k = e & 3;
+      const T *P = static_cast<const T *>(d.mat[t]);
+      T v = T(0);
+#pragma unroll
+      for (int l = 0; l < 4; l++)
+        v += (tipvec ? tipvec[code * 4 + l] : T((code >> l) & 1)) * P[cc * 16 + k * 4 + l];
+      tabs[t][e & 255] = v;
+    }
   }
   if (threadIdx.x < kNodes) nacc[threadIdx.x] = 0;
   __syncthreads();
+  const int trow = c * 64;  // + 4*code: this lane's table row
   T E[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) E[i] = EV[i];
@@ -1331,19 +1351,29 @@ plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
       sq[u] = valid[u] ? base + u * 16 + qs : n - 1;  // past n: any valid record (unused)
       w[u] = kSum ? wgt_at(wgt, sq[u], ws) : 0;
     }
-    auto node_eval = [&](int node, const T (&a)[U][4], const T (&b)[U][4], T (&o)[U][4]) {
+    // kT level-1 nodes: codes ka, kb instead of matrices
+    auto node_eval = [&](int node, const T (&a)[U][4], const T (&b)[U][4], T (&o)[U][4],
+                         const int *ka = nullptr, const int *kb = nullptr) {
+      const bool tipn = kT && node < kLeafOps;  // compile-time after unrolling
       T PL[16], PR[16];
+      if (!tipn) {
 #pragma unroll
-      for (int j = 0; j < 16; j++) {
-        PL[j] = mz[128 * node + c * 16 + j];
-        PR[j] = mz[128 * node + 64 + c * 16 + j];
+        for (int j = 0; j < 16; j++) {
+          PL[j] = mz[128 * (node - kM0) + c * 16 + j];
+          PR[j] = mz[128 * (node - kM0) + 64 + c * 16 + j];
+        }
       }
       T *dst = static_cast<T *>(d.x[node]);
       uint8_t *scp = d.sc[node];
 #pragma unroll
       for (int u = 0; u < U; u++) {
         bool sc;
-        cat_node<T, false, false>(a[u], b[u], nullptr, nullptr, PL, PR, E, valid[u], nib, m, o[u], sc);
+        if (tipn)
+          cat_node<T, true, true>(a[u], b[u], &tabs[kT ? 2 * node : 0][trow + 4 * ka[u]],
+                                  &tabs[kT ? 2 * node + 1 : 0][trow + 4 * kb[u]], PL, PR, E, valid[u],
+                                  nib, m, o[u], sc);
+        else
+          cat_node<T, false, false>(a[u], b[u], nullptr, nullptr, PL, PR, E, valid[u], nib, m, o[u], sc);
         if (valid[u]) {
           Num<T>::store4_nt(dst + sq[u] * 16 + c * 4, o[u]);
           if (c == 0 && scp) scp[sq[u]] = (uint8_t)sc;
@@ -1365,15 +1395,23 @@ plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
 #pragma unroll 1
     for (int q = 0; q < kGroups; q++) {
       T v[8][U][4];
+      int k8[8][U];
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        const T *gp = static_cast<const T *>(d.g[8 * q + i]);
 #pragma unroll
-        for (int u = 0; u < U; u++) Num<T>::template load4<NT>(gp + sq[u] * 16 + c * 4, v[i][u]);
+        for (int u = 0; u < U; u++) {
+          if constexpr (kT) {
+            k8[i][u] = static_cast<const uint8_t *>(d.g[8 * q + i])[sq[u]] & 15;
+#pragma unroll
+            for (int l = 0; l < 4; l++) v[i][u][l] = T(0);
+          } else {
+            Num<T>::template load4<NT>(static_cast<const T *>(d.g[8 * q + i]) + sq[u] * 16 + c * 4, v[i][u]);
+          }
+        }
       }
       T a1[4][U][4], a2[2][U][4], r[U][4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i]);
+      for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i], k8[2 * i], k8[2 * i + 1]);
 #pragma unroll
       for (int i = 0; i < 2; i++) node_eval(deep_off<D>(1) + 2 * q + i, a1[2 * i], a1[2 * i + 1], a2[i]);
       node_eval(deep_off<D>(2) + q, a2[0], a2[1], r);

@@ -318,12 +318,10 @@ hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt
                          unsigned long long *ws, int max_blocks, hipStream_t s,
                          const T *tipvec = nullptr) {
   static int resident = 0;
-  // f64: lane pairs, 8 sites per wave instruction; f32: lane = category, 16;
-  // coded leaves (kTips = 2): f64 only
-  static_assert(kTips == 0 || sizeof(T) == 8, "coded-leaf deep pass: f64");
+  // f64: lane pairs, 8 sites per wave instruction; f32: lane = category, 16
   auto kernel = [] {
     if constexpr (sizeof(T) == 8) return &dev::plf_dna_f64_deep_kernel<D, kSum, kNtl64, U, kThreads, kTips>;
-    else return &dev::plf_dna_cat_deep_kernel<D, T, kSum, kNt, U, kThreads>;
+    else return &dev::plf_dna_cat_deep_kernel<D, T, kSum, kNt, U, kThreads, kTips>;
   }();
   constexpr int kSitesPerWave = sizeof(T) == 8 ? 8 : 16;
   if (!resident) {
@@ -340,10 +338,7 @@ hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt
   const int64_t per_block = (int64_t)(kThreads / 64) * kSitesPerWave * U;
   int64_t gx = (n + per_block - 1) / per_block;
   gx = std::max<int64_t>(1, std::min<int64_t>(gx, max_blocks > 0 ? max_blocks : resident));
-  if constexpr (sizeof(T) == 8)
-    hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kThreads), 0, s, d, EV, wgt, n, ws, tipvec);
-  else
-    hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kThreads), 0, s, d, EV, wgt, n, ws);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kThreads), 0, s, d, EV, wgt, n, ws, tipvec);
   return hipGetLastError();
 }
 
@@ -355,8 +350,15 @@ hipError_t launch_deep_d(int dtype, bool any_sum, const dev::DeepDesc &d, const 
                          hipStream_t s, int tips, const void *tipvec) {
   const double *E64 = (const double *)EV;
   const float *E32 = (const float *)EV;
+  if (tips == 2 && dtype != 1) {  // coded leaves, f32
+    const float *V = (const float *)tipvec;
+    // 4 x 16-site blocks per trip, as f64: tree64 f32 --tips 0.664 (U = 2) ->
+    // 0.707 same box, U = 1 0.673; three-level passes 0.633
+    // (profiles/r03_ab_deep_tips_u_f32.log)
+    return any_sum ? launch_deep_t<D, float, true, 4, 512, 2>(d, E32, wgt, n, ws, max_blocks, s, V)
+                   : launch_deep_t<D, float, false, 4, 512, 2>(d, E32, wgt, n, ws, max_blocks, s, V);
+  }
   if (tips == 2) {
-    if (dtype != 1) return hipErrorInvalidValue;
     const double *V = (const double *)tipvec;
     // coded leaves: 4 x 8-site blocks per trip (every output stream gets 4 KiB
     // runs per wave and trip; the pass is write-bound): 0.693 -> 0.727 of

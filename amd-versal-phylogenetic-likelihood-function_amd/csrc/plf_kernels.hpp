@@ -93,7 +93,7 @@ hipError_t launch_plf_dna_septets(int dtype, const SeptetDescH *t, int count, co
 // Fused complete subtree of depth 4..6 (plf_dna.hpp DeepDesc: 2^depth leaves,
 // 2^depth - 1 nodes in heap order by level), dtype 0 f32 / 1 f64, one per
 // launch, ws >= 2^depth - 1 regions.  tips: 0 dense leaves; 2 every leaf a tip
-// (uint8 state codes; f64 only), tipvec as launch_plf_dna_batch's.
+// (uint8 state codes), tipvec as launch_plf_dna_batch's.
 struct DeepDescH {
   const void *g[64];
   void *x[63];

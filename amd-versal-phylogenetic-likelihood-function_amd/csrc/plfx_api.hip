@@ -761,7 +761,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   // Fused deep subtrees (DNA, plf_dna.hpp DeepDesc): a complete binary
   // subtree of depth D = 6, 5 or 4 (2^D - 1 ops on consecutive levels
   // L..L+D-1), every op's own slot free by L (pdep <= L), all leaves dense
-  // or (f64) all leaves tips.  Collected per level in heap
+  // or all leaves tips.  Collected per level in heap
   // order (children left to right before parents): the ops of level k are
   // lv[k], and lv[k][i]'s children were written by lv[k-1][2i], lv[k-1][2i+1].
   // Tried before the three-level subtrees.
@@ -785,9 +785,9 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         if (level[r] < D - 1 || used[r]) continue;
         std::vector<int> lv[6];
         if (!complete(r, D, level[r] - (D - 1), lv)) continue;
-        // every leaf dense, or every leaf a tip (f64: the coded-leaf pass's
+        // every leaf dense, or every leaf a tip (the coded-leaf pass's
         // tables); mixed leaves stay with the three-level passes
-        bool dense = true, coded = dtype == PLFX_F64;
+        bool dense = true, coded = true;
         for (int j : lv[0]) {
           const bool t1 = is_tip(ops[j].child1), t2 = is_tip(ops[j].child2);
           dense = dense && !t1 && !t2;

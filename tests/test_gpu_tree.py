@@ -242,8 +242,8 @@ def test_fused_level_pairs_match_unfused(ctx, oracle, tipmode, dtype, monkeypatc
 def test_fused_six_level_subtrees(oracle, tipmode, dtype, monkeypatch):
     """PLFX_FUSE=3 (the default): complete six-level subtrees over dense
     leaves run as one 63-node pass (plf_dna_f64_deep_kernel, f32:
-    plf_dna_cat_deep_kernel), and in f64 also over all-coded leaves (the
-    coded-leaf pass's LDS tip tables).  A 128-taxon balanced tree (two such
+    plf_dna_cat_deep_kernel), also over all-coded leaves (the coded-leaf
+    pass's LDS tip tables).  A 128-taxon balanced tree (two such
     passes, then the root) with a tail that reuses tips and inner slots, n not
     a multiple of the trip; with mixed / left-coded tips (or a caller tipvec
     table over a mix) the scheduler keeps the three-level passes: CLVs, scaler
@@ -289,7 +289,7 @@ def test_fused_six_level_subtrees(oracle, tipmode, dtype, monkeypatch):
         sched = c.last_schedule()
     finally:
         c.close()
-    deep = tipmode == "dense" or (tipmode == "coded" and dtype == np.float64)
+    deep = tipmode in ("dense", "coded")
     assert sched["deep6"] == (2 if deep else 0), sched
     for s_ in range(ntax, nslots):
         assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
@@ -298,12 +298,13 @@ def test_fused_six_level_subtrees(oracle, tipmode, dtype, monkeypatch):
         assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
 
 
-@pytest.mark.parametrize("dtype,coded", [(np.float64, False), (np.float32, False), (np.float64, True)])
+@pytest.mark.parametrize("dtype,coded", [(np.float64, False), (np.float32, False), (np.float64, True),
+                                         (np.float32, True)])
 @pytest.mark.parametrize("n", [1, 7, 17, 33, 4099])
 def test_six_level_pass_tiny_alignments(oracle, n, dtype, coded, monkeypatch):
     """The 63-node pass on alignments shorter than one trip (one wave
     active, partial 8/16-site blocks) and past it: a 64-taxon balanced tree
-    (dense leaves, or in f64 all leaves coded) equals the oracle bit for bit,
+    (dense leaves, or all leaves coded) equals the oracle bit for bit,
     sums included, with nothing written past n."""
     import plfx
     import torch
@@ -413,11 +414,9 @@ def test_fused_depth4_depth5_subtrees(oracle, tipmode, dtype, monkeypatch):
         c.close()
     if tipmode == "dense":  # the 16-taxon subtree one depth-4 pass, the 32-taxon one depth-5
         assert sched["deep5"] == 1 and sched["deep4"] == 1, sched
-    else:  # the mixed 32-taxon subtree splits: its dense half runs depth-4, its coded half
-        # depth-4 too in f64 (coded-leaf pass), three-level passes in f32
-        assert sched["deep5"] == 0 and sched["deep4"] >= (3 if dtype == np.float64 else 1), sched
-        if dtype == np.float32:
-            assert sched["septets"] >= 1, sched
+    else:  # the mixed 32-taxon subtree splits: its dense half and its coded half
+        # (the coded-leaf pass) run depth-4 each, beside the 16-taxon subtree's
+        assert sched["deep5"] == 0 and sched["deep4"] >= 3, sched
     for s_ in range(ntax, nslots):
         assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
     assert np.array_equal(sums.cpu().numpy(), esums)
