@@ -208,13 +208,20 @@ hipError_t launch_prot_mfma_t(const DnaArgs &a, int max_blocks, hipStream_t s,
   static int cache = 0;
   // X3 to LDS through permuted back-transform rows (kX3 = 2: conflict-free
   // b128 writes; 90.2 vs 91.2 us at 2^18, 342 vs 345 at 2^20, tools/tune_prot.hip,
-  // profiles/r02_tune_protein_v3.log); first tile's loads before the matrix fragments
-  auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, kTips>;
+  // profiles/r02_tune_protein_v3.log); first tile's loads before the matrix fragments.
+  // From 32 tiles per block (2^20 sites at 512 blocks) on, tiles come from the
+  // device-wide queue (kDyn, plf_prot.hpp ProtQueue): 2^20 -3..-5 %, 2^22 -10 %
+  // dense, tip/inner -8 / -14 %; below that, and for tip/tip nodes at any size,
+  // the fixed stride is as fast or faster (tools/tune_prot64d.hip,
+  // profiles/r03_tune_protein_dyn.log)
+  auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, kTips, false>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
-  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
-                     (const double *)a.x2, (double *)a.x3, (const double *)a.EV,
-                     (const double *)a.left, (const double *)a.right, a.wgt, a.scaler, a.n, a.ws,
-                     a.scaler_sum, tipvec);
+  const bool dyn = kTips < 2 && a.ws && (a.n + 63) / 64 >= 32 * gx;
+  auto dyn_kernel = &dev::plf_prot_mfma_kernel<kSum, 2, kTips, true>;
+  hipLaunchKernelGGL(dyn ? dyn_kernel : kernel, dim3((unsigned)gx),
+                     dim3(kBlock), 0, s, (const double *)a.x1, (const double *)a.x2, (double *)a.x3,
+                     (const double *)a.EV, (const double *)a.left, (const double *)a.right, a.wgt,
+                     a.scaler, a.n, a.ws, a.scaler_sum, tipvec);
   return hipGetLastError();
 }
 

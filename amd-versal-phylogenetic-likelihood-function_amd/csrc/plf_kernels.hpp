@@ -16,7 +16,9 @@ struct DnaArgs {
   const int32_t *wgt;       // may be null (weights = 1)
   uint8_t *scaler;          // may be null
   int64_t *scaler_sum;      // may be null
-  unsigned long long *ws;   // ticket word (needed iff scaler_sum)
+  unsigned long long *ws;   // ticket words (needed iff scaler_sum); the f64 protein FMA
+                            // launch also takes its tile queue from ws + kWsWords when
+                            // non-null (2 x kWsWords words, zero at rest)
   int64_t n;
 };
 

@@ -469,7 +469,63 @@ plf_prot_lds_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__res
 // phase 2); the first tile's loads go out before the matrix fragments'.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-template <bool kSum, int kMinWaves, int kTips>
+// Device-wide tile queue for the protein kernels (kDyn).  Why: with two or
+// three co-resident blocks per CU the oldest block's waves win the SIMD's issue
+// arbitration -- at 2^18 sites the first block on each CU finished its 8 fixed
+// trips at ~75 us, the second at ~83 us (tools/probes/prot_timeline.hip) -- so
+// a fixed grid stride leaves CUs half idle at the end, more so the more trips a
+// block makes.  Tiles: trip 0 takes blockIdx.x, trip 1 G + blockIdx.x, trip
+// i >= 2 2G + d, d from a returning atomic add on a head word that thread 0
+// issues in the middle of trip i - 2 (right after the wave's next-tile loads,
+// so no wait lands on it before the next trip's start) and publishes in LDS at
+// the start of trip i - 1 (its only use: any use makes the wave wait for the
+// atomic there).  The head address carries an offset laundered through an
+// empty asm (a VGPR 0), so the compiler's atomic optimizer (a uniform address
+// makes it aggregate lanes and read the result at once) leaves the single-lane
+// add alone, and the address stays global (a laundered pointer turns it into
+// a flat atomic, which every LDS wait would then wait for).  Words: the stream
+// workspace's second region (ws + kWsWords; the protein launches use only the
+// first): [0] head, [16] exit count.  The last block out zeroes both for the
+// next launch; a block's last dequeue has returned before its exit add (the
+// add depends on the returned value).  Every dequeued tile index is consumed
+// in order, and one past the end ends the block, so no tile is lost.
+struct ProtQueue {
+  unsigned long long *head, *done;
+  int64_t G, ntiles;
+  long long pend = 0;  // thread 0: the dequeued value for the tile of trip i + 2
+  bool dyn;
+  __device__ ProtQueue(unsigned long long *ws, int64_t n, bool on) {
+    int zero = 0;  // a divergent-looking 0: the address stays global, not uniform
+    if (on) asm volatile("" : "+v"(zero));
+    head = ws + kWsWords + zero;
+    done = ws + kWsWords + 16;
+    G = gridDim.x;
+    ntiles = (n + 63) / 64;
+    dyn = ntiles > 2 * G;
+  }
+  __device__ __forceinline__ void dequeue() {
+    if (dyn && threadIdx.x == 0)
+      pend = (long long)__hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // thread 0: the base of trip i + 1 (n * 64 sentinel clipped by the caller's loop)
+  __device__ __forceinline__ int64_t next_base(int i) const {
+    int64_t t = ntiles;
+    if (i == 0) t = G + blockIdx.x;
+    else if (dyn) t = 2 * G + pend;
+    return (t < ntiles ? t : ntiles) * 64;
+  }
+  __device__ __forceinline__ void finish() const {
+    if (threadIdx.x != 0) return;
+    const unsigned long long after = (unsigned long long)(pend >> 62);  // 0, once it returned
+    const unsigned long long d = __hip_atomic_fetch_add(done, 1ull + after, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (unsigned long long)G - 1) {
+      __hip_atomic_store(head, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+};
+
+template <bool kSum, int kMinWaves, int kTips, bool kDyn = false>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                      double *__restrict__ x3, const double *__restrict__ EV,
@@ -516,6 +572,9 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
     u0 = f64x4{r[g], r[g + 4], r[g + 8], r[g + 12]};
     u1 = f64x4{r[16 + g], 0.0, 0.0, 0.0};
   };
+  // kDyn: tiles handed out by a device-wide dequeue (prot_queue below)
+  ProtQueue pq(ws, n, kDyn);
+  __shared__ long long qslot;
   __shared__ f64x2 tile[64 * PT::kStride];
   __shared__ unsigned long long small_mask[kWavesPerBlock];
   const double *td = reinterpret_cast<const double *>(tile);
@@ -526,7 +585,8 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
 #pragma unroll
     for (int st = 0; st < 5; st++) bv[st] = xr[4 * st];
   };
-  auto trip = [&](const int64_t base) {
+  auto trip = [&](const int64_t base) -> int64_t {
+    int64_t next = base + stride;  // kDyn: read from qslot after the trip's first barrier
     f64x4 P[4][2];  // per sub-tile: U_L^T, then p = U_L^T * U_R^T
     const int64_t sq = base + lane < n ? base + lane : n - 1;
     const int code1 = T1 ? prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) : 0;
@@ -537,6 +597,7 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
     } else {
       tile_put<double>(tile, pf);
       __syncthreads();
+      if constexpr (kDyn) next = qslot;
       tile_fetch<double>(x2, base, n, pf);
 #pragma unroll
       for (int t = 0; t < 4; t++) {
@@ -563,11 +624,17 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
         P[t][0] = P[t][0] * u0;  // prod[k] = umpL[k] * umpR[k]
         P[t][1] = P[t][1] * u1;
       }
+      if constexpr (kDyn) {
+        next = qslot;  // published before the trip's extra barrier
+        pq.dequeue();
+      }
     } else {
       tile_put<double>(tile, pf);
       __syncthreads();
+      if constexpr (kDyn && T1) next = qslot;
       // next trip's first dense child: x1, or x2 when x1 is a tip
-      if (base + stride < n) tile_fetch<double>(T1 ? x2 : x1, base + stride, n, pf);
+      if (next < n) tile_fetch<double>(T1 ? x2 : x1, next, n, pf);
+      if constexpr (kDyn) pq.dequeue();
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         double bv[5];
@@ -643,9 +710,20 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
       }
     }
     __syncthreads();
+    return next;
   };
-  int64_t base = (int64_t)blockIdx.x * 64;
-  for (; base < n; base += stride) trip(base);
+  if constexpr (kDyn) {
+    int64_t base = (int64_t)blockIdx.x * 64;
+    for (int i = 0; base < n; i++) {
+      if (threadIdx.x == 0) qslot = pq.next_base(i);
+      if constexpr (T1 && T2) __syncthreads();
+      base = trip(base);
+    }
+    pq.finish();
+  } else {
+    int64_t base = (int64_t)blockIdx.x * 64;
+    for (; base < n; base += stride) trip(base);
+  }
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
 

@@ -116,6 +116,64 @@ def test_protein_full_size_256k(ctx, oracle):
     assert abs(float(out.item()) - exp) <= 1e-12 * abs(exp)
 
 
+@pytest.fixture
+def small_grid_ctx(monkeypatch):
+    """A context whose grid-stride kernels launch 3 blocks (PLFX_MAX_BLOCKS):
+    a few thousand sites then give every block dozens of trips."""
+    import plfx
+
+    monkeypatch.setenv("PLFX_MAX_BLOCKS", "3")
+    c = plfx.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("kind", ["dense", "tip1", "tip2", "both"])
+def test_protein_f64_fma_tile_queue(small_grid_ctx, oracle, kind):
+    """The f64 FMA kernel's device-wide tile queue (kDyn: from 32 tiles per
+    block; here 3 blocks, 121 tiles, a ragged last one): bit-identical to the
+    oracle's fused restatement on the expanded CLVs, scaler bytes and sum exact,
+    three launches in a row (the queue words reset themselves).  Both-tip nodes
+    keep the fixed stride."""
+    import torch
+
+    ctx = small_grid_ctx
+    n = 3 * 64 * 40 + 37
+    rng = np.random.default_rng(321)
+    x1, x2, EV, left, right, w = gen(n, np.float64, 99)
+    c1, c2 = oracle.random_protein_codes(rng, n, 0.3), oracle.random_protein_codes(rng, n, 0.3)
+    e1 = oracle.expand_protein_tips(c1, np.float64) if kind in ("tip1", "both") else x1
+    e2 = oracle.expand_protein_tips(c2, np.float64) if kind in ("tip2", "both") else x2
+    f3, fsc, finc = oracle.plf_generic(S, CAT, e1, e2, EV, left, right, w, fma=True)
+    t = [dev(a) for a in (x1, x2, EV, left, right, w)]
+    for rep in range(3):
+        x3 = torch.full((V * n,), float("nan"), dtype=torch.float64, device="cuda")
+        sc = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        s = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+        if kind == "dense":
+            ctx.plf_dev_gen(t[0], t[1], x3, t[2], t[3], t[4], S, t[5], sc, s, n=n, fma=True)
+        else:
+            kw = dict(x1=t[0]) if kind == "tip2" else dict(tip1=dev(c1))
+            kw.update(x2=t[1]) if kind == "tip1" else kw.update(tip2=dev(c2))
+            ctx.plf_tips_dev(x3, t[2], n, t[3], t[4], wgt=t[5], scaler=sc, scaler_sum=s, states=S,
+                             fma=True, **kw)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(x3.cpu().numpy()), bits(f3)), rep
+        assert np.array_equal(sc.cpu().numpy(), fsc) and int(s.item()) == finc, rep
+
+
+def test_protein_f64_fma_tile_queue_full_grid(ctx, oracle):
+    """2^20 + 37 sites at the default grid (512 blocks: 32 tiles per block and
+    more, the queue path) and then 2^18 (the fixed stride) on the same stream:
+    bit-identical to the oracle's fused restatement, sums exact."""
+    for n in ((1 << 20) + 37, 1 << 18):
+        x1, x2, EV, left, right, w = gen(n, np.float64, 1234 + n)
+        x3, sc, s = run(ctx, x1, x2, EV, left, right, w, n, fma=True)
+        f3, fsc, finc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
+        assert np.array_equal(bits(x3), bits(f3))
+        assert np.array_equal(sc, fsc) and s == finc and fsc.sum() > 0
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_protein_traverse_exact(ctx, oracle, dtype):
     """Protein traversal (states=20, one launch per node): CLVs, scaler bytes
