@@ -1150,6 +1150,60 @@ __device__ constexpr int deep_off(int l) {
   return o;
 }
 
+// Wave-level chunk queue of the deep passes (kDyn).  Their waves run the
+// grid stride independently (no block barriers), and with a fixed stride the
+// launch ends when the slowest wave ends: a per-wave timeline of the 2^20-site
+// six-level pass (tools/tune_deep_dyn.hip) shows wave exits from 2.61 to
+// 3.36 ms.  Chunk = one wave trip (8U f64 / 16U f32 sites); trip 0 takes
+// chunk `wave`, trip 1 W + wave (W = waves in the grid), trip i >= 2 2W + d,
+// d from a returning atomic add on the head word that lane 0 issues in trip
+// i - 2 (after that trip's first leaf loads) and the wave reads at the end of
+// that trip.  The head address carries an offset laundered through an empty
+// asm (a VGPR 0): the compiler's atomic optimizer then leaves the single-lane
+// add alone (with a uniform address it aggregates lanes and waits for the
+// result at once) and the address stays global.  Words: region
+// kDeepQueueRegion of the stream workspace ([0] head, [16] exit count); the
+// last wave out zeroes both for the next launch, after every wave's last
+// dequeue has returned (its exit add depends on the value).
+constexpr int kDeepQueueRegion = 63;
+struct WaveQueue {
+  unsigned long long *head, *done;
+  int64_t W, nch, chunk;
+  long long pend = 0;  // lane 0: the dequeued chunk offset for trip i + 2
+  bool dyn;
+  __device__ WaveQueue(unsigned long long *ws, int64_t n, int64_t chunk_sites, int waves_per_block, bool on) {
+    int zero = 0;
+    if (on) asm volatile("" : "+v"(zero));
+    head = ws + (size_t)kDeepQueueRegion * kWsWords + zero;
+    done = ws + (size_t)kDeepQueueRegion * kWsWords + 16;
+    chunk = chunk_sites;
+    W = (int64_t)gridDim.x * waves_per_block;
+    nch = (n + chunk_sites - 1) / chunk_sites;
+    dyn = on && nch > 2 * W;
+  }
+  __device__ __forceinline__ void dequeue() {
+    if (dyn && (threadIdx.x & 63) == 0)
+      pend = (long long)__hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // base of trip i + 2, at the end of trip i (n: none)
+  __device__ __forceinline__ int64_t after(int64_t n) const {
+    if (!dyn) return n;
+    const long long d = (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)pend) |
+                        ((long long)__builtin_amdgcn_readfirstlane((int)(pend >> 32)) << 32);
+    const int64_t b = (2 * W + d) * chunk;
+    return b < n ? b : n;
+  }
+  __device__ __forceinline__ void finish() const {
+    if ((threadIdx.x & 63) != 0) return;
+    const unsigned long long later = (unsigned long long)(pend >> 62);  // 0, once it returned
+    const unsigned long long d = __hip_atomic_fetch_add(done, 1ull + later, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (unsigned long long)W - 1) {
+      __hip_atomic_store(head, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+};
+
 struct DeepDesc {
   const void *g[64];
   void *x[63];
@@ -1158,7 +1212,7 @@ struct DeepDesc {
   int64_t *ss[63];
 };
 
-template <int D, bool kSum, bool NTL, int U, int kThreads, int kTips = 0>
+template <int D, bool kSum, bool NTL, int U, int kThreads, int kTips = 0, bool kDyn = false>
 __global__ void __launch_bounds__(kThreads, 1)
 plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
                         const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
@@ -1200,7 +1254,9 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
   const double m = Num<double>::minlik();
   const int64_t wave = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const int64_t stride = (int64_t)gridDim.x * kWaves * 8 * U;
-  for (int64_t base = wave * 8 * U; base < n; base += stride) {
+  WaveQueue wq(ws, n, 8 * U, kWaves, kDyn);
+  int64_t nbase = wave * 8 * U + stride;  // kDyn: the base of the next trip
+  for (int64_t base = wave * 8 * U; base < n;) {
     int z = 0;
     asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keep the matrix reads inside the loop
     const double *mz = &mats[0][0] + z;
@@ -1264,6 +1320,7 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
           }
         }
       }
+      if (kDyn && q == 0) wq.dequeue();
       f64x2 a1[4][U], a2[2][U], r[U];
 #pragma unroll
       for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i], k8[2 * i], k8[2 * i + 1]);
@@ -1285,7 +1342,14 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
         for (int j = 0; j < U; j++) r[j] = up[j];
       }
     }
+    if constexpr (kDyn) {
+      base = nbase;
+      nbase = wq.after(n);
+    } else {
+      base += stride;
+    }
   }
+  if constexpr (kDyn) wq.finish();
   if constexpr (kSum) {
     __syncthreads();
     if (threadIdx.x < kNodes)
@@ -1298,7 +1362,7 @@ plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
 // category's 32 matrix values per node from the LDS copy (31.5 KB f32).
 // kTips = 2: every leaf a tip, as the f64 pass (2^D per-child tables of 256
 // values, 64 KiB f32 at D = 6, beside the upper levels' 15.5 KiB of matrices).
-template <int D, typename T, bool kSum, bool NT, int U, int kThreads, int kTips = 0>
+template <int D, typename T, bool kSum, bool NT, int U, int kThreads, int kTips = 0, bool kDyn = false>
 __global__ void __launch_bounds__(kThreads, 1)
 plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
                         const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
@@ -1338,7 +1402,9 @@ plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
   const T m = Num<T>::minlik();
   const int64_t wave = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const int64_t stride = (int64_t)gridDim.x * kWaves * 16 * U;
-  for (int64_t base = wave * 16 * U; base < n; base += stride) {
+  WaveQueue wq(ws, n, 16 * U, kWaves, kDyn);
+  int64_t nbase = wave * 16 * U + stride;  // kDyn: the base of the next trip
+  for (int64_t base = wave * 16 * U; base < n;) {
     int z = 0;
     asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keep the matrix reads inside the loop
     const T *mz = mats + z;
@@ -1409,6 +1475,7 @@ plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
           }
         }
       }
+      if (kDyn && q == 0) wq.dequeue();
       T a1[4][U][4], a2[2][U][4], r[U][4];
 #pragma unroll
       for (int i = 0; i < 4; i++) node_eval(4 * q + i, v[2 * i], v[2 * i + 1], a1[i], k8[2 * i], k8[2 * i + 1]);
@@ -1434,7 +1501,14 @@ plf_dna_cat_deep_kernel(const DeepDesc d, const T *__restrict__ EV,
         keep(r, up);
       }
     }
+    if constexpr (kDyn) {
+      base = nbase;
+      nbase = wq.after(n);
+    } else {
+      base += stride;
+    }
   }
+  if constexpr (kDyn) wq.finish();
   if constexpr (kSum) {
     __syncthreads();
     if (threadIdx.x < kNodes)

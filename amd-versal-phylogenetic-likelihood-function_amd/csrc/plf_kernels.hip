@@ -15,7 +15,6 @@
 // blocks over the batch's nodes (blockIdx.y = node).
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 
 #include <algorithm>
 #include <cstdint>
@@ -38,6 +37,7 @@ static_assert(sizeof(TripleDescH) == sizeof(dev::TripleDesc), "triple descriptor
 static_assert(kMaxTriples == dev::kMaxTriples && 3 * kMaxTriples <= kMaxBatch, "triple batch size");
 static_assert(sizeof(SeptetDescH) == sizeof(dev::SeptetDesc), "septet descriptor mismatch");
 static_assert(kMaxSeptets == dev::kMaxSeptets, "septet batch size");
+static_assert(kDeepQueueRegion == dev::kDeepQueueRegion, "deep queue region");
 static_assert(sizeof(DeepDescH) == sizeof(dev::DeepDesc), "deep descriptor mismatch");
 
 // Tuned on MI355X (tools/tune_plf.hip, profiles/r01_tune.log):
@@ -320,15 +320,14 @@ hipError_t launch_septets32_t(const dev::SeptetBatch &b, int count, const float 
 // fused six-level subtrees: 512-thread blocks (one LDS copy of the 63 nodes'
 // matrices per 8 waves), 2 x 8-site blocks per trip, grid = co-resident blocks
 // (tools/gpu_deep.sh, profiles/r01_deep.log)
-template <int D, typename T, bool kSum, int U, int kThreads, int kTips = 0>
-hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt, int64_t n,
-                         unsigned long long *ws, int max_blocks, hipStream_t s,
-                         const T *tipvec = nullptr) {
+template <int D, typename T, bool kSum, int U, int kThreads, int kTips, bool kDyn>
+hipError_t launch_deep_k(const dev::DeepDesc &d, const T *EV, const int32_t *wgt, int64_t n,
+                         unsigned long long *ws, int max_blocks, hipStream_t s, const T *tipvec) {
   static int resident = 0;
   // f64: lane pairs, 8 sites per wave instruction; f32: lane = category, 16
   auto kernel = [] {
-    if constexpr (sizeof(T) == 8) return &dev::plf_dna_f64_deep_kernel<D, kSum, kNtl64, U, kThreads, kTips>;
-    else return &dev::plf_dna_cat_deep_kernel<D, T, kSum, kNt, U, kThreads, kTips>;
+    if constexpr (sizeof(T) == 8) return &dev::plf_dna_f64_deep_kernel<D, kSum, kNtl64, U, kThreads, kTips, kDyn>;
+    else return &dev::plf_dna_cat_deep_kernel<D, T, kSum, kNt, U, kThreads, kTips, kDyn>;
   }();
   constexpr int kSitesPerWave = sizeof(T) == 8 ? 8 : 16;
   if (!resident) {
@@ -347,6 +346,19 @@ hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt
   gx = std::max<int64_t>(1, std::min<int64_t>(gx, max_blocks > 0 ? max_blocks : resident));
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kThreads), 0, s, d, EV, wgt, n, ws, tipvec);
   return hipGetLastError();
+}
+
+template <int D, typename T, bool kSum, int U, int kThreads, int kTips = 0>
+hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt, int64_t n,
+                         unsigned long long *ws, int max_blocks, hipStream_t s,
+                         const T *tipvec = nullptr) {
+  // chunks from the wave-level queue (plf_dna.hpp WaveQueue) whenever there is
+  // a workspace: the fixed stride left wave exits spread over 2.61-3.36 ms of a
+  // 2^20-site f64 pass (same process: 3358 -> 3116 us,
+  // profiles/r03_tune_deep_dyn.log; bench tree64 f64 --tips 1688 -> 1643 us,
+  // f32 --tips 875 -> 861, f32 dense equal, profiles/r03_ab_deep_dyn.log)
+  if (ws) return launch_deep_k<D, T, kSum, U, kThreads, kTips, true>(d, EV, wgt, n, ws, max_blocks, s, tipvec);
+  return launch_deep_k<D, T, kSum, U, kThreads, kTips, false>(d, EV, wgt, n, ws, max_blocks, s, tipvec);
 }
 
 }  // namespace

@@ -104,6 +104,8 @@ struct DeepDescH {
   int64_t *ss[63];
 };
 constexpr int kDeepNodes = 63;
+// the deep passes' chunk queue: this region of the stream workspace (plf_dna.hpp WaveQueue)
+constexpr int kDeepQueueRegion = 63;
 hipError_t launch_plf_dna_deep(int dtype, int depth, const DeepDescH *t, const void *EV,
                                const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
                                hipStream_t s, int tips = 0, const void *tipvec = nullptr);

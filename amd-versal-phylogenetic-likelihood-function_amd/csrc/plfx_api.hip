@@ -90,7 +90,7 @@ struct DeviceGuard {
   DeviceGuard plfx_guard_((ctx)->device)
 
 constexpr size_t kWsRegions = std::max({(size_t)plfx::kMaxBatch, (size_t)7 * plfx::kMaxSeptets,
-                                        (size_t)plfx::kDeepNodes});
+                                        (size_t)plfx::kDeepNodes, (size_t)plfx::kDeepQueueRegion + 1});
 constexpr size_t kWsBytes = kWsRegions * plfx::kWsWords * sizeof(unsigned long long);
 constexpr size_t kLnlPartialBytes = plfx::kLnlMaxGrid * sizeof(double);
 constexpr size_t kLnlTicketBytes = plfx::kWsWords * sizeof(unsigned long long);

@@ -350,6 +350,57 @@ def test_six_level_pass_tiny_alignments(oracle, n, dtype, coded, monkeypatch):
         assert (got[n:] == 7).all(), j
 
 
+@pytest.mark.parametrize("dtype,coded", [(np.float64, False), (np.float32, False), (np.float64, True),
+                                         (np.float32, True)])
+def test_six_level_pass_chunk_queue(oracle, dtype, coded, monkeypatch):
+    """The deep passes' wave-level chunk queue (plf_dna.hpp WaveQueue): one
+    512-thread block (PLFX_MAX_BLOCKS=1: 8 waves) over 4099 sites -- dozens of
+    dequeued chunks per wave, a ragged last one -- and the whole sweep twice
+    on the same stream (the queue words reset themselves): CLVs, scaler bytes
+    and sums bit-identical to the oracle both times."""
+    import plfx
+    import torch
+
+    n = 4099
+    rng = np.random.default_rng(4242)
+    ntax = 64
+    ops = np.array(oracle.balanced_tree_ops(ntax), np.int32)
+    nslots, nops = 2 * ntax - 1, ops.shape[0]
+    dense = [rng.random(16 * n).astype(dtype) for _ in range(ntax)]
+    dense[0][::3] *= 1e-30 if dtype == np.float64 else 1e-20
+    codes = [oracle.random_tip_codes(rng, n, 0.2) for _ in range(ntax)]
+    pm = (rng.random(nops * 128) * 0.3).astype(dtype)
+    if coded:
+        pm[:128] *= 1e-30
+    EV = (rng.random(16) * 0.3).astype(dtype)
+    wgt = rng.integers(1, 5, n).astype(np.int32)
+    leaves = [oracle.expand_tips(codes[t], dtype) for t in range(ntax)] if coded else dense
+    host = [d.copy() for d in leaves] + [np.zeros(16 * n, dtype) for _ in range(nslots - ntax)]
+    esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
+    monkeypatch.setenv("PLFX_FUSE", "3")
+    monkeypatch.setenv("PLFX_MAX_BLOCKS", "1")
+    c = plfx.Context(0)
+    try:
+        tt = torch.float64 if dtype == np.float64 else torch.float32
+        for rep in range(2):
+            clv = [None if coded else dev(d) for d in dense] + [torch.full((16 * n,), float("nan"), dtype=tt,
+                                                                         device="cuda")
+                                                              for _ in range(nslots - ntax)]
+            tips = [dev(codes[t]) for t in range(ntax)] + [None] * (nslots - ntax) if coded else None
+            sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
+            scal = [torch.full((n,), 7, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+            c.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips)
+            torch.cuda.synchronize()
+            assert c.last_schedule()["deep6"] == 1
+            for s_ in range(ntax, nslots):
+                assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), (rep, s_)
+            assert np.array_equal(sums.cpu().numpy(), esums), rep
+            for j in range(nops):
+                assert np.array_equal(scal[j].cpu().numpy(), escal[j]), (rep, j)
+    finally:
+        c.close()
+
+
 def _balanced_ops(tips, slot, pmat):
     """Level-order ops of a balanced subtree over `tips` (a power of two)."""
     ops, level = [], list(tips)
