@@ -68,6 +68,11 @@
  * still holds a workspace it waits for the whole device (hipDeviceSynchronize,
  * which must not overlap a global-mode capture in another thread), so release
  * streams first to keep destroy local.
+ * The same workspace also holds the tile/chunk queues of the protein f64 FMA
+ * kernel (from 2^20 sites) and of the fused six-level tree passes: blocks or
+ * waves that run ahead take more of the alignment instead of a fixed share
+ * (every site is computed the same way, so results do not change); the queue
+ * words, like the sums, reset themselves at the end of each launch.
  * The reduction encodes arrival counts next to the sums and needs
  * sum_j |wgt[j]| < 2^40 per launch (the reference's own scalerIncrement is a
  * 32-bit int); the host entry points check this, the device entry points

@@ -82,16 +82,12 @@ int main(int argc, char **argv) {
   const int sel = argc > 3 ? atoi(argv[3]) : 0;
   if (sel == 0 || sel == 1 || sel == 3) {
     add("product static", 0, &plf_prot_mfma_kernel<true, 2, 0, false>, 64);
+    add("split 17/32 to the first-dispatched half", 0, &plf_prot_mfma_split_kernel<true, 2, 0, 17, 32>, 64);
+    add("split 9/16", 0, &plf_prot_mfma_split_kernel<true, 2, 0, 9, 16>, 64);
+    add("split 1/2 (= static order per half)", 0, &plf_prot_mfma_split_kernel<true, 2, 0, 1, 2>, 64);
     add("product kDyn", 0, &plf_prot_mfma_kernel<true, 2, 0, true>, 64);
-    adds("tune copy: dyn (one head)", 0, &plf_prot_mfma_dyn_kernel<true, 2, 0>, 64);
     add("product static again", 0, &plf_prot_mfma_kernel<true, 2, 0, false>, 64);
-    add("product kDyn again", 0, &plf_prot_mfma_kernel<true, 2, 0, true>, 64);
-  }
-  if (sel == 0 || sel == 2 || sel == 3) {
-    add("product static tip/inner", 1, &plf_prot_mfma_kernel<true, 2, 1, false>, 64);
-    add("product kDyn tip/inner", 1, &plf_prot_mfma_kernel<true, 2, 1, true>, 64);
-    add("product static tip/tip", 2, &plf_prot_mfma_kernel<true, 2, 2, false>, 64);
-    add("product kDyn tip/tip", 2, &plf_prot_mfma_kernel<true, 2, 2, true>, 64);
+    add("split 17/32 again", 0, &plf_prot_mfma_split_kernel<true, 2, 0, 17, 32>, 64);
   }
   std::vector<uint64_t> ref[3], got(n * 80);
   std::vector<uint8_t> rsc[3], gsc(n);
