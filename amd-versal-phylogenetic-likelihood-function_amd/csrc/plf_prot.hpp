@@ -322,6 +322,12 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
             *mE = mats + off + oE / E;
     T U[S];
     const int64_t sq = base + lane < n ? base + lane : n - 1;
+    // the site weight up front, unconditionally (wgt_at, plf_dna.hpp): loaded
+    // inside the scaled-site branch, its wait also drained the next child tile
+    // in flight (2^18: f64 142.2 -> 138.9 us, f32 76.5 -> 74.6 us; the FMA
+    // kernels ran 1-2 % slower this way and keep the branch load,
+    // tools/tune_prot_wgt.hip, profiles/r03_tune_protein_wgt.log)
+    const int wsite = kSum ? wgt_at(wgt, sq, ws) : 0;
     // stage a dense child's tile from the prefetch registers, then fetch the
     // next tile in the sequence
     auto stage = [&](const T *next, int64_t nbase) {
@@ -418,7 +424,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
     const int64_t site = base + lane;
     if (site < n && c == 0) {
       if (scaler) scaler[site] = (uint8_t)sc;
-      if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
+      if (kSum && sc) acc += wsite;
     }
     __syncthreads();
     tile_store<T>(x3, base, n, tile);
