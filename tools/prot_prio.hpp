@@ -164,6 +164,10 @@ plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restric
         if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
       }
     }
+    // kMode 4: every wave waits for its loads in flight (the next tile) before
+    // its share of the store pass (the product: wave 0 only, through the wait
+    // of its weight load)
+    if constexpr (kMode == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // coalesced store with the rescale of the scaled sites (exact: x 2^32)
     {
       f64x2 *dst = reinterpret_cast<f64x2 *>(x3 + base * 80);
@@ -194,7 +198,8 @@ plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restric
     // wave priority (s_setprio) by trip: the SIMD's arbiter favours the older
     // waves, i.e. the first-dispatched block of each CU (blockIdx < G/2);
     // kMode 1: the younger block at priority 1 for its first kH trips;
-    // 2: the younger block at 1 throughout; 3: leadership alternating by trip
+    // 2: the younger block at 1 throughout; 3: leadership alternating by trip;
+    // 4: no priorities, every wave drains its loads before the store pass
     const bool young = blockIdx.x >= (gridDim.x + 1) / 2;
     int i = 0;
     for (int64_t b = (int64_t)blockIdx.x * 64; b < n; b += stride, i++) {
@@ -202,13 +207,13 @@ plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restric
       if constexpr (kMode == 1) hi = young && i < kH;
       if constexpr (kMode == 2) hi = young;
       if constexpr (kMode == 3) hi = young == ((i & 1) == 0);
-      if constexpr (kMode != 0) {
+      if constexpr (kMode >= 1 && kMode <= 3) {
         if (hi) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
       }
       trip(b, b + stride < n ? b + stride : n);
     }
-    if constexpr (kMode != 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (kMode >= 1 && kMode <= 3) __builtin_amdgcn_s_setprio(0);
   }
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }

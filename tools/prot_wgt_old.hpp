@@ -215,7 +215,7 @@ plf_prot_lds_old_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *_
                                               scaler_sum, tipvec);
 }
 
-template <bool kSum, int kMinWaves, int kTips>
+template <bool kSum, int kMinWaves, int kTips, int kWaitAll = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma32_old_kernel(const float *__restrict__ x1, const float *__restrict__ x2,
                        float *__restrict__ x3, const float *__restrict__ EV,
@@ -418,6 +418,9 @@ plf_prot_mfma32_old_kernel(const float *__restrict__ x1, const float *__restrict
         if (kSum && sc) acc += wgt ? (long long)wgt[site] : 1ll;
       }
     }
+    // kWaitAll: every wave waits for its loads in flight before its share of
+    // the store pass (the product: wave 0 only, through its weight load)
+    if constexpr (kWaitAll == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // coalesced store with the rescale of the scaled sites (exact: x 2^32)
     {
       f32x4 *dst = reinterpret_cast<f32x4 *>(x3 + base * 80);

@@ -11,7 +11,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //     -I amd-versal-phylogenetic-likelihood-function_amd/csrc -I tools tools/tune_prot_wgt.hip -o build/tune_prot_wgt
-//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32]
+//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32, 3 FMA: all waves wait before the stores]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -152,6 +152,20 @@ int main(int argc, char **argv) {
     b.add("f32 exact product", 1, &plf_prot_lds_kernel<float, true, 2, 0, 4, false>);
     b.add("f32 exact old", 1, &plf_prot_lds_old_kernel<float, true, 2, 0, 4, false>);
     failures += b.run(reps, 5, "f32");
+  }
+  if (sel == 3) {  // every wave drains its loads in flight before the store pass
+    Bench<double> b(n);
+    b.add("f64 FMA product (wave 0 waits)", 0, &plf_prot_mfma_kernel<true, 2, 0, false>);
+    b.add("f64 FMA all waves wait", 0, &plf_prot_mfma_prio_kernel<true, 2, 0, 4, 0>);
+    b.add("f64 FMA product again", 0, &plf_prot_mfma_kernel<true, 2, 0, false>);
+    b.add("f64 FMA all waves wait again", 0, &plf_prot_mfma_prio_kernel<true, 2, 0, 4, 0>);
+    failures += b.run(reps, 5, "f64");
+    Bench<float> c(n);
+    c.add("f32 FMA product (wave 0 waits)", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
+    c.add("f32 FMA all waves wait", 0, &plf_prot_mfma32_old_kernel<true, 3, 0, 1>);
+    c.add("f32 FMA product again", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
+    c.add("f32 FMA all waves wait again", 0, &plf_prot_mfma32_old_kernel<true, 3, 0, 1>);
+    failures += c.run(reps, 5, "f32");
   }
   return failures ? 1 : 0;
 }
