@@ -11,7 +11,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //     -I amd-versal-phylogenetic-likelihood-function_amd/csrc -I tools tools/tune_prot_wgt.hip -o build/tune_prot_wgt
-//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32, 3 FMA: all waves wait before the stores]
+//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32, 3 FMA: all waves wait before the stores, 4 f32 LDS-DMA tiles]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,6 +22,7 @@
 
 #include "prot_prio.hpp"
 #include "prot_wgt_old.hpp"
+#include "prot_dma32.hpp"
 
 using namespace plfx::dev;
 
@@ -165,6 +166,15 @@ int main(int argc, char **argv) {
     c.add("f32 FMA all waves wait", 0, &plf_prot_mfma32_old_kernel<true, 3, 0, 1>);
     c.add("f32 FMA product again", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
     c.add("f32 FMA all waves wait again", 0, &plf_prot_mfma32_old_kernel<true, 3, 0, 1>);
+    failures += c.run(reps, 5, "f32");
+  }
+  if (sel == 4) {  // f32 FMA: child tiles by LDS-DMA (tools/prot_dma32.hpp)
+    Bench<float> c(n);
+    c.add("f32 FMA product", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
+    c.add("f32 FMA LDS-DMA tiles, 3 blocks/CU", 0, &plf_prot_mfma32d_kernel<true, 3>);
+    c.add("f32 FMA LDS-DMA tiles, 4 blocks/CU", 0, &plf_prot_mfma32d_kernel<true, 4>);
+    c.add("f32 FMA product again", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
+    c.add("f32 FMA LDS-DMA tiles, 3 blocks/CU again", 0, &plf_prot_mfma32d_kernel<true, 3>);
     failures += c.run(reps, 5, "f32");
   }
   return failures ? 1 : 0;
