@@ -408,7 +408,7 @@ __device__ __forceinline__ void pin_chains(T (&u)[R]) {
 // Bit-identical; within the run-to-run spread of the LDS form on two boxes
 // (profiles/r02_tune_protein_exact_sgpr.log), so the product keeps the LDS form.
 template <typename T, bool kFma, bool kSum, int kTips, int kRows, bool kPf, bool kPack,
-          bool kE3S = false, int kPS = 0>
+          bool kE3S = false, int kPS = 0, bool kNoMats = false>
 __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T *__restrict__ x2,
                                               T *__restrict__ x3, const T *__restrict__ EV,
                                               const T *__restrict__ left, const T *__restrict__ right,
@@ -443,8 +443,10 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
   // P_L[4][400] (unless x1 is a tip) | P_R[4][400] (unless x2 is a tip) | EV[400]
   // in T elements; a tip child's matrix lives in its table instead
   constexpr int oR = T1 ? 0 : 4 * S * S, oE = oR + (T2 ? 0 : 4 * S * S);
-  __shared__ V mats[(oE + S * S) / E];
-  {
+  // kNoMats (with kPS = 3 and kE3S: every matrix as SGPR operands): no LDS copy,
+  // so the block's LDS is the tile alone and three blocks fit a CU
+  __shared__ V mats[kNoMats ? 1 : (oE + S * S) / E];
+  if constexpr (!kNoMats) {
     T *md = reinterpret_cast<T *>(mats);
     for (int i = threadIdx.x; i < 4 * S * S; i += kBlock) {  // P[c][k][l] -> [c][k/kRows][l][k%kRows]
       const int cc = i / (S * S), r = i - cc * S * S, k = r / S, l = r - k * S;
@@ -466,7 +468,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
     int o = 0;
     T tok = T(0);
     if constexpr (kPS != 0 && !kFma && !kPacked) {
-      if (gsrc) {
+      if (kNoMats || gsrc) {
 #pragma unroll
         for (int gk = 0; gk < S / kRows; gk++) {
           const T *gp = gsrc + gk * S * kRows;
@@ -499,6 +501,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
         return;
       }
     }
+    if constexpr (kNoMats) return;
 #pragma unroll
     for (int gk = 0; gk < S / kRows; gk++) {
       const V *G = M + gk * S * RV;
@@ -630,6 +633,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
 #pragma unroll
         for (int q = 0; q < (kPacked ? kPh3 / 2 : 1); q++) v2[q] = f32x2{0.f, 0.f};
         asm volatile("" : "+v"(o) : "v"(tok));
+        if constexpr (!kNoMats)
 #pragma unroll
         for (int k = 0; k < 2; k++)
 #pragma unroll
@@ -637,7 +641,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
 #pragma unroll
         for (int k = 0; k < S; k++) {
           asm volatile("" : "+v"(o) : "v"(tok));
-          if (k + 2 < S) {
+          if (!kNoMats && k + 2 < S) {
 #pragma unroll
             for (int j = 0; j < PV; j++) ring[(k + 2) % 3][j] = G[o + (S / E) * (k + 2) + j];
           }
@@ -757,6 +761,21 @@ plf_prot_exact64_kernel(const double *__restrict__ x1, const double *__restrict_
                         const double *__restrict__ pr_t) {
   prot_lds_body<double, false, kSum, kTips, 10, true, false, true, 2>(
       x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum, tipvec, nullptr, pr_t);
+}
+
+// Tuning form of the exact f64 kernel with EVERY matrix as SGPR operands (kPS =
+// 3 from the group-transposed copies pl_t / pr_t, kE3S for EV) and no LDS copy
+// of the matrices (kNoMats), so up to three blocks fit a CU (LDS = the tile).
+template <bool kSum, int kMinWaves, bool kPf>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_exact_sgpr_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                           double *__restrict__ x3, const double *__restrict__ EV,
+                           const double *__restrict__ left, const double *__restrict__ right,
+                           const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                           unsigned long long *ws, int64_t *scaler_sum, const double *__restrict__ pl_t,
+                           const double *__restrict__ pr_t) {
+  prot_lds_body<double, false, kSum, 0, 10, kPf, false, true, 3, true>(
+      x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum, nullptr, pl_t, pr_t);
 }
 
 // The group-transposed copy of a 4-category S = 20 matrix for kPS:
