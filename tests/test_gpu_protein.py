@@ -97,6 +97,21 @@ def test_protein_f32_many_trips(ctx, oracle, fma):
     assert np.array_equal(sc, esc) and s == einc and esc.sum() > 0
 
 
+@pytest.mark.parametrize("fma", [False, True])
+def test_protein_f64_many_trips(ctx, oracle, fma):
+    """f64 at 3 x 2^16 + 5 sites (six trips per block at the co-resident grid,
+    the last tile ragged; weights 0..3): the exact kernel loads each site's
+    weight at the top of the trip (plf_prot.hpp prot_lds_body), the FMA kernel
+    inside the scaled-site branch -- both give plf()'s (resp. the fma
+    restatement's) CLVs bit for bit and the exact weighted scaler sum."""
+    n = 3 * (1 << 16) + 5
+    x1, x2, EV, left, right, w = gen(n, np.float64, 78)
+    x3, sc, s = run(ctx, x1, x2, EV, left, right, w, n, fma=fma)
+    e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=fma)
+    assert np.array_equal(bits(x3), bits(e3))
+    assert np.array_equal(sc, esc) and s == einc and esc.sum() > 0
+
+
 def test_protein_full_size_256k(ctx, oracle):
     """BASELINE configs[4]: 2^18 sites, f64, bit-exact (EXACT mode), lnL."""
     import torch
