@@ -12,6 +12,36 @@
 namespace plfx {
 namespace dev {
 
+// kMode 5: the first trip's x1 tile by LDS-DMA straight into the padded tile
+// (slot j of the 64 x 41 layout <- chunk (j / 41, min(j % 41, 39)): the pad
+// slots get a harmless copy), issued at kernel start together with the
+// register fetch of the first x2 tile, so the first trip waits for one load
+// latency instead of two in series.
+__device__ __forceinline__ void glds16_prio(const void *src, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_byte)
+               : "memory");
+}
+__device__ __forceinline__ void tile_dma_padded64(const double *__restrict__ g, int64_t base, int64_t n,
+                                                  unsigned tile_byte) {
+  using PT = ProtTile<double>;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int kSlots = 64 * PT::kStride;  // 2624
+#pragma unroll
+  for (int i = 0; i < (kSlots + kBlock - 1) / kBlock; i++) {
+    const int j0 = i * kBlock + wv * 64;  // the wave's first slot (wave-uniform)
+    if (j0 >= kSlots) break;
+    const int j = j0 + (threadIdx.x & 63);
+    const int jj = j < kSlots ? j : kSlots - 1;
+    const int s = jj / PT::kStride, q0 = jj - s * PT::kStride;
+    const int q = q0 < PT::kChunksPerSite ? q0 : PT::kChunksPerSite - 1;
+    const int64_t site = base + s < n ? base + s : n - 1;
+    glds16_prio(reinterpret_cast<const f64x2 *>(g + site * 80) + q, tile_byte + (unsigned)j0 * 16u);
+  }
+}
+
 template <bool kSum, int kMinWaves, int kTips, int kMode, int kH>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
@@ -32,7 +62,13 @@ plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restric
   const int lo16 = lane & 15, g = lane >> 4;
   f64x2 pf[K];
   const int64_t stride = (int64_t)gridDim.x * 64;
-  if constexpr (!T2)  // the first dense child's first tile, before the matrix fragments
+  __shared__ f64x2 tile[64 * ProtTile<double>::kStride];
+  if constexpr (kMode == 5 && kTips == 0) {
+    if ((int64_t)blockIdx.x * 64 < n) {
+      tile_dma_padded64(x1, (int64_t)blockIdx.x * 64, n, (unsigned)(uintptr_t)tile);
+      tile_fetch<double>(x2, (int64_t)blockIdx.x * 64, n, pf);
+    }
+  } else if constexpr (!T2)  // the first dense child's first tile, before the matrix fragments
     if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
   // A fragments: [0][s] -> lane holds M[row = lo16][col = 4s + g];
   // [1][s] -> M[row = 16 + lane%4][col = 4s + g] (the 4x4x4_4b form)
@@ -59,8 +95,6 @@ plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restric
     u0 = f64x4{r[g], r[g + 4], r[g + 8], r[g + 12]};
     u1 = f64x4{r[16 + g], 0.0, 0.0, 0.0};
   };
-  // kDyn: tiles handed out by a device-wide dequeue (prot_queue below)
-  __shared__ f64x2 tile[64 * PT::kStride];
   __shared__ unsigned long long small_mask[kWavesPerBlock];
   const double *td = reinterpret_cast<const double *>(tile);
   double *tw = reinterpret_cast<double *>(tile);
@@ -70,7 +104,7 @@ plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restric
 #pragma unroll
     for (int st = 0; st < 5; st++) bv[st] = xr[4 * st];
   };
-  auto trip = [&](const int64_t base, const int64_t nb) -> int64_t {
+  auto trip = [&](const int64_t base, const int64_t nb, bool first) -> int64_t {
     int64_t next = nb;
     f64x4 P[4][2];  // per sub-tile: U_L^T, then p = U_L^T * U_R^T
     const int64_t sq = base + lane < n ? base + lane : n - 1;
@@ -80,9 +114,14 @@ plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restric
 #pragma unroll
       for (int t = 0; t < 4; t++) tip_u(tabs[0], code1, t, P[t][0], P[t][1]);
     } else {
-      tile_put<double>(tile, pf);
-      __syncthreads();
-      tile_fetch<double>(x2, base, n, pf);
+      if (kMode == 5 && first) {  // x1 landed in the tile by DMA, x2 in flight in pf
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      } else {
+        tile_put<double>(tile, pf);
+        __syncthreads();
+        tile_fetch<double>(x2, base, n, pf);
+      }
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         double bv[5];
@@ -199,7 +238,8 @@ plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restric
     // waves, i.e. the first-dispatched block of each CU (blockIdx < G/2);
     // kMode 1: the younger block at priority 1 for its first kH trips;
     // 2: the younger block at 1 throughout; 3: leadership alternating by trip;
-    // 4: no priorities, every wave drains its loads before the store pass
+    // 4: no priorities, every wave drains its loads before the store pass;
+    // 5: the first trip's x1 by LDS-DMA beside the first x2 fetch (above)
     const bool young = blockIdx.x >= (gridDim.x + 1) / 2;
     int i = 0;
     for (int64_t b = (int64_t)blockIdx.x * 64; b < n; b += stride, i++) {
@@ -211,7 +251,7 @@ plf_prot_mfma_prio_kernel(const double *__restrict__ x1, const double *__restric
         if (hi) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
       }
-      trip(b, b + stride < n ? b + stride : n);
+      trip(b, b + stride < n ? b + stride : n, i == 0);
     }
     if constexpr (kMode >= 1 && kMode <= 3) __builtin_amdgcn_s_setprio(0);
   }

@@ -11,7 +11,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //     -I amd-versal-phylogenetic-likelihood-function_amd/csrc -I tools tools/tune_prot_wgt.hip -o build/tune_prot_wgt
-//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32, 3 FMA: all waves wait before the stores, 4 f32 LDS-DMA tiles]
+//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32, 3 FMA: all waves wait before the stores, 4 f32 LDS-DMA tiles, 5 f64 first tile by DMA]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -176,6 +176,14 @@ int main(int argc, char **argv) {
     c.add("f32 FMA product again", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
     c.add("f32 FMA LDS-DMA tiles, 3 blocks/CU again", 0, &plf_prot_mfma32d_kernel<true, 3>);
     failures += c.run(reps, 5, "f32");
+  }
+  if (sel == 5) {  // f64 FMA: the first trip's x1 by LDS-DMA (tools/prot_prio.hpp kMode 5)
+    Bench<double> b(n);
+    b.add("f64 FMA product", 0, &plf_prot_mfma_kernel<true, 2, 0, false>);
+    b.add("f64 FMA first x1 by DMA + x2 at start", 0, &plf_prot_mfma_prio_kernel<true, 2, 0, 5, 0>);
+    b.add("f64 FMA product again", 0, &plf_prot_mfma_kernel<true, 2, 0, false>);
+    b.add("f64 FMA first x1 by DMA again", 0, &plf_prot_mfma_prio_kernel<true, 2, 0, 5, 0>);
+    failures += b.run(reps, 5, "f64");
   }
   return failures ? 1 : 0;
 }
