@@ -466,6 +466,66 @@ hipError_t launch_plf_dna_triples(int dtype, const TripleDescH *t, int count, co
   }
 }
 
+// Protein batches: grid (resident blocks, count) -- every node gets the grid a
+// one-node launch would (the kernels keep their one-node grid stride) and the
+// nodes' blocks follow each other through the co-resident slots.
+template <typename K, typename TT>
+hipError_t launch_prot_batch_k(K kernel, int &cache, const dev::NodeBatch &b, int count, const TT *EV,
+                               const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                               hipStream_t s, const TT *tipvec) {
+  const int64_t gx = grid_x((const void *)kernel, cache, 1, n, 64, 1, max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt, n, ws,
+                     tipvec);
+  return hipGetLastError();
+}
+
+template <int kTips, bool kSum>
+hipError_t launch_prot_batch_t(int dtype, bool fma, const dev::NodeBatch &b, int count, const void *EV,
+                               const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                               hipStream_t s, const void *tipvec) {
+  const double *E64 = (const double *)EV, *V64 = (const double *)tipvec;
+  const float *E32 = (const float *)EV, *V32 = (const float *)tipvec;
+  if (dtype == 1 && fma) {
+    static int cache = 0;
+    return launch_prot_batch_k(&dev::plf_prot_mfma_batch_kernel<kSum, 2, kTips>, cache, b, count, E64, wgt,
+                               n, ws, max_blocks, s, V64);
+  }
+  if (dtype == 1) {
+    static int cache = 0;
+    return launch_prot_batch_k(&dev::plf_prot_lds_batch_kernel<double, kSum, 2, kTips, 10, true>, cache, b,
+                               count, E64, wgt, n, ws, max_blocks, s, V64);
+  }
+  if (fma) {
+    static int cache = 0;
+    return launch_prot_batch_k(&dev::plf_prot_mfma32_batch_kernel<kSum, 3, kTips>, cache, b, count, E32,
+                               wgt, n, ws, max_blocks, s, V32);
+  }
+  static int cache = 0;
+  return launch_prot_batch_k(&dev::plf_prot_lds_batch_kernel<float, kSum, 2, kTips, 4, false>, cache, b,
+                             count, E32, wgt, n, ws, max_blocks, s, V32);
+}
+
+hipError_t launch_plf_prot_batch(int dtype, bool fma, const NodeDescH *nodes, int count, const void *EV,
+                                 const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                                 hipStream_t s, int tips, const void *tipvec) {
+  if (count < 1 || count > kMaxBatch || tips < 0 || tips > 2) return hipErrorInvalidValue;
+  dev::NodeBatch b{};
+  bool any_sum = false;
+  for (int i = 0; i < count; i++) {
+    b.d[i] = dev::NodeDesc{nodes[i].x1, nodes[i].x2, nodes[i].x3, nodes[i].left, nodes[i].right,
+                           nodes[i].scaler, nodes[i].scaler_sum};
+    any_sum |= nodes[i].scaler_sum != nullptr;
+  }
+  switch (tips * 2 + (any_sum ? 1 : 0)) {
+    case 0: return launch_prot_batch_t<0, false>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 1: return launch_prot_batch_t<0, true>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 2: return launch_prot_batch_t<1, false>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 3: return launch_prot_batch_t<1, true>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    case 4: return launch_prot_batch_t<2, false>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    default: return launch_prot_batch_t<2, true>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+  }
+}
+
 hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s,
                            int tips, const void *tipvec) {
   switch (tips) {

@@ -47,6 +47,10 @@ hipError_t launch_plf_dna_batch(int dtype, const NodeDescH *nodes, int count, co
                                 const int32_t *wgt, int64_t n, unsigned long long *ws,
                                 int max_blocks, hipStream_t s, int tips = 0,
                                 const void *tipvec = nullptr);
+// Protein (S = 20) nodes batched the same way; fma as launch_plf_prot.
+hipError_t launch_plf_prot_batch(int dtype, bool fma, const NodeDescH *nodes, int count, const void *EV,
+                                 const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                                 hipStream_t s, int tips, const void *tipvec);
 
 // Root log-likelihood; partials: >= kLnlMaxGrid doubles; ticket: kWsWords u64 (zero at rest).
 constexpr int kLnlMaxGrid = 4096;

@@ -18,6 +18,8 @@
 //                           and f32: matrices as LDS broadcasts, row groups
 //   plf_prot_mfma_kernel    FMA mode, f64, on the matrix cores
 //   plf_prot_mfma32_kernel  FMA mode, f32, on the matrix cores
+// each as a device body with a one-node kernel and a batched-nodes kernel
+// (*_batch_kernel: node = blockIdx.y, plf_dna.hpp NodeBatch).
 // The measured-and-not-adopted forms and knobs (the round-1 readlane kernel,
 // ablations, swizzles, rings, SGPR operands, ...) live in the tuning copy
 // tools/plf_prot_tune.hpp; DESIGN.md section 3.3 has the measurements.
@@ -443,6 +445,16 @@ plf_prot_lds_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__res
                                               scaler_sum, tipvec);
 }
 
+template <typename T, bool kSum, int kMinWaves, int kTips, int kRows, bool kE3S>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_lds_batch_kernel(const NodeBatch nodes, const T *__restrict__ EV, const int32_t *__restrict__ wgt,
+                          int64_t n, unsigned long long *ws, const T *__restrict__ tipvec) {
+  const NodeDesc &d = nodes.d[blockIdx.y];
+  prot_lds_body<T, kSum, kTips, kRows, kE3S>((const T *)d.x1, (const T *)d.x2, (T *)d.x3, EV,
+                                             (const T *)d.left, (const T *)d.right, wgt, d.scaler, n,
+                                             ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, tipvec);
+}
+
 // ---------------------------------------------------------------------------
 // FMA mode on the matrix cores (f64).  v_mfma_f64_16x16x4_f64 is bit-for-bit a
 // k-ordered fma chain (probed on MI355X: tools/probes/mfma_f64_numerics.hip),
@@ -531,14 +543,13 @@ struct ProtQueue {
   }
 };
 
-template <bool kSum, int kMinWaves, int kTips, bool kDyn = false>
-__global__ void __launch_bounds__(kBlock, kMinWaves)
-plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
-                     double *__restrict__ x3, const double *__restrict__ EV,
-                     const double *__restrict__ left, const double *__restrict__ right,
-                     const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                     unsigned long long *ws, int64_t *scaler_sum,
-                     const double *__restrict__ tipvec = nullptr) {
+template <bool kSum, int kTips, bool kDyn>
+__device__ __forceinline__ void prot_mfma_body(const double *__restrict__ x1, const double *__restrict__ x2,
+                                               double *__restrict__ x3, const double *__restrict__ EV,
+                                               const double *__restrict__ left, const double *__restrict__ right,
+                                               const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler,
+                                               int64_t n, unsigned long long *ws, int64_t *scaler_sum,
+                                               const double *__restrict__ tipvec) {
   constexpr int S = 20;
   // tips (kTips 1: x1, 2: both): the child's U^T comes from its LDS table in the
   // accumulator layout (lane: rows g + 4r and 16 + g of site lo16), no MFMA, no tile
@@ -733,6 +744,33 @@ plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
 
+// One node per launch (the grid strides over its sites)
+template <bool kSum, int kMinWaves, int kTips, bool kDyn = false>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_mfma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
+                     double *__restrict__ x3, const double *__restrict__ EV,
+                     const double *__restrict__ left, const double *__restrict__ right,
+                     const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                     unsigned long long *ws, int64_t *scaler_sum,
+                     const double *__restrict__ tipvec = nullptr) {
+  prot_mfma_body<kSum, kTips, kDyn>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum, tipvec);
+}
+
+// Batched protein nodes (a tree level, a shard of independent nodes): node =
+// blockIdx.y, descriptors by value as the DNA batches (plf_dna.hpp NodeBatch),
+// each node with its own kWsWords of scaler-sum workspace; the fixed grid stride
+// (no tile queue: its words would overlap the next node's sum region).
+template <bool kSum, int kMinWaves, int kTips>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_mfma_batch_kernel(const NodeBatch nodes, const double *__restrict__ EV,
+                           const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
+                           const double *__restrict__ tipvec) {
+  const NodeDesc &d = nodes.d[blockIdx.y];
+  prot_mfma_body<kSum, kTips, false>((const double *)d.x1, (const double *)d.x2, (double *)d.x3, EV,
+                                     (const double *)d.left, (const double *)d.right, wgt, d.scaler, n,
+                                     ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, tipvec);
+}
+
 
 // ---------------------------------------------------------------------------
 // FMA mode on the matrix cores, f32: v_mfma_f32_16x16x4_f32 is exact f32, a
@@ -782,14 +820,13 @@ __device__ __forceinline__ void transpose_groups44(unsigned (&v)[4]) {
   }
 }
 
-template <bool kSum, int kMinWaves, int kTips>
-__global__ void __launch_bounds__(kBlock, kMinWaves)
-plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x2,
-                       float *__restrict__ x3, const float *__restrict__ EV,
-                       const float *__restrict__ left, const float *__restrict__ right,
-                       const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                       unsigned long long *ws, int64_t *scaler_sum,
-                       const float *__restrict__ tipvec = nullptr) {
+template <bool kSum, int kTips>
+__device__ __forceinline__ void prot_mfma32_body(const float *__restrict__ x1, const float *__restrict__ x2,
+                                                 float *__restrict__ x3, const float *__restrict__ EV,
+                                                 const float *__restrict__ left, const float *__restrict__ right,
+                                                 const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler,
+                                                 int64_t n, unsigned long long *ws, int64_t *scaler_sum,
+                                                 const float *__restrict__ tipvec) {
   constexpr int S = 20;
   constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
   using PT = ProtTile<float>;
@@ -1011,6 +1048,28 @@ plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x
     __syncthreads();
   }
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
+}
+
+template <bool kSum, int kMinWaves, int kTips>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_mfma32_kernel(const float *__restrict__ x1, const float *__restrict__ x2,
+                       float *__restrict__ x3, const float *__restrict__ EV,
+                       const float *__restrict__ left, const float *__restrict__ right,
+                       const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
+                       unsigned long long *ws, int64_t *scaler_sum,
+                       const float *__restrict__ tipvec = nullptr) {
+  prot_mfma32_body<kSum, kTips>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum, tipvec);
+}
+
+template <bool kSum, int kMinWaves, int kTips>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
+plf_prot_mfma32_batch_kernel(const NodeBatch nodes, const float *__restrict__ EV,
+                             const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
+                             const float *__restrict__ tipvec) {
+  const NodeDesc &d = nodes.d[blockIdx.y];
+  prot_mfma32_body<kSum, kTips>((const float *)d.x1, (const float *)d.x2, (float *)d.x3, EV,
+                                (const float *)d.left, (const float *)d.right, wgt, d.scaler, n,
+                                ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, tipvec);
 }
 
 }  // namespace dev

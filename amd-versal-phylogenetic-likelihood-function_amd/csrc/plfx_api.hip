@@ -354,15 +354,32 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
   }
   if (n == 0 || count == 0) return PLFX_OK;
   PLFX_WS(ctx, s, w);
-  if (states == 20) {  // protein: one full-GPU launch per node (plf_prot.hpp)
-    for (int i = 0; i < count; i++) {
-      const plfx_node &d = nodes[i];
-      plfx::DnaArgs a{d.x1, d.x2, d.x3, EV, d.left, d.right, wgt, d.scaler, d.scaler_sum, w->ws, n};
-      hipError_t e = plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s,
-                                           tips, tipvec);
-      if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot launch");
+  if (states == 20 && count > 1) {
+    // protein: up to kMaxBatch nodes per launch, node = blockIdx.y, each node
+    // with the full resident grid so the nodes' blocks follow each other
+    // through the co-resident slots (the next node's blocks fill the CUs the
+    // previous node's last trips leave idle).  64-taxon tree at 2^18 sites per
+    // sweep vs one launch per node: f64 FMA 5.67 -> 5.38 ms, f64 exact 8.45 ->
+    // 8.02 ms, f32 FMA 2.94 -> 2.66 ms; splitting the resident grid over the
+    // nodes (the DNA batches' rule) gains only 1-3 % (tools/prot_batch_ab.py,
+    // profiles/r03_protein_batch_ab.log).
+    const plfx::NodeDescH *all = reinterpret_cast<const plfx::NodeDescH *>(nodes);
+    for (int j = 0; j < count; j += plfx::kMaxBatch) {
+      const int c = std::min(count - j, plfx::kMaxBatch);
+      hipError_t e = plfx::launch_plf_prot_batch(dtype, (flags & PLFX_FMA) != 0, all + j, c, EV, wgt, n,
+                                                 w->ws, ctx->max_blocks, s, tips, tipvec);
+      if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot batch launch");
       if (launches) ++*launches;
     }
+    return PLFX_OK;
+  }
+  if (states == 20) {  // protein, one node: one full-GPU launch (plf_prot.hpp)
+    const plfx_node &d = nodes[0];
+    plfx::DnaArgs a{d.x1, d.x2, d.x3, EV, d.left, d.right, wgt, d.scaler, d.scaler_sum, w->ws, n};
+    hipError_t e = plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s, tips,
+                                         tipvec);
+    if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot launch");
+    if (launches) ++*launches;
     return PLFX_OK;
   }
   // More than kMaxBatch nodes: launch j takes nodes j, j + L, j + 2L, ... (L

@@ -112,6 +112,75 @@ def test_protein_f64_many_trips(ctx, oracle, fma):
     assert np.array_equal(sc, esc) and s == einc and esc.sum() > 0
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("n", [4099, 3 * (1 << 15) + 7])
+def test_protein_batched_nodes(ctx, oracle, dtype, n):
+    """Several protein nodes in one batched launch (plf_prot_lds_batch_kernel:
+    node = blockIdx.y, each node with its own grid stride and sum workspace):
+    every node's CLV, scaler bytes and weighted sum bit-exact vs plf()'s loop,
+    nodes with and without a scaler-sum output mixed in one launch."""
+    import torch
+
+    nodes, exp = [], []
+    EV = None
+    for k in range(5):
+        x1, x2, ev, left, right, w = gen(n, dtype, 90 + k)
+        if EV is None:
+            EV, wgt = ev, w
+        e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, wgt)
+        nd = {"x1": dev(x1), "x2": dev(x2), "left": dev(left), "right": dev(right),
+              "x3": torch.empty(V * n, dtype=torch.float64 if dtype == np.float64 else torch.float32,
+                                device="cuda"),
+              "scaler": torch.empty(n, dtype=torch.uint8, device="cuda")}
+        if k != 2:
+            nd["scaler_sum"] = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+        nodes.append(nd)
+        exp.append((e3, esc, einc))
+    ctx.plf_batch_dev(nodes, dev(EV), n, dev(wgt), states=S)
+    torch.cuda.synchronize()
+    for k, (nd, (e3, esc, einc)) in enumerate(zip(nodes, exp)):
+        assert np.array_equal(bits(nd["x3"].cpu().numpy()), bits(e3)), k
+        assert np.array_equal(nd["scaler"].cpu().numpy(), esc), k
+        if "scaler_sum" in nd:
+            assert int(nd["scaler_sum"].item()) == einc, k
+    assert sum(e[2] for e in exp) > 0
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_protein_batched_level_fma(ctx, oracle, dtype):
+    """A 4-taxon protein tree in FMA mode: its first level (two nodes) runs as
+    one batched launch of the matrix-core kernel (plf_prot_mfma(32)_batch_kernel),
+    the root as a one-node launch; every node bit-exact vs the oracle's fma()
+    restatement applied node by node, scaler sums exact."""
+    import torch
+
+    n, ntips = (1 << 16) + 3, 4
+    rng = np.random.default_rng(11)
+    ops = oracle.balanced_tree_ops(ntips)
+    nops = ops.shape[0]
+    tips = [rng.random(V * n).astype(dtype) for _ in range(ntips)]
+    tips[0].reshape(n, V)[0::4] *= 1e-14
+    pm = rng.random(nops * 2 * CAT * S * S).astype(dtype)
+    EV = (rng.random(S * S) - 0.25).astype(dtype)
+    wgt = rng.integers(0, 4, n).astype(np.int32)
+    host = [t.copy() for t in tips] + [None] * nops
+    esums = []
+    for j, (p, c1, c2, m) in enumerate(ops):
+        L = pm[(2 * m) * CAT * S * S:(2 * m + 1) * CAT * S * S]
+        R = pm[(2 * m + 1) * CAT * S * S:(2 * m + 2) * CAT * S * S]
+        e3, _, einc = oracle.plf_generic(S, CAT, host[c1], host[c2], EV, L, R, wgt, fma=True)
+        host[p] = e3
+        esums.append(einc)
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    clv = [dev(t) for t in tips] + [torch.zeros(V * n, dtype=tt, device="cuda") for _ in range(nops)]
+    sums = torch.zeros(nops, dtype=torch.int64, device="cuda")
+    ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), None, sums, states=S, fma=True)
+    torch.cuda.synchronize()
+    for s_ in range(ntips, ntips + nops):
+        assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
+    assert sums.cpu().numpy().tolist() == esums and sum(esums) > 0
+
+
 def test_protein_full_size_256k(ctx, oracle):
     """BASELINE configs[4]: 2^18 sites, f64, bit-exact (EXACT mode), lnL."""
     import torch
