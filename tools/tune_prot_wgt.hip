@@ -11,7 +11,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //     -I amd-versal-phylogenetic-likelihood-function_amd/csrc -I tools tools/tune_prot_wgt.hip -o build/tune_prot_wgt
-//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32, 3 FMA: all waves wait before the stores, 4 f32 LDS-DMA tiles, 5 f64 first tile by DMA]
+//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32, 3 FMA: all waves wait before the stores, 4 f32 LDS-DMA tiles, 5 f64 first tile by DMA, 6 one-node kernels vs pre-refactor copies]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -184,6 +184,20 @@ int main(int argc, char **argv) {
     b.add("f64 FMA product again", 0, &plf_prot_mfma_kernel<true, 2, 0, false>);
     b.add("f64 FMA first x1 by DMA again", 0, &plf_prot_mfma_prio_kernel<true, 2, 0, 5, 0>);
     failures += b.run(reps, 5, "f64");
+  }
+  if (sel == 6) {  // one-node kernels after the body / batch refactor vs the pre-refactor copies
+    Bench<double> b(n);
+    b.add("f64 FMA product (body + wrapper)", 0, &plf_prot_mfma_kernel<true, 2, 0, false>);
+    b.add("f64 FMA pre-refactor copy", 0, &plf_prot_mfma_prio_kernel<true, 2, 0, 0, 0>);
+    b.add("f64 FMA product again", 0, &plf_prot_mfma_kernel<true, 2, 0, false>);
+    b.add("f64 FMA pre-refactor copy again", 0, &plf_prot_mfma_prio_kernel<true, 2, 0, 0, 0>);
+    failures += b.run(reps, 5, "f64");
+    Bench<float> c(n);
+    c.add("f32 FMA product (body + wrapper)", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
+    c.add("f32 FMA pre-refactor copy", 0, &plf_prot_mfma32_old_kernel<true, 3, 0>);
+    c.add("f32 FMA product again", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
+    c.add("f32 FMA pre-refactor copy again", 0, &plf_prot_mfma32_old_kernel<true, 3, 0>);
+    failures += c.run(reps, 5, "f32");
   }
   return failures ? 1 : 0;
 }
