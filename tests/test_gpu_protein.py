@@ -481,3 +481,22 @@ def test_protein_signed_zero_inputs(ctx, oracle, dtype, fma):
     e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=fma)
     assert np.array_equal(bits(x3), bits(e3))
     assert np.array_equal(sc, esc) and s == einc
+
+
+def test_bench_prottree64_small():
+    """bench.py --workload prottree64 end to end at a small size: the level-
+    batched protein tree sweep + root lnL runs, rescales (scaler events > 0),
+    and its first node matches the oracle bit for bit (cpu_baseline check)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    cmd = [sys.executable, str(root / "bench.py"), "--workload", "prottree64", "--sites", "4099",
+           "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.2", "--no-second-region"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(root))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["check"] == "ok" and d["cpu_baseline"]["check"] == "ok", d
+    assert d["config"]["scaler_events"] > 0 and d["config"]["nodes_per_gpu_per_step"] == 63
