@@ -222,8 +222,9 @@ typedef struct {
 
 /* `count` independent nodes sharing EV, n and wgt; all device pointers, the
  * `nodes` array itself is host memory (it travels in the kernel arguments, 32
- * nodes per launch: graph-capture safe).  states 4 (DNA) or 20 (protein, one
- * launch per node, exact mode). */
+ * nodes per launch: graph-capture safe).  states 4 (DNA) or 20 (protein,
+ * exact mode; up to 32 nodes per launch, node = blockIdx.y, each node with
+ * its own scaler-sum workspace region). */
 int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *nodes, int count,
                        const void *EV, int64_t n, const int32_t *wgt, void *stream);
 
