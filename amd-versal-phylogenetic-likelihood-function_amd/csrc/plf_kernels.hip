@@ -176,6 +176,21 @@ hipError_t launch_lnl_t(const T *x, int64_t n, const double *catw, const double 
   return hipGetLastError();
 }
 
+// protein root lnL: 64-site LDS tiles, the co-resident grid (plf_lnl.hpp
+// root_lnl_prot_kernel; the C-lanes form took 94 us for 2^18 f64 sites)
+template <typename T>
+hipError_t launch_lnl_prot_t(const T *x, int64_t n, const double *catw, const double *freq,
+                             const int32_t *wgt, const int64_t *sums, int nsums, double *partials,
+                             unsigned long long *ticket, double *out, double *site_lnl, hipStream_t s) {
+  static int cache = 0;
+  auto kernel = &dev::root_lnl_prot_kernel<T>;
+  int64_t gx = grid_x((const void *)kernel, cache, 1, n, 64, 1, 0);
+  if (gx > kLnlMaxGrid) gx = kLnlMaxGrid;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, x, n, catw, freq, wgt, sums, nsums,
+                     partials, ticket, out, site_lnl);
+  return hipGetLastError();
+}
+
 template <typename T, bool kFma, bool kSum, int kTips>
 hipError_t launch_prot_t(const DnaArgs &a, int max_blocks, hipStream_t s, const T *tipvec) {
   static_assert(sizeof(T) == 4, "f32 protein; f64 runs launch_prot_mfma_t / launch_prot_exact64_t");
@@ -588,11 +603,11 @@ hipError_t launch_root_lnl(int dtype, int states, const void *x, int64_t n, cons
     return launch_lnl_t<float, 4, 4>((const float *)x, n, catw, freq, wgt, scaler_sums, nsums,
                                      partials, ticket, out, site_lnl, s);
   if (states == 20 && dtype == 1)
-    return launch_lnl_t<double, 20, 4>((const double *)x, n, catw, freq, wgt, scaler_sums, nsums,
-                                       partials, ticket, out, site_lnl, s);
+    return launch_lnl_prot_t<double>((const double *)x, n, catw, freq, wgt, scaler_sums, nsums,
+                                     partials, ticket, out, site_lnl, s);
   if (states == 20 && dtype == 0)
-    return launch_lnl_t<float, 20, 4>((const float *)x, n, catw, freq, wgt, scaler_sums, nsums,
-                                      partials, ticket, out, site_lnl, s);
+    return launch_lnl_prot_t<float>((const float *)x, n, catw, freq, wgt, scaler_sums, nsums,
+                                    partials, ticket, out, site_lnl, s);
   return hipErrorInvalidValue;
 }
 
