@@ -11,7 +11,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //     -I amd-versal-phylogenetic-likelihood-function_amd/csrc -I tools tools/tune_prot_wgt.hip -o build/tune_prot_wgt
-//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32, 3 FMA: all waves wait before the stores, 4 f32 LDS-DMA tiles, 5 f64 first tile by DMA, 6 one-node kernels vs pre-refactor copies]
+//   build/tune_prot_wgt [sites] [reps] [sel: 0 all, 1 f64, 2 f32, 3 FMA: all waves wait before the stores, 4 f32 LDS-DMA tiles, 5 f64 first tile by DMA, 6 one-node kernels vs pre-refactor copies, 7 one node as k site slices]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,17 +46,17 @@ struct Bench {
   typedef void (*Kern)(const T *, const T *, T *, const T *, const T *, const T *, const int32_t *, uint8_t *,
                        int64_t, unsigned long long *, int64_t *, const T *);
   struct Set { T *x1, *x2, *x3; int *wgt; uint8_t *sc; int64_t *sum; };
-  struct V { std::string name; int group; std::function<void(const Set &)> run; std::vector<float> us; };
+  struct V { std::string name; int group; std::function<void(const Set &)> run; std::vector<float> us; int slices = 0; };
   int64_t n; int R = 4, CUs;
   std::vector<Set> sets;
   T *EV, *L, *Rm; unsigned long long *ws;
   std::vector<V> vs;
-  explicit Bench(int64_t n_) : n(n_) {
+  explicit Bench(int64_t n_, bool ones = false) : n(n_) {
     hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
     CUs = prop.multiProcessorCount;
     sets.resize(R);
     CK(hipMalloc(&EV, 400 * sizeof(T))); CK(hipMalloc(&L, 1600 * sizeof(T))); CK(hipMalloc(&Rm, 1600 * sizeof(T)));
-    CK(hipMalloc(&ws, 2 * kWsWords * 8)); CK(hipMemset(ws, 0, 2 * kWsWords * 8));
+    CK(hipMalloc(&ws, 64 * kWsWords * 8)); CK(hipMemset(ws, 0, 64 * kWsWords * 8));  // slices: one region each
     fill<T><<<8, 64>>>(EV, 400, 7, T(1), 1); fill<T><<<32, 64>>>(L, 1600, 8, T(1), 1); fill<T><<<32, 64>>>(Rm, 1600, 9, T(1), 1);
     const T tiny = sizeof(T) == 8 ? T(1e-14) : T(1e-14f);
     for (auto &s : sets) {
@@ -67,7 +67,7 @@ struct Bench {
       fill<T><<<2048, 256>>>(s.x1, (n + 64) * 80, 10 + r, tiny, 80);
       fill<T><<<2048, 256>>>(s.x2, (n + 64) * 80, 20 + r, T(1), 80);
       std::vector<int> w(n);
-      for (int64_t i = 0; i < n; i++) w[i] = 1 + (int)(i % 3);  // non-trivial weights
+      for (int64_t i = 0; i < n; i++) w[i] = ones ? 1 : 1 + (int)(i % 3);  // non-trivial weights
       CK(hipMemcpy(s.wgt, w.data(), n * 4, hipMemcpyHostToDevice));
     }
     CK(hipDeviceSynchronize());
@@ -80,6 +80,29 @@ struct Bench {
     vs.push_back({nm, group, [=](const Set &s) {
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), 0, 0, s.x1, s.x2, s.x3, ev, l, rm,
                          s.wgt, s.sc, nn, w, s.sum, nullptr); }, {}});
+  }
+  // one node as k site slices of a batched launch (node = blockIdx.y = slice,
+  // each with the full resident grid); slice sums land in sum[0..k) of a
+  // scratch array (the harness compares their total)
+  typedef void (*KB)(const NodeBatch, const T *, const int32_t *, int64_t, unsigned long long *, const T *);
+  int64_t *slice_sums = nullptr;
+  void add_sliced(const char *name, int group, KB k, int slices) {
+    if (!slice_sums) CK(hipMalloc(&slice_sums, 64 * sizeof(int64_t)));
+    int o = 0; CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void *)k, 256, 0));
+    const int64_t per = ((n + slices - 1) / slices + 63) / 64 * 64;  // whole tiles per slice
+    const int64_t gx = std::min<int64_t>((per + 63) / 64, (int64_t)o * CUs);
+    char nm[200]; snprintf(nm, sizeof nm, "%s (%d slices) occ=%d/CU grid=%lldx%d", name, slices, o, (long long)gx, slices);
+    const int64_t nn = n; T *ev = EV, *l = L, *rm = Rm; unsigned long long *w = ws; int64_t *ss = slice_sums;
+    vs.push_back({nm, group, [=](const Set &s) {
+      NodeBatch b{};
+      for (int y = 0; y < slices; y++) {
+        const int64_t lo = std::min<int64_t>(nn, y * per);
+        b.d[y] = NodeDesc{s.x1 + lo * 80, s.x2 + lo * 80, s.x3 + lo * 80, l, rm, s.sc + lo, ss + y};
+      }
+      // the slices share n: every slice but the last covers `per` sites
+      hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)slices), dim3(256), 0, 0, b, ev, s.wgt, per, w,
+                         (const T *)nullptr);
+      (void)nn; }, {}, slices});
   }
   int run(int reps, int rounds, const char *tag) {
     typedef typename std::conditional<sizeof(T) == 8, uint64_t, uint32_t>::type U;
@@ -94,6 +117,12 @@ struct Bench {
       CK(hipMemcpy(got.data(), sets[0].x3, n * 80 * sizeof(T), hipMemcpyDeviceToHost));
       CK(hipMemcpy(gsc.data(), sets[0].sc, n, hipMemcpyDeviceToHost));
       CK(hipMemcpy(&gsum, sets[0].sum, 8, hipMemcpyDeviceToHost));
+      if (v.slices) {  // the slices' sums
+        std::vector<int64_t> ps(v.slices);
+        CK(hipMemcpy(ps.data(), slice_sums, v.slices * 8, hipMemcpyDeviceToHost));
+        gsum = 0;
+        for (int64_t x : ps) gsum += x;
+      }
       if (ref[v.group].empty()) { ref[v.group] = got; rsc[v.group] = gsc; rsum[v.group] = gsum; }
       int64_t bad = 0;
       for (int64_t i = 0; i < n * 80; i++) bad += got[i] != ref[v.group][i];
@@ -197,6 +226,19 @@ int main(int argc, char **argv) {
     c.add("f32 FMA pre-refactor copy", 0, &plf_prot_mfma32_old_kernel<true, 3, 0>);
     c.add("f32 FMA product again", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
     c.add("f32 FMA pre-refactor copy again", 0, &plf_prot_mfma32_old_kernel<true, 3, 0>);
+    failures += c.run(reps, 5, "f32");
+  }
+  if (sel == 7) {  // one f64 / f32 FMA node as k site slices of a batched launch (weights 1)
+    Bench<double> b(n, true);
+    b.add("f64 FMA one-node kernel", 0, &plf_prot_mfma_kernel<true, 2, 0, false>);
+    for (int k : {2, 4, 8}) b.add_sliced("f64 FMA batch kernel", 0, &plf_prot_mfma_batch_kernel<true, 2, 0>, k);
+    b.add("f64 FMA one-node kernel again", 0, &plf_prot_mfma_kernel<true, 2, 0, false>);
+    b.add_sliced("f64 FMA batch kernel again", 0, &plf_prot_mfma_batch_kernel<true, 2, 0>, 4);
+    failures += b.run(reps, 5, "f64");
+    Bench<float> c(n, true);
+    c.add("f32 FMA one-node kernel", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
+    for (int k : {2, 4, 8}) c.add_sliced("f32 FMA batch kernel", 0, &plf_prot_mfma32_batch_kernel<true, 3, 0>, k);
+    c.add("f32 FMA one-node kernel again", 0, &plf_prot_mfma32_kernel<true, 3, 0>);
     failures += c.run(reps, 5, "f32");
   }
   return failures ? 1 : 0;
