@@ -9,6 +9,11 @@
 //
 //   usage: plfx_tree <taxa (power of 2)> <sites> <sweeps>
 //                    [--dtype f32|f64] [--tips] [--alpha A] [--seed S] [--quiet]
+//                    [--states 4|20] [--fma]
+//
+// --states 20: a 20-state reversible model (fixed exchangeabilities and
+// frequencies), amino-acid tips (codes 0..19, 5 % X), the protein kernels
+// (exact, or --fma on the matrix cores), tree levels as batched launches.
 //
 // Prints the per-sweep device time, the node-site rate and the lnL (%.17g);
 // with the same seed, dense tips and coded tips give the identical lnL (the tip
@@ -62,7 +67,8 @@ struct Opts {
   int taxa = 0;
   int64_t sites = 0;
   int sweeps = 1;
-  bool f64 = true, tips = false, quiet = false;
+  bool f64 = true, tips = false, quiet = false, fma = false;
+  int states = 4;
   double alpha = 0.5;
   uint32_t seed = 20250117u;
 };
@@ -74,15 +80,25 @@ int run(const Opts &o) {
   const int dt = o.f64 ? PLFX_F64 : PLFX_F32;
   const int T_ = o.taxa, nops = T_ - 1, nslots = 2 * T_ - 1;
   const int64_t n = o.sites;
+  const int S = o.states, V = 4 * S, M = 4 * S * S;  // values per site, per P pair member
 
-  // model: GTR exchangeabilities AC AG AT CG CT GT, frequencies, Gamma(alpha)
-  const double exch[6] = {1.2, 3.9, 0.8, 1.1, 4.6, 1.0};
-  const double freqs[4] = {0.31, 0.19, 0.22, 0.28};
-  std::vector<double> eig(4 + 2 * 16), rates(4), EVd(16), w(4);
-  plfx_model_eigen(4, exch, freqs, eig.data());
+  // model: GTR exchangeabilities AC AG AT CG CT GT, frequencies, Gamma(alpha);
+  // S = 20: a fixed pattern of the 190 exchangeabilities and 20 frequencies
+  std::vector<double> exch = {1.2, 3.9, 0.8, 1.1, 4.6, 1.0};
+  std::vector<double> freqs = {0.31, 0.19, 0.22, 0.28};
+  if (S == 20) {
+    exch.resize(190);
+    for (int k = 0; k < 190; k++) exch[k] = 0.5 + (double)((k * 37) % 29) / 10.0;
+    freqs.resize(20);
+    double tot = 0.0;
+    for (int s = 0; s < 20; s++) tot += (freqs[s] = 1.0 + (double)((s * 7) % 11));
+    for (double &f : freqs) f /= tot;
+  }
+  std::vector<double> eig(S + 2 * S * S), rates(4), EVd(S * S), w(S);
+  if (plfx_model_eigen(S, exch.data(), freqs.data(), eig.data()) != PLFX_OK) die("model_eigen");
   plfx_gamma_rates(o.alpha, 4, 0, rates.data());
-  plfx_model_ev(4, PLFX_PMAT_STATE, eig.data(), EVd.data());
-  plfx_model_root_weights(4, PLFX_PMAT_STATE, eig.data(), freqs, w.data());
+  plfx_model_ev(S, PLFX_PMAT_STATE, eig.data(), EVd.data());
+  plfx_model_root_weights(S, PLFX_PMAT_STATE, eig.data(), freqs.data(), w.data());
 
   // balanced tree: tips 0..T-1, inner slots T.. in post-order, op j = pmat j
   std::vector<plfx_trav_op> ops;
@@ -102,11 +118,18 @@ int run(const Opts &o) {
   std::uniform_real_distribution<double> U(0.0, 1.0);
   std::vector<double> blen(2 * nops);
   for (double &b : blen) b = 0.01 + 0.3 * U(gen);
-  // alignment: A/C/G/T codes, 5 % ambiguous (random non-empty subsets)
+  // alignment: A/C/G/T codes, 5 % ambiguous (random non-empty subsets);
+  // S = 20: amino-acid codes 0..19, 5 % X (code 22: every state)
   std::vector<std::vector<uint8_t>> codes(T_, std::vector<uint8_t>(n));
   const uint8_t acgt[4] = {1, 2, 4, 8};
   for (auto &c : codes)
-    for (auto &v : c) v = U(gen) < 0.05 ? (uint8_t)(1 + (int)(U(gen) * 15)) : acgt[(int)(U(gen) * 4) & 3];
+    for (auto &v : c) {
+      if (S == 4) v = U(gen) < 0.05 ? (uint8_t)(1 + (int)(U(gen) * 15)) : acgt[(int)(U(gen) * 4) & 3];
+      else {  // two draws per site, as the DNA form
+        const double a = U(gen), b = U(gen);
+        v = a < 0.05 ? (uint8_t)22 : (uint8_t)((int)(b * 20) % 20);
+      }
+    }
 
   // device state
   std::vector<void *> clv(nslots, nullptr);
@@ -114,18 +137,22 @@ int run(const Opts &o) {
   for (int t = 0; t < T_; t++) {
     if (o.tips) {
       tip[t] = upload(codes[t]);
-    } else {  // dense tip CLV: x[i][c][s] = bit s of the code, every category
-      std::vector<T> x(16 * n);
+    } else {  // dense tip CLV: x[i][c][s] = bit s of the code (DNA) / state s of the code
+      std::vector<T> x((size_t)V * n);
       for (int64_t i = 0; i < n; i++)
         for (int c = 0; c < 4; c++)
-          for (int s = 0; s < 4; s++) x[16 * i + 4 * c + s] = (T)((codes[t][i] >> s) & 1);
+          for (int s = 0; s < S; s++) {
+            const int code = codes[t][i];
+            const bool on = S == 4 ? ((code >> s) & 1) : (code >= 20 || code == s);
+            x[(size_t)V * i + S * c + s] = (T)(on ? 1 : 0);
+          }
       clv[t] = upload(x);
     }
   }
-  for (int s = T_; s < nslots; s++) clv[s] = dalloc<T>(16 * n);
+  for (int s = T_; s < nslots; s++) clv[s] = dalloc<T>((size_t)V * n);
   double *d_eig = upload(eig), *d_rates = upload(rates), *d_blen = upload(blen);
   std::vector<T> EVt(EVd.begin(), EVd.end());
-  T *d_EV = upload(EVt), *d_pm = dalloc<T>((size_t)2 * nops * 64);
+  T *d_EV = upload(EVt), *d_pm = dalloc<T>((size_t)2 * nops * M);
   double *d_w = upload(w), *d_lnl = dalloc<double>(1);
   int64_t *d_sums = dalloc<int64_t>(nops);
   hipStream_t st = reinterpret_cast<hipStream_t>(plfx_ctx_stream(ctx));
@@ -133,11 +160,11 @@ int run(const Opts &o) {
   for (auto &e : ev) HIPCHK(hipEventCreate(&e));
 
   auto sweep = [&]() {
-    PLFXCHK(ctx, plfx_pmatrix(ctx, dt, 4, PLFX_PMAT_STATE, d_eig, d_rates, 4, d_blen, 2 * nops, d_pm, st));
-    PLFXCHK(ctx, plfx_traverse_tips(ctx, dt, 4, PLFX_EXACT, ops.data(), nops, clv.data(),
+    PLFXCHK(ctx, plfx_pmatrix(ctx, dt, S, PLFX_PMAT_STATE, d_eig, d_rates, 4, d_blen, 2 * nops, d_pm, st));
+    PLFXCHK(ctx, plfx_traverse_tips(ctx, dt, S, o.fma ? PLFX_FMA : PLFX_EXACT, ops.data(), nops, clv.data(),
                                     o.tips ? tip.data() : nullptr, nslots, d_pm, nops, d_EV, n,
                                     nullptr, nullptr, d_sums, nullptr, st));
-    PLFXCHK(ctx, plfx_root_lnl(ctx, dt, 4, clv[nslots - 1], n, nullptr, d_w, nullptr, d_sums, nops,
+    PLFXCHK(ctx, plfx_root_lnl(ctx, dt, S, clv[nslots - 1], n, nullptr, d_w, nullptr, d_sums, nops,
                                d_lnl, nullptr, st));
   };
   sweep();  // warm-up
@@ -169,6 +196,7 @@ int run(const Opts &o) {
     std::printf("| alignment sites:        | %54lld |\n", (long long)n);
     std::printf("| element type / tips:    | %24s / %26s |\n", o.f64 ? "f64" : "f32",
                 o.tips ? "state codes" : "dense CLVs");
+    std::printf("| states / mode:          | %24d / %26s |\n", S, o.fma ? "FMA" : "exact");
     std::printf("| sweeps (P + traversal + lnL) | %49d |\n", o.sweeps);
     std::printf("==================================================================================\n");
     std::printf("| sweep time (ms) avg / min / max | %14.4f / %10.4f / %10.4f |\n", avg, mn, mx);
@@ -190,7 +218,7 @@ int run(const Opts &o) {
 int main(int argc, char **argv) {
   if (argc < 4)
     die("usage: plfx_tree <taxa (power of 2)> <sites> <sweeps> [--dtype f32|f64] [--tips] "
-        "[--alpha A] [--seed S] [--quiet]");
+        "[--alpha A] [--seed S] [--quiet] [--states 4|20] [--fma]");
   Opts o;
   try {
     o.taxa = std::stoi(argv[1]);
@@ -218,6 +246,11 @@ int main(int argc, char **argv) {
       o.seed = (uint32_t)std::stoul(next());
     } else if (a == "--quiet") {
       o.quiet = true;
+    } else if (a == "--states") {
+      o.states = std::stoi(next());
+      if (o.states != 4 && o.states != 20) die("states must be 4 or 20");
+    } else if (a == "--fma") {
+      o.fma = true;
     } else {
       die("unknown option " + a);
     }
