@@ -483,7 +483,8 @@ def test_protein_signed_zero_inputs(ctx, oracle, dtype, fma):
     assert np.array_equal(sc, esc) and s == einc
 
 
-def test_bench_prottree64_small():
+@pytest.mark.parametrize("tips", [False, True])
+def test_bench_prottree64_small(tips):
     """bench.py --workload prottree64 end to end at a small size: the level-
     batched protein tree sweep + root lnL runs, rescales (scaler events > 0),
     and its first node matches the oracle bit for bit (cpu_baseline check)."""
@@ -494,7 +495,8 @@ def test_bench_prottree64_small():
 
     root = Path(__file__).resolve().parents[1]
     cmd = [sys.executable, str(root / "bench.py"), "--workload", "prottree64", "--sites", "4099",
-           "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.2", "--no-second-region"]
+           "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.2", "--no-second-region"] + \
+        (["--tips"] if tips else [])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(root))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
