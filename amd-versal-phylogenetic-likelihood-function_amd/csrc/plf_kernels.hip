@@ -541,6 +541,34 @@ hipError_t launch_plf_prot_batch(int dtype, bool fma, const NodeDescH *nodes, in
   }
 }
 
+template <typename T, bool kSum>
+hipError_t launch_gather_t(const dev::ProtGatherBatch &b, int count, const int32_t *wgt, int64_t n,
+                           unsigned long long *ws, int max_blocks, hipStream_t s) {
+  static int cache = 0;
+  auto kernel = &dev::prot_tiptip_gather_kernel<T, kSum>;
+  const int64_t gx = grid_x((const void *)kernel, cache, 1, n, 64, 1, max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, wgt, n, ws);
+  return hipGetLastError();
+}
+
+hipError_t launch_prot_tiptip_gather(int dtype, const ProtGatherDescH *d, int count, const int32_t *wgt,
+                                     int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s) {
+  if (count < 1 || count > kMaxBatch) return hipErrorInvalidValue;
+  static_assert(kProtCombos == dev::kProtCombos, "combination count");
+  dev::ProtGatherBatch b{};
+  bool any_sum = false;
+  for (int i = 0; i < count; i++) {
+    static_assert(sizeof(b.d[0]) == sizeof(d[0]), "layout");
+    __builtin_memcpy(&b.d[i], &d[i], sizeof(d[i]));
+    any_sum |= d[i].scaler_sum != nullptr;
+  }
+  if (dtype == 1)
+    return any_sum ? launch_gather_t<double, true>(b, count, wgt, n, ws, max_blocks, s)
+                   : launch_gather_t<double, false>(b, count, wgt, n, ws, max_blocks, s);
+  return any_sum ? launch_gather_t<float, true>(b, count, wgt, n, ws, max_blocks, s)
+                 : launch_gather_t<float, false>(b, count, wgt, n, ws, max_blocks, s);
+}
+
 hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s,
                            int tips, const void *tipvec) {
   switch (tips) {

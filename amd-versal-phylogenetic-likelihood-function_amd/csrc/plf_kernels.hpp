@@ -47,6 +47,20 @@ hipError_t launch_plf_dna_batch(int dtype, const NodeDescH *nodes, int count, co
                                 const int32_t *wgt, int64_t n, unsigned long long *ws,
                                 int max_blocks, hipStream_t s, int tips = 0,
                                 const void *tipvec = nullptr);
+// Tip/tip protein nodes from their 576-combination tables (plf_prot.hpp
+// prot_tiptip_gather_kernel): x3 / scaler / sum of each node gathered by code pair.
+struct ProtGatherDescH {
+  const uint8_t *c1, *c2;
+  void *x3;
+  uint8_t *scaler;
+  int64_t *scaler_sum;
+  const void *tab;
+  const uint8_t *tsc;
+};
+constexpr int kProtCombos = 24 * 24;
+hipError_t launch_prot_tiptip_gather(int dtype, const ProtGatherDescH *d, int count, const int32_t *wgt,
+                                     int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s);
+
 // Protein (S = 20) nodes batched the same way; fma as launch_plf_prot.
 hipError_t launch_plf_prot_batch(int dtype, bool fma, const NodeDescH *nodes, int count, const void *EV,
                                  const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,

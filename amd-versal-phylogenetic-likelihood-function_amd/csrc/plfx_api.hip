@@ -42,6 +42,7 @@ struct StreamWs {
   unsigned long long *ws = nullptr;  // kWsRegions x kWsWords u64
   double *lnl_partials = nullptr;    // kLnlMaxGrid doubles
   unsigned long long *lnl_ticket = nullptr;
+  void *tt = nullptr;  // tip/tip protein combination tables (kTtBytes, on first use; stays with the entry)
 };
 constexpr int kWsPool = PLFX_WS_POOL;
 
@@ -191,6 +192,43 @@ StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
   ws_carve(w, block);
   ctx->wss.push_back(w);
   return &ctx->wss.back();
+}
+
+// Tip/tip protein combination tables of one stream entry: the two constant
+// 576-code arrays (combo k = code1 * 24 + code2) and, per node of a batch, a
+// 576 x 80 table of the node's dtype and 576 scaler bytes (plf_prot.hpp
+// prot_tiptip_gather_kernel).  Allocated on the entry's first tip/tip protein
+// call (not inside a capture: the caller then takes the direct kernel).
+constexpr size_t kTtCodeBytes = 2048;
+constexpr size_t kTtTabBytes = (size_t)plfx::kProtCombos * 80 * sizeof(double);
+constexpr size_t kTtScBytes = 1024;
+constexpr size_t kTtBytes = kTtCodeBytes + (size_t)plfx::kMaxBatch * (kTtTabBytes + kTtScBytes);
+
+void *tt_for(plfx_ctx *ctx, StreamWs *w, hipStream_t s) {
+  if (w->tt) return w->tt;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (s && hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) return nullptr;
+  struct Codes {
+    uint8_t v[kTtCodeBytes] = {};
+    Codes() {
+      for (int k = 0; k < plfx::kProtCombos; k++) {
+        v[k] = (uint8_t)(k / 24);
+        v[1024 + k] = (uint8_t)(k % 24);
+      }
+    }
+  };
+  static const Codes codes;  // thread-safe one-time initialisation
+
+  void *b = nullptr;
+  if (hipMalloc(&b, kTtBytes) != hipSuccess) return nullptr;
+  if (hipMemcpyAsync(b, codes.v, kTtCodeBytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    (void)hipFree(b);
+    return nullptr;
+  }
+  ctx->ws_blocks.push_back(b);  // freed with the context
+  w->tt = b;
+  return b;
 }
 
 // the workspace of stream s as `out`; returns from the caller on failure
@@ -354,6 +392,34 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
   }
   if (n == 0 || count == 0) return PLFX_OK;
   PLFX_WS(ctx, s, w);
+  if (states == 20 && tips == 2) {
+    // both children coded tips: the node's 576 code pairs through its own
+    // kernel, then x3 / scaler / sum gathered by code pair (a write stream;
+    // the direct kernel is compute-bound: 77 us f64, 95 us f32 per 2^18 sites)
+    if (char *tt = static_cast<char *>(tt_for(ctx, w, s))) {
+      const uint8_t *cc1 = reinterpret_cast<const uint8_t *>(tt), *cc2 = cc1 + 1024;
+      for (int j = 0; j < count; j += plfx::kMaxBatch) {
+        const int c = std::min(count - j, plfx::kMaxBatch);
+        plfx::NodeDescH comb[plfx::kMaxBatch];
+        plfx::ProtGatherDescH g[plfx::kMaxBatch];
+        for (int i = 0; i < c; i++) {
+          const plfx_node &d = nodes[j + i];
+          char *tab = tt + kTtCodeBytes + (size_t)i * (kTtTabBytes + kTtScBytes);
+          uint8_t *tsc = reinterpret_cast<uint8_t *>(tab + kTtTabBytes);
+          comb[i] = plfx::NodeDescH{cc1, cc2, tab, d.left, d.right, tsc, nullptr};
+          g[i] = plfx::ProtGatherDescH{static_cast<const uint8_t *>(d.x1), static_cast<const uint8_t *>(d.x2),
+                                       d.x3, d.scaler, d.scaler_sum, tab, tsc};
+        }
+        hipError_t e = plfx::launch_plf_prot_batch(dtype, (flags & PLFX_FMA) != 0, comb, c, EV, nullptr,
+                                                   plfx::kProtCombos, w->ws, ctx->max_blocks, s, 2, tipvec);
+        if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot combination tables");
+        e = plfx::launch_prot_tiptip_gather(dtype, g, c, wgt, n, w->ws, ctx->max_blocks, s);
+        if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot tip/tip gather");
+        if (launches) *launches += 2;
+      }
+      return PLFX_OK;
+    }
+  }
   if (states == 20 && count > 1) {
     // protein: up to kMaxBatch nodes per launch, node = blockIdx.y, each node
     // with the full resident grid so the nodes' blocks follow each other

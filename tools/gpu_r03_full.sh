@@ -20,5 +20,6 @@ for w in $W; do
     tree64_tips) bash tools/gpu_r03_measure.sh $T/tree64_tips 20 --workload tree64 --tips --steps 50 --warmup 5 || exit 1 ;;
     nodes512) EXTRA_STEPS=1 bash tools/gpu_r03_measure.sh $T/nodes512 2 --workload nodes512 --steps 10 --warmup 2 || exit 1 ;;
     prottree64) bash tools/gpu_r03_measure.sh $T/prottree64 10 --workload prottree64 --steps 50 --warmup 5 || exit 1 ;;
+    prottree64_tips) bash tools/gpu_r03_measure.sh $T/prottree64_tips 10 --workload prottree64 --tips --steps 50 --warmup 5 || exit 1 ;;
   esac
 done
