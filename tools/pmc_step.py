@@ -18,7 +18,7 @@ import json
 import statistics as st
 
 
-PLF_KERNELS = ("plf_dna", "root_lnl", "plf_prot", "pmatrix")
+PLF_KERNELS = ("plf_dna", "root_lnl", "plf_prot", "pmatrix", "prot_tiptip")
 
 
 def groups(path, name, exclude=()):
