@@ -531,3 +531,49 @@ def test_protein_root_lnl_tiles(ctx, oracle, dtype):
     got = sl.cpu().numpy()
     assert np.max(np.abs(got - esl) / np.maximum(np.abs(esl), 1e-300)) <= 1e-15
     assert abs(float(out.item()) - exp) <= 1e-12 * abs(exp)
+
+
+@pytest.mark.parametrize("warm", [False, True])
+def test_protein_tiptip_in_graph_capture(ctx, oracle, warm):
+    """A tip/tip protein node captured in a HIP graph: on a stream whose
+    combination tables do not exist yet (cold) the node takes the direct
+    kernel (no allocation inside a capture); on a warmed stream the capture
+    holds the combination-table launch and the gather.  Replays are
+    bit-identical to the oracle either way."""
+    import torch
+
+    n = 5003
+    rng = np.random.default_rng(31)
+    _, _, EV, left, right, w = gen(n, np.float64, 12)
+    c1, c2 = oracle.random_protein_codes(rng, n, 0.3), oracle.random_protein_codes(rng, n, 0.3)
+    e1, e2 = oracle.expand_protein_tips(c1, np.float64), oracle.expand_protein_tips(c2, np.float64)
+    f3, fsc, finc = oracle.plf_generic(S, CAT, e1, e2, EV, left, right, w)
+    t = [dev(a) for a in (c1, c2, EV, left, right, w)]
+    x3 = torch.empty(V * n, dtype=torch.float64, device="cuda")
+    sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st = torch.cuda.Stream()
+
+    def call():
+        ctx.plf_tips_dev(x3, t[2], n, t[3], t[4], tip1=t[0], tip2=t[1], wgt=t[5], scaler=sc,
+                         scaler_sum=s, states=S, stream=st)
+
+    torch.cuda.synchronize()
+    if warm:
+        call()
+    else:  # the stream's workspace exists, its combination tables do not
+        xd = dev(np.zeros(V * n))
+        ctx.plf_tips_dev(x3, t[2], n, t[3], t[4], tip1=t[0], x2=xd, wgt=t[5], scaler=sc,
+                         scaler_sum=s, states=S, stream=st)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        call()
+    for _ in range(3):
+        x3.zero_()
+        s.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(x3.cpu().numpy()), bits(f3))
+        assert np.array_equal(sc.cpu().numpy(), fsc) and int(s.item()) == finc
