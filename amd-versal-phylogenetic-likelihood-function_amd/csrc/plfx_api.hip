@@ -219,10 +219,16 @@ void *tt_for(plfx_ctx *ctx, StreamWs *w, hipStream_t s) {
   };
   static const Codes codes;  // thread-safe one-time initialisation
 
+  // on failure the caller takes the direct kernel; the error is cleared so
+  // that the launch check after it does not report it
   void *b = nullptr;
-  if (hipMalloc(&b, kTtBytes) != hipSuccess) return nullptr;
+  if (hipMalloc(&b, kTtBytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
   if (hipMemcpyAsync(b, codes.v, kTtCodeBytes, hipMemcpyHostToDevice, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess) {
+    (void)hipGetLastError();
     (void)hipFree(b);
     return nullptr;
   }
