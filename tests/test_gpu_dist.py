@@ -103,3 +103,38 @@ def test_nodes_three_ranks_ragged_split():
     assert d["n_gpus"] == 2 and len(d["config"]["lnl_per_rank"]) == 2
     assert d["config"]["lnl_all_ranks"] == sum(d["config"]["lnl_per_rank"])
     assert d["config"]["scaler_events_all_ranks"] == 2 * (65536 // 4)
+
+
+def test_nodes512_full_size_windows(oracle):
+    """BASELINE configs[3] at full size on one GPU, as bench.py times it: the
+    512 nodes x 2^20 f64 sites of bench.NodesWorkload (201 GB of CLVs) in its
+    16 interleaved 32-node launches.  A 1024-site window of every node is
+    checked bit for bit against the oracle on that window (x3 and scaler
+    bytes), and every node's scaler sum is its N/4 rescaled sites."""
+    import torch
+
+    import bench
+    import plfx
+
+    n = 1 << 20
+    a = bench.parse(["--workload", "nodes512"])
+    assert a.nodes == 512 and a.sites == n
+    dev = torch.device("cuda", 0)
+    with plfx.Context(0) as ctx:
+        wl = bench.NodesWorkload(ctx, a, dev, None, torch.float64, 8, 1, 0)
+        assert wl.cnt == 512 and len(wl.launchers) == 16
+        wl.step(0, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        EV = wl.EV.cpu().numpy()
+        ones = np.ones(1024, dtype=np.int32)
+        for j, nd in enumerate(wl.nodes):
+            lo = (j * 40961) % (n - 1024)
+            sl = slice(16 * lo, 16 * (lo + 1024))
+            h = {k: nd[k][sl].cpu().numpy() for k in ("x1", "x2", "x3")}
+            e3, esc, _ = oracle.plf(h["x1"], h["x2"], EV, nd["left"].cpu().numpy(),
+                                    nd["right"].cpu().numpy(), ones)
+            assert np.array_equal(h["x3"].view(np.uint64), e3.view(np.uint64)), j
+            assert np.array_equal(nd["scaler"][lo:lo + 1024].cpu().numpy(), esc), j
+        assert wl.sums.cpu().tolist() == [n // 4] * 512
+        del wl
+    torch.cuda.empty_cache()
