@@ -291,7 +291,12 @@ int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const
  * fused where possible (bit-identical results; env PLFX_FUSE=2 no six-level
  * passes, 1 pairs only, 0 none).  states 4 or 20; flags as
  * plfx_plf_dev_gen (PLFX_FMA: protein nodes on the f64 / f32 matrix cores;
- * DNA is always exact).  plfx_traverse == flags PLFX_EXACT, no tips, no tipvec. */
+ * DNA is always exact).  plfx_traverse == flags PLFX_EXACT, no tips, no tipvec.
+ * Protein tip/tip nodes (here and in plfx_plf_tips_dev_gen) are evaluated once
+ * per code pair (24 x 24) into tables of the stream's workspace (about 11.8 MB,
+ * allocated on that stream's first such call, freed with the context) and
+ * gathered per site: the same values as the direct computation; a capture on
+ * a stream without the tables yet runs the direct kernel. */
 int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const plfx_trav_op *ops,
                        int nops, void *const *clv, const uint8_t *const *tips, int nslots,
                        const void *pmats,
