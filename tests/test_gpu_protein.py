@@ -577,3 +577,71 @@ def test_protein_tiptip_in_graph_capture(ctx, oracle, warm):
         torch.cuda.synchronize()
         assert np.array_equal(bits(x3.cpu().numpy()), bits(f3))
         assert np.array_equal(sc.cpu().numpy(), fsc) and int(s.item()) == finc
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 129])
+def test_protein_tiptip_edge_sizes(ctx, oracle, dtype, fma, n):
+    """Tip/tip protein nodes (combination tables + gather) at ragged sizes
+    around the 64-site tile, with and without weights and per-site scaler
+    output, junk codes >= 24 included: the same values as the oracle on the
+    expanded leaves (exact: bit for bit; FMA: the fused restatement)."""
+    import torch
+
+    rng = np.random.default_rng(900 + n)
+    _, _, EV, left, right, w = gen(n, dtype, 40 + n)
+    left = (left * 1e-10).astype(dtype)  # code pairs on both sides of the 2^-32 rescale threshold
+    c1, c2 = oracle.random_protein_codes(rng, n, 0.3), oracle.random_protein_codes(rng, n, 0.3)
+    c1[0] = 200  # junk code: the all-ones row
+    e1, e2 = oracle.expand_protein_tips(c1, dtype), oracle.expand_protein_tips(c2, dtype)
+    for wgt in (None, w):
+        ww = np.ones(n, np.int32) if wgt is None else wgt
+        f3, fsc, finc = oracle.plf_generic(S, CAT, e1, e2, EV, left, right, ww, fma=fma)
+        for with_scaler in (False, True):
+            x3 = torch.empty(V * n, dtype=torch.float64 if dtype == np.float64 else torch.float32,
+                             device="cuda")
+            sc = torch.empty(n, dtype=torch.uint8, device="cuda") if with_scaler else None
+            s = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+            ctx.plf_tips_dev(x3, dev(EV), n, dev(left), dev(right), tip1=dev(c1), tip2=dev(c2),
+                             wgt=None if wgt is None else dev(wgt), scaler=sc, scaler_sum=s,
+                             states=S, fma=fma)
+            torch.cuda.synchronize()
+            assert np.array_equal(bits(x3.cpu().numpy()), bits(f3))
+            assert int(s.item()) == finc
+            if with_scaler:
+                assert np.array_equal(sc.cpu().numpy(), fsc)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_protein_traverse_all_coded_128(ctx, oracle, dtype):
+    """A 128-taxon protein tree with every leaf coded: its first level is 64
+    tip/tip nodes, two batches of 32 through the same stream's combination
+    tables (the second batch overwrites the first's tables in stream order).
+    Exact traversal bit for bit against the oracle's sequential traversal."""
+    import torch
+
+    n, ntips = 300, 128
+    rng = np.random.default_rng(128)
+    ops = oracle.balanced_tree_ops(ntips)
+    nops, nslots = ops.shape[0], ntips + ops.shape[0]
+    codes = [oracle.random_protein_codes(rng, n, 0.2) for _ in range(ntips)]
+    pm = (rng.random(nops * 2 * CAT * S * S) * 0.05).astype(dtype)
+    EV = (rng.random(S * S) * 0.05).astype(dtype)
+    wgt = rng.integers(1, 4, n).astype(np.int32)
+    host = [oracle.expand_protein_tips(codes[t], dtype) for t in range(ntips)]
+    host += [np.zeros(V * n, dtype) for _ in range(nops)]
+    esums, escal = oracle.traverse(S, CAT, ops, host, pm, EV, n, wgt, want_scalers=True)
+    assert esums.sum() > 0
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    clv = [None] * ntips + [torch.zeros(V * n, dtype=tt, device="cuda") for _ in range(nops)]
+    tips = [dev(c) for c in codes] + [None] * nops
+    sums = torch.zeros(nops, dtype=torch.int64, device="cuda")
+    scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+    ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips, states=S)
+    torch.cuda.synchronize()
+    for s in range(ntips, nslots):
+        assert np.array_equal(bits(clv[s].cpu().numpy()), bits(host[s])), s
+    assert np.array_equal(sums.cpu().numpy(), esums)
+    for j in range(nops):
+        assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
