@@ -67,6 +67,13 @@ def build():
     subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
 
 
+def _gen_omp_argtypes(L, sfx, fp):
+    f = getattr(L, f"plfo_plf_gen_omp_{sfx}")
+    f.argtypes = [C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_longlong, fp, fp,
+                  C.c_void_p, C.POINTER(C.c_longlong), C.c_void_p, C.c_int]
+    f.restype = None
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -90,6 +97,7 @@ def lib():
             f.argtypes = [C.c_int, C.c_int, fp, fp, fp, fp, C.c_longlong, fp, fp,
                           C.c_void_p, C.POINTER(C.c_longlong), C.c_void_p]
             f.restype = None
+            _gen_omp_argtypes(L, sfx, fp)
             f = getattr(L, f"plfo_gen_hostmem_{sfx}")
             f.argtypes = [C.c_uint32, C.c_longlong, fp, fp, fp, fp, fp, C.c_void_p]
             f.restype = None
@@ -135,6 +143,12 @@ def native_lib():
             f.argtypes = [fp, fp, fp, fp, C.c_longlong, fp, fp, C.c_void_p,
                           C.POINTER(C.c_int), C.c_void_p, C.c_int]
             f.restype = None
+            for name in (f"plfo_plf_gen_{sfx}", f"plfo_plf_gen_fma_{sfx}"):
+                f = getattr(L, name)
+                f.argtypes = [C.c_int, C.c_int, fp, fp, fp, fp, C.c_longlong, fp, fp,
+                              C.c_void_p, C.POINTER(C.c_longlong), C.c_void_p]
+                f.restype = None
+            _gen_omp_argtypes(L, sfx, fp)
         _native = L
     return _native or None
 
@@ -227,10 +241,12 @@ def plf(x1, x2, EV, left, right, wgt=None, n=None, threads=0, out=None, L=None):
     return x3, sc, inc.value
 
 
-def plf_generic(S, Ccat, x1, x2, EV, left, right, wgt=None, fma=False):
+def plf_generic(S, Ccat, x1, x2, EV, left, right, wgt=None, fma=False, threads=0, L=None):
     """Generic S-state / C-category restatement (protein S=20): unpinned
     extension; identical to plf() for S=C=4.  fma=True: every multiply-add
-    fused in the same order (the PLFX_FMA mode)."""
+    fused in the same order (the PLFX_FMA mode).  threads > 0: the OpenMP
+    variant (identical results); L another build of the same source
+    (native_lib())."""
     dt = x1.dtype
     V = S * Ccat
     n = x1.size // V
@@ -239,8 +255,13 @@ def plf_generic(S, Ccat, x1, x2, EV, left, right, wgt=None, fma=False):
     inc = C.c_longlong(0)
     if wgt is not None:
         wgt = np.ascontiguousarray(wgt, dtype=np.int32)
+    L = L or lib()
+    if threads > 0:
+        getattr(L, f"plfo_plf_gen_omp_{_sfx(dt)}")(int(fma), S, Ccat, x1, x2, x3, EV, n, left, right,
+                                                   _ptr(wgt), C.byref(inc), _ptr(sc), threads)
+        return x3, sc, inc.value
     name = f"plfo_plf_gen_fma_{_sfx(dt)}" if fma else f"plfo_plf_gen_{_sfx(dt)}"
-    getattr(lib(), name)(S, Ccat, x1, x2, x3, EV, n, left, right, _ptr(wgt), C.byref(inc), _ptr(sc))
+    getattr(L, name)(S, Ccat, x1, x2, x3, EV, n, left, right, _ptr(wgt), C.byref(inc), _ptr(sc))
     return x3, sc, inc.value
 
 

@@ -206,6 +206,40 @@ PLFO_DEFINE_GEN(f64, double)
 PLFO_DEFINE_GEN_FMA(f32, float, fmaf)
 PLFO_DEFINE_GEN_FMA(f64, double, fma)
 
+/* OpenMP variant of the generic loops (static site split, one contiguous
+ * chunk per thread through the serial function) used only as the multi-core
+ * CPU baseline; per-site results are identical to the serial loop. */
+#define PLFO_DEFINE_GEN_OMP(SUFFIX, T)                                             \
+  void plfo_plf_gen_omp_##SUFFIX(int fma, int S, int C, const T *x1s, const T *x2s, \
+                                 T *x3s, const T *EV, long long n, const T *left,  \
+                                 const T *right, const int *wgt,                   \
+                                 long long *scalerIncrement, unsigned char *scaler, \
+                                 int threads) {                                    \
+    long long addScale = 0;                                                        \
+    const long long V = (long long)S * C;                                          \
+    _Pragma("omp parallel num_threads(threads) reduction(+:addScale)")            \
+    {                                                                              \
+      const long long t = omp_get_thread_num(), nt = omp_get_num_threads();        \
+      const long long lo = n * t / nt, hi = n * (t + 1) / nt;                      \
+      long long inc = 0;                                                           \
+      if (hi > lo) {                                                               \
+        if (fma)                                                                   \
+          plfo_plf_gen_fma_##SUFFIX(S, C, x1s + lo * V, x2s + lo * V, x3s + lo * V, \
+                                    EV, hi - lo, left, right, wgt ? wgt + lo : 0,  \
+                                    &inc, scaler ? scaler + lo : 0);               \
+        else                                                                       \
+          plfo_plf_gen_##SUFFIX(S, C, x1s + lo * V, x2s + lo * V, x3s + lo * V, EV, \
+                                hi - lo, left, right, wgt ? wgt + lo : 0, &inc,    \
+                                scaler ? scaler + lo : 0);                         \
+      }                                                                            \
+      addScale += inc;                                                             \
+    }                                                                              \
+    if (scalerIncrement) *scalerIncrement = addScale;                              \
+  }
+
+PLFO_DEFINE_GEN_OMP(f32, float)
+PLFO_DEFINE_GEN_OMP(f64, double)
+
 /* Host-side scaler reduction, app/src/host_mem.cpp:384-388. */
 long long plfo_scaler_sum(const unsigned char *scaler, const int *wgt, long long n) {
   long long s = 0, j;

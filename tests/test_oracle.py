@@ -373,3 +373,26 @@ def test_ump_chain_start_is_exact(oracle, dtype):
     exp = out["zero"].reshape(n, 16).copy()
     exp[small] *= dtype(2.0 ** 32)
     assert np.array_equal(bits(exp.reshape(-1)), bits(e3))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("fma", [False, True])
+def test_generic_openmp_equals_serial(dtype, fma):
+    """The OpenMP generic loop (the protein CPU baseline) gives the serial
+    loop's x3, scaler bytes and weighted sum at ragged thread splits."""
+    import oracle as O
+
+    rng = np.random.default_rng(3)
+    S, Cc = 20, 4
+    for n in (1, 7, 1001):
+        x1 = rng.random(S * Cc * n).astype(dtype)
+        x1.reshape(n, -1)[0::3] *= 1e-14
+        x2 = rng.random(S * Cc * n).astype(dtype)
+        EV = (rng.random(S * S) - 0.25).astype(dtype)
+        L, R = (rng.random(Cc * S * S).astype(dtype) for _ in range(2))
+        w = rng.integers(0, 4, n).astype(np.int32)
+        ser = O.plf_generic(S, Cc, x1, x2, EV, L, R, w, fma=fma)
+        for threads in (1, 3, 8):
+            par = O.plf_generic(S, Cc, x1, x2, EV, L, R, w, fma=fma, threads=threads)
+            assert np.array_equal(ser[0], par[0]) and np.array_equal(ser[1], par[1])
+            assert ser[2] == par[2]
