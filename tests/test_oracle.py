@@ -396,3 +396,31 @@ def test_generic_openmp_equals_serial(dtype, fma):
             par = O.plf_generic(S, Cc, x1, x2, EV, L, R, w, fma=fma, threads=threads)
             assert np.array_equal(ser[0], par[0]) and np.array_equal(ser[1], par[1])
             assert ser[2] == par[2]
+
+
+@pytest.mark.parametrize("S", [4, 20])
+def test_generic_against_independent_numpy(oracle, S):
+    """The generic S-state restatement (the protein oracle, an unpinned
+    extension of the pinned loop) against an independent numpy statement of
+    the same mathematics: U = P_L x1, V = P_R x2 per category, x3 = EV^T (U * V),
+    rescaled by 2^32 where every value of the site is below 2^-32.  Different
+    summation order, so within 1e-13 relative (positive inputs: no
+    cancellation); identical scaler decisions and weighted sum."""
+    rng = np.random.default_rng(20 + S)
+    Cc, n = 4, 777
+    x1 = rng.random((n, Cc, S))
+    x1[0::5] *= 1e-14                      # clearly rescaled sites
+    x2 = rng.random((n, Cc, S))
+    P_L, P_R = rng.random((Cc, S, S)), rng.random((Cc, S, S))
+    EV = rng.random((S, S))
+    w = rng.integers(0, 5, n).astype(np.int32)
+    g3, gsc, ginc = oracle.plf_generic(S, Cc, x1.ravel(), x2.ravel(), EV.ravel(), P_L.ravel(),
+                                       P_R.ravel(), w)
+    U = np.einsum("ckl,icl->ick", P_L, x1)
+    Vv = np.einsum("ckl,icl->ick", P_R, x2)
+    x3 = np.einsum("ick,kl->icl", U * Vv, EV)
+    sc = np.all(np.abs(x3.reshape(n, -1)) < 2.0 ** -32, axis=1)
+    x3[sc] *= 2.0 ** 32
+    assert np.array_equal(gsc.astype(bool), sc) and sc.sum() >= n // 5
+    assert ginc == int((sc * w).sum())
+    assert np.allclose(g3, x3.ravel(), rtol=1e-13, atol=0)
