@@ -5,7 +5,7 @@
 //                    [--target hw|sw_emu] [--dtype f32|f64] [--layout comb|sep]
 //                    [--aie window|stream] [--window BYTES] [--seed S]
 //                    [--dump PREFIX] [--no-check] [--quiet]
-//                    [--no-intermediate] [--csv FILE]
+//                    [--no-intermediate] [--csv FILE] [--devices D0,D1,...]
 //
 // Mirrors host_mem.cpp:
 //   * argv shape <sites> <calls> <instances> (host_mem.cpp:13-38); the xclbin
@@ -32,6 +32,11 @@
 //   * --csv FILE: the per-call timing CSV of write_to_csv (timing.h:153-194):
 //     hm<k>,msasm<k>,mh<k> columns per instance, or preparation,plf,scaling
 //     with --no-intermediate;
+//   * --devices D0,D1,...: instance k runs on GPU D[k % count] (one plfx
+//     context per GPU, the instance's buffers, streams and events on it):
+//     the reference's instance partition (include.h:181-195) spread over the
+//     GPUs of a node the way its instances share one card; a device may be
+//     listed twice (two contexts on one GPU).  Default: GPU 0;
 //   * host scaler reduction sum scaler[j]*wgt[j] (host_mem.cpp:384-388);
 //   * the correctness check of host_mem.cpp:403-442: this program's own CPU
 //     plf() (below, plf.cpp:19-65 restated) run plf_calls times and timed,
@@ -85,13 +90,14 @@ struct Opts {
   std::string csv;
   bool quiet = false;
   bool no_intermediate = false;
+  std::vector<int> devices{0};
 };
 
 Opts parse(int argc, char **argv) {
   if (argc < 4)
     die("usage: plfx_host <alignment sites> <plf calls> <parallel instances> [--target hw|sw_emu] "
         "[--dtype f32|f64] [--layout comb|sep] [--aie window|stream] [--window BYTES] [--seed S] "
-        "[--dump PREFIX] [--no-check] [--quiet] [--no-intermediate] [--csv FILE]");
+        "[--dump PREFIX] [--no-check] [--quiet] [--no-intermediate] [--csv FILE] [--devices D0,D1,...]");
   Opts o;
   try {
     o.sites = std::stoull(argv[1]);
@@ -140,6 +146,20 @@ Opts parse(int argc, char **argv) {
       o.no_intermediate = true;
     } else if (a == "--csv") {
       o.csv = next();
+    } else if (a == "--devices") {
+      o.devices.clear();
+      const std::string v = next();
+      size_t p = 0;
+      while (p <= v.size()) {
+        const size_t q = std::min(v.find(',', p), v.size());
+        try {
+          o.devices.push_back(std::stoi(v.substr(p, q - p)));
+        } catch (const std::exception &) {
+          die("bad device list " + v);
+        }
+        if (o.devices.back() < 0) die("bad device list " + v);
+        p = q + 1;
+      }
     } else {
       die("unknown option " + a);
     }
@@ -149,6 +169,7 @@ Opts parse(int argc, char **argv) {
   if (o.sw_emu && o.aie == plfx::STREAM && o.layout != plfx::COMBINED)
     die("stream movers exist in the COMBINED layout only");
   if (o.sw_emu && o.no_intermediate) die("--no-intermediate is a GPU (hw) run mode");
+  if (o.sw_emu && (o.devices.size() != 1 || o.devices[0] != 0)) die("--devices is a GPU (hw) option");
   return o;
 }
 
@@ -215,6 +236,11 @@ int run(const Opts &o) {
     std::printf("| element type:           | %54s |\n", o.f64 ? "f64" : "f32");
     std::printf("| layout / aie / window:  | %34s %8s %10u |\n", o.layout == plfx::COMBINED ? "COMBINED" : "SEPARATE",
                 o.aie == plfx::WINDOW ? "window" : "stream", o.window);
+    if (!o.sw_emu) {
+      std::string dl;
+      for (size_t q = 0; q < o.devices.size(); q++) dl += (q ? "," : "") + std::to_string(o.devices[q]);
+      std::printf("| GPUs (instance k: #k%%n): | %54s |\n", dl.c_str());
+    }
     std::printf("==================================================================================\n");
     std::printf("|                         |       alignments |         elements |     size (bytes) |\n");
     std::printf("| instance left:          | %16llu | %16llu | %16llu |\n", (unsigned long long)n0,
@@ -270,9 +296,16 @@ int run(const Opts &o) {
     roctxRangePop();
     wall_ms = ms_since(std::chrono::steady_clock::now());
   } else {
-    plfx_ctx *ctx = nullptr;
-    int rc = plfx_ctx_create(0, &ctx);
-    if (rc != PLFX_OK) die("plfx_ctx_create failed: " + std::to_string(rc));
+    // one context per listed GPU; instance k on list entry k % count
+    const size_t nd = o.devices.size();
+    std::vector<plfx_ctx *> ctxs(nd, nullptr);
+    int rc = PLFX_OK;
+    for (size_t q = 0; q < nd; q++) {
+      rc = plfx_ctx_create(o.devices[q], &ctxs[q]);
+      if (rc != PLFX_OK) die("plfx_ctx_create(" + std::to_string(o.devices[q]) + ") failed: " + std::to_string(rc));
+    }
+    auto slot = [&](uint32_t k) { return (size_t)k % nd; };
+    auto on = [&](uint32_t k) { HIPCHK(hipSetDevice(o.devices[slot(k)])); };
     // per-instance pinned host buffers, device buffers, the reference's three
     // queues (main / right / output, host_mem.cpp:123-127) as HIP streams, and
     // the events that join them
@@ -281,28 +314,33 @@ int run(const Opts &o) {
     std::vector<hipStream_t> st(P), sr(P), so(P);
     std::vector<hipEvent_t> eb(P * o.calls), e1(P * o.calls), e2(P * o.calls), ee(P * o.calls);
     std::vector<hipEvent_t> j_up(P), j_run(P), j_dn(P);  // joins: right upload, kernel, side download
-    hipEvent_t e0;
+    std::vector<hipEvent_t> e0(P);  // per instance: events time against one on their own GPU
     for (uint32_t k = 0; k < P; k++) {
-      HIPCHK(hipHostMalloc((void **)&hL[k], tb.instance_elements_left() * es));
-      HIPCHK(hipHostMalloc((void **)&hR[k], tb.instance_elements_right() * es));
+      on(k);
+      HIPCHK(hipHostMalloc((void **)&hL[k], tb.instance_elements_left() * es, hipHostMallocPortable));
+      HIPCHK(hipHostMalloc((void **)&hR[k], tb.instance_elements_right() * es, hipHostMallocPortable));
       HIPCHK(hipMalloc((void **)&dL[k], tb.instance_elements_left() * es));
       HIPCHK(hipMalloc((void **)&dR[k], tb.instance_elements_right() * es));
       HIPCHK(hipMalloc((void **)&dO[k], std::max<uint64_t>(tb.instance_elements_out(), 16) * es));
       HIPCHK(hipMalloc((void **)&dS[k], std::max<uint64_t>(n0, 1)));
       for (auto *q : {&st, &sr, &so}) HIPCHK(hipStreamCreateWithFlags(&(*q)[k], hipStreamNonBlocking));
       for (auto *q : {&j_up, &j_run, &j_dn}) HIPCHK(hipEventCreateWithFlags(&(*q)[k], hipEventDisableTiming));
+      HIPCHK(hipEventCreate(&e0[k]));
+      for (uint32_t i = 0; i < o.calls; i++)
+        for (auto *v : {&eb, &e1, &e2, &ee}) HIPCHK(hipEventCreate(&(*v)[(size_t)i * P + k]));
       if (!o.no_intermediate) tb.pack<T>(k, ev, bl, br, xl.data(), xr.data(), hL[k], hR[k]);
     }
-    for (auto *v : {&eb, &e1, &e2, &ee})
-      for (auto &e : *v) HIPCHK(hipEventCreate(&e));
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipDeviceSynchronize());
+    for (size_t q = 0; q < nd; q++) {
+      HIPCHK(hipSetDevice(o.devices[q]));
+      HIPCHK(hipDeviceSynchronize());
+    }
     auto t0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point a) {
       return std::chrono::duration<double, std::milli>(a - t0).count();
     };
     auto run_instance = [&](uint32_t k) {
       const uint64_t nk = tb.alignments_per_instance(k);
+      plfx_ctx *ctx = ctxs[slot(k)];
       rc = plfx_instance_run(ctx, dL[k], dR[k], dO[k], dS[k], (uint32_t)nk,
                              o.aie == plfx::WINDOW ? o.window : 0, o.layout, dt, st[k]);
       if (rc != PLFX_OK) die(std::string("plfx_instance_run: ") + plfx_last_error(ctx));
@@ -312,7 +350,7 @@ int run(const Opts &o) {
     // and each plf call's enqueue + wait; the H2D / kernel / D2H regions
     // themselves are the events below and the kernel trace
     roctxRangePush("plfx_host roundtrip");
-    HIPCHK(hipEventRecord(e0, st[0]));
+    for (uint32_t k = 0; k < P; k++) HIPCHK(hipEventRecord(e0[k], st[k]));
     for (uint32_t i = 0; i < o.calls; i++) {
       roctxRangePush("plf call (all instances)");
       if (!o.no_intermediate) {
@@ -376,25 +414,27 @@ int run(const Opts &o) {
     wall_ms = ms_since(std::chrono::steady_clock::now());
     if (!o.no_intermediate) {
       for (size_t q = 0; q < reg.size(); q++) {
+        const hipEvent_t z = e0[q % P];
         float a, b, c, d;
-        HIPCHK(hipEventElapsedTime(&a, e0, eb[q]));
-        HIPCHK(hipEventElapsedTime(&b, e0, e1[q]));
-        HIPCHK(hipEventElapsedTime(&c, e0, e2[q]));
-        HIPCHK(hipEventElapsedTime(&d, e0, ee[q]));
+        HIPCHK(hipEventElapsedTime(&a, z, eb[q]));
+        HIPCHK(hipEventElapsedTime(&b, z, e1[q]));
+        HIPCHK(hipEventElapsedTime(&c, z, e2[q]));
+        HIPCHK(hipEventElapsedTime(&d, z, ee[q]));
         reg[q] = Regions{a, b, c, d};
       }
     }
     for (uint32_t k = 0; k < P; k++) {
-      (void)plfx_ctx_release_stream(ctx, st[k]);  // before the stream is destroyed (plfx.h)
+      on(k);
+      (void)plfx_ctx_release_stream(ctxs[slot(k)], st[k]);  // before the stream is destroyed (plfx.h)
       (void)hipHostFree(hL[k]); (void)hipHostFree(hR[k]);
       (void)hipFree(dL[k]); (void)hipFree(dR[k]); (void)hipFree(dO[k]); (void)hipFree(dS[k]);
       for (auto *q : {&st, &sr, &so}) (void)hipStreamDestroy((*q)[k]);
       for (auto *q : {&j_up, &j_run, &j_dn}) (void)hipEventDestroy((*q)[k]);
+      (void)hipEventDestroy(e0[k]);
+      for (uint32_t i = 0; i < o.calls; i++)
+        for (auto *v : {&eb, &e1, &e2, &ee}) (void)hipEventDestroy((*v)[(size_t)i * P + k]);
     }
-    for (auto *v : {&eb, &e1, &e2, &ee})
-      for (auto &e : *v) (void)hipEventDestroy(e);
-    (void)hipEventDestroy(e0);
-    plfx_ctx_destroy(ctx);
+    for (plfx_ctx *c : ctxs) plfx_ctx_destroy(c);
   }
 
   // ---- correctness check and the CPU "Reference" region (host_mem.cpp:403-442)

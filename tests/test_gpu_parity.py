@@ -350,13 +350,18 @@ def test_host_driver_end_to_end(oracle, tmp_path):
     events; dumped CLVs/scalers equal the oracle on the same host_mem-protocol
     inputs (std::mt19937, same seed).  --no-intermediate is the reference's
     NO_INTERMEDIATE_RESULTS mode (host_mem.cpp:327-392,454-468) and --csv its
-    write_to_csv (timing.h:153-194)."""
+    write_to_csv (timing.h:153-194); --devices spreads the instances over a
+    GPU list, one context per entry."""
     exe = PKG / "build" / "plfx_host"
     assert exe.exists()
     cases = ((np.float32, ["--dtype", "f32", "--layout", "comb", "--window", "1024"], False),
              (np.float64, ["--dtype", "f64", "--layout", "sep", "--window", "8192"], False),
              (np.float64, ["--dtype", "f64", "--layout", "comb", "--window", "8192"], True),
-             (np.float32, ["--dtype", "f32", "--layout", "sep", "--window", "1024"], True))
+             (np.float32, ["--dtype", "f32", "--layout", "sep", "--window", "1024"], True),
+             # instances over a GPU list (one context per entry; the box has one GPU,
+             # so two contexts on it): instances 0 and 2 on context 0, 1 on context 1
+             (np.float64, ["--dtype", "f64", "--layout", "sep", "--window", "8192", "--devices", "0,0"], False),
+             (np.float32, ["--dtype", "f32", "--layout", "comb", "--window", "1024", "--devices", "0,0"], True))
     for ci, (dtype, args, noint) in enumerate(cases):
         n, calls, P = 3001, 2, 3
         pre = str(tmp_path / f"out{ci}_{np.dtype(dtype).name}")
