@@ -9,11 +9,18 @@
 //
 //   usage: plfx_tree <taxa (power of 2)> <sites> <sweeps>
 //                    [--dtype f32|f64] [--tips] [--alpha A] [--seed S] [--quiet]
-//                    [--states 4|20] [--fma]
+//                    [--states 4|20] [--fma] [--devices D0,D1,...]
 //
 // --states 20: a 20-state reversible model (fixed exchangeabilities and
 // frequencies), amino-acid tips (codes 0..19, 5 % X), the protein kernels
 // (exact, or --fma on the matrix cores), tree levels as batched launches.
+//
+// --devices D0,D1,...: the alignment's sites split over the listed GPUs by
+// the reference's ceil rule (plfx_shard, include.h:181-189), one context per
+// entry; every GPU sweeps the whole tree over its own site block (its P
+// matrices, traversal and root lnL), the host adds the per-GPU lnL in list
+// order -- the same value as one GPU up to the summation order (a device may
+// be listed twice: two contexts on one GPU).
 //
 // Prints the per-sweep device time, the node-site rate and the lnL (%.17g);
 // with the same seed, dense tips and coded tips give the identical lnL (the tip
@@ -71,12 +78,27 @@ struct Opts {
   int states = 4;
   double alpha = 0.5;
   uint32_t seed = 20250117u;
+  std::vector<int> devices{0};
+};
+
+// One GPU's share: its context, its site block [off, off + n) and the device
+// state of the whole tree over that block.
+template <typename T>
+struct Part {
+  int device = 0;
+  plfx_ctx *ctx = nullptr;
+  int64_t off = 0, n = 0;
+  std::vector<void *> clv;
+  std::vector<const uint8_t *> tip;
+  double *d_eig = nullptr, *d_rates = nullptr, *d_blen = nullptr, *d_w = nullptr, *d_lnl = nullptr;
+  T *d_EV = nullptr, *d_pm = nullptr;
+  int64_t *d_sums = nullptr;
+  hipStream_t st = nullptr;
+  std::vector<hipEvent_t> ev;
 };
 
 template <typename T>
 int run(const Opts &o) {
-  plfx_ctx *ctx = nullptr;
-  if (plfx_ctx_create(0, &ctx) != PLFX_OK) die("no gfx950 device");
   const int dt = o.f64 ? PLFX_F64 : PLFX_F32;
   const int T_ = o.taxa, nops = T_ - 1, nslots = 2 * T_ - 1;
   const int64_t n = o.sites;
@@ -131,69 +153,101 @@ int run(const Opts &o) {
       }
     }
 
-  // device state
-  std::vector<void *> clv(nslots, nullptr);
-  std::vector<const uint8_t *> tip(nslots, nullptr);
-  for (int t = 0; t < T_; t++) {
-    if (o.tips) {
-      tip[t] = upload(codes[t]);
-    } else {  // dense tip CLV: x[i][c][s] = bit s of the code (DNA) / state s of the code
-      std::vector<T> x((size_t)V * n);
-      for (int64_t i = 0; i < n; i++)
-        for (int c = 0; c < 4; c++)
-          for (int s = 0; s < S; s++) {
-            const int code = codes[t][i];
-            const bool on = S == 4 ? ((code >> s) & 1) : (code >= 20 || code == s);
-            x[(size_t)V * i + S * c + s] = (T)(on ? 1 : 0);
-          }
-      clv[t] = upload(x);
+  // device state: one Part per listed GPU, its site block by the reference's
+  // ceil rule
+  const uint32_t nd = (uint32_t)o.devices.size();
+  std::vector<Part<T>> parts(nd);
+  for (uint32_t q = 0; q < nd; q++) {
+    Part<T> &p = parts[q];
+    p.device = o.devices[q];
+    uint64_t off = 0, cnt = 0;
+    if (plfx_shard((uint64_t)n, nd, q, &off, &cnt) != PLFX_OK) die("too many devices for this many sites");
+    p.off = (int64_t)off;
+    p.n = (int64_t)cnt;
+    if (plfx_ctx_create(p.device, &p.ctx) != PLFX_OK) die("no gfx950 device " + std::to_string(p.device));
+    HIPCHK(hipSetDevice(p.device));
+    p.clv.assign(nslots, nullptr);
+    p.tip.assign(nslots, nullptr);
+    for (int t = 0; t < T_; t++) {
+      if (o.tips) {
+        p.tip[t] = upload(std::vector<uint8_t>(codes[t].begin() + p.off, codes[t].begin() + p.off + p.n));
+      } else {  // dense tip CLV: x[i][c][s] = bit s of the code (DNA) / state s of the code
+        std::vector<T> x((size_t)V * p.n);
+        for (int64_t i = 0; i < p.n; i++)
+          for (int c = 0; c < 4; c++)
+            for (int s = 0; s < S; s++) {
+              const int code = codes[t][p.off + i];
+              const bool on = S == 4 ? ((code >> s) & 1) : (code >= 20 || code == s);
+              x[(size_t)V * i + S * c + s] = (T)(on ? 1 : 0);
+            }
+        p.clv[t] = upload(x);
+      }
     }
+    for (int s = T_; s < nslots; s++) p.clv[s] = dalloc<T>((size_t)V * p.n);
+    p.d_eig = upload(eig);
+    p.d_rates = upload(rates);
+    p.d_blen = upload(blen);
+    std::vector<T> EVt(EVd.begin(), EVd.end());
+    p.d_EV = upload(EVt);
+    p.d_pm = dalloc<T>((size_t)2 * nops * M);
+    p.d_w = upload(w);
+    p.d_lnl = dalloc<double>(1);
+    p.d_sums = dalloc<int64_t>(nops);
+    p.st = reinterpret_cast<hipStream_t>(plfx_ctx_stream(p.ctx));
+    p.ev.resize(o.sweeps + 1);
+    for (auto &e : p.ev) HIPCHK(hipEventCreate(&e));
   }
-  for (int s = T_; s < nslots; s++) clv[s] = dalloc<T>((size_t)V * n);
-  double *d_eig = upload(eig), *d_rates = upload(rates), *d_blen = upload(blen);
-  std::vector<T> EVt(EVd.begin(), EVd.end());
-  T *d_EV = upload(EVt), *d_pm = dalloc<T>((size_t)2 * nops * M);
-  double *d_w = upload(w), *d_lnl = dalloc<double>(1);
-  int64_t *d_sums = dalloc<int64_t>(nops);
-  hipStream_t st = reinterpret_cast<hipStream_t>(plfx_ctx_stream(ctx));
-  std::vector<hipEvent_t> ev(o.sweeps + 1);
-  for (auto &e : ev) HIPCHK(hipEventCreate(&e));
 
-  auto sweep = [&]() {
-    PLFXCHK(ctx, plfx_pmatrix(ctx, dt, S, PLFX_PMAT_STATE, d_eig, d_rates, 4, d_blen, 2 * nops, d_pm, st));
-    PLFXCHK(ctx, plfx_traverse_tips(ctx, dt, S, o.fma ? PLFX_FMA : PLFX_EXACT, ops.data(), nops, clv.data(),
-                                    o.tips ? tip.data() : nullptr, nslots, d_pm, nops, d_EV, n,
-                                    nullptr, nullptr, d_sums, nullptr, st));
-    PLFXCHK(ctx, plfx_root_lnl(ctx, dt, S, clv[nslots - 1], n, nullptr, d_w, nullptr, d_sums, nops,
-                               d_lnl, nullptr, st));
+  auto sweep = [&](Part<T> &p) {  // enqueued on the part's stream, returns at once
+    plfx_ctx *ctx = p.ctx;
+    PLFXCHK(ctx, plfx_pmatrix(ctx, dt, S, PLFX_PMAT_STATE, p.d_eig, p.d_rates, 4, p.d_blen, 2 * nops, p.d_pm,
+                              p.st));
+    PLFXCHK(ctx, plfx_traverse_tips(ctx, dt, S, o.fma ? PLFX_FMA : PLFX_EXACT, ops.data(), nops, p.clv.data(),
+                                    o.tips ? p.tip.data() : nullptr, nslots, p.d_pm, nops, p.d_EV, p.n,
+                                    nullptr, nullptr, p.d_sums, nullptr, p.st));
+    PLFXCHK(ctx, plfx_root_lnl(ctx, dt, S, p.clv[nslots - 1], p.n, nullptr, p.d_w, nullptr, p.d_sums, nops,
+                               p.d_lnl, nullptr, p.st));
   };
-  sweep();  // warm-up
-  HIPCHK(hipStreamSynchronize(st));
-  HIPCHK(hipEventRecord(ev[0], st));
-  for (int i = 0; i < o.sweeps; i++) {
-    sweep();
-    HIPCHK(hipEventRecord(ev[i + 1], st));
-  }
-  HIPCHK(hipStreamSynchronize(st));
+  for (auto &p : parts) sweep(p);  // warm-up
+  for (auto &p : parts) HIPCHK(hipStreamSynchronize(p.st));
+  for (auto &p : parts) HIPCHK(hipEventRecord(p.ev[0], p.st));
+  for (int i = 0; i < o.sweeps; i++)
+    for (auto &p : parts) {  // every GPU's sweep i before any GPU's sweep i + 1
+      sweep(p);
+      HIPCHK(hipEventRecord(p.ev[i + 1], p.st));
+    }
+  for (auto &p : parts) HIPCHK(hipStreamSynchronize(p.st));
   double lnl = 0.0;
-  HIPCHK(hipMemcpy(&lnl, d_lnl, sizeof lnl, hipMemcpyDeviceToHost));
-  std::vector<int64_t> sums(nops);
-  HIPCHK(hipMemcpy(sums.data(), d_sums, nops * sizeof(int64_t), hipMemcpyDeviceToHost));
   long long scale_events = 0;
-  for (int64_t v : sums) scale_events += v;
+  std::vector<int64_t> sums(nops);
+  for (auto &p : parts) {  // list order: a fixed summation order
+    double v = 0.0;
+    HIPCHK(hipMemcpy(&v, p.d_lnl, sizeof v, hipMemcpyDeviceToHost));
+    lnl += v;
+    HIPCHK(hipMemcpy(sums.data(), p.d_sums, nops * sizeof(int64_t), hipMemcpyDeviceToHost));
+    for (int64_t s : sums) scale_events += s;
+  }
+  // a sweep's time: the slowest GPU's
   float tot_ms = 0.f, mn = 1e30f, mx = 0.f;
   for (int i = 0; i < o.sweeps; i++) {
-    float ms;
-    HIPCHK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+    float ms = 0.f;
+    for (auto &p : parts) {
+      float m;
+      HIPCHK(hipEventElapsedTime(&m, p.ev[i], p.ev[i + 1]));
+      ms = std::max(ms, m);
+    }
     tot_ms += ms;
     mn = std::min(mn, ms);
     mx = std::max(mx, ms);
   }
   const double avg = tot_ms / o.sweeps;
   if (!o.quiet) {
+    std::string dl;
+    for (uint32_t q = 0; q < nd; q++) dl += (q ? "," : "") + std::to_string(o.devices[q]);
     std::printf("==================================================================================\n");
     std::printf("| taxa / inner nodes:     | %24d / %26d |\n", T_, nops);
     std::printf("| alignment sites:        | %54lld |\n", (long long)n);
+    std::printf("| GPUs (site blocks):     | %54s |\n", dl.c_str());
     std::printf("| element type / tips:    | %24s / %26s |\n", o.f64 ? "f64" : "f32",
                 o.tips ? "state codes" : "dense CLVs");
     std::printf("| states / mode:          | %24d / %26s |\n", S, o.fma ? "FMA" : "exact");
@@ -205,11 +259,14 @@ int run(const Opts &o) {
     std::printf("==================================================================================\n");
   }
   std::printf("lnL = %.17g\n", lnl);
-  for (auto &e : ev) (void)hipEventDestroy(e);
-  for (int s = 0; s < nslots; s++) (void)hipFree(s < T_ && o.tips ? (void *)tip[s] : clv[s]);
-  (void)hipFree(d_eig); (void)hipFree(d_rates); (void)hipFree(d_blen); (void)hipFree(d_EV);
-  (void)hipFree(d_pm); (void)hipFree(d_w); (void)hipFree(d_lnl); (void)hipFree(d_sums);
-  plfx_ctx_destroy(ctx);
+  for (auto &p : parts) {
+    HIPCHK(hipSetDevice(p.device));
+    for (auto &e : p.ev) (void)hipEventDestroy(e);
+    for (int s = 0; s < nslots; s++) (void)hipFree(s < T_ && o.tips ? (void *)p.tip[s] : p.clv[s]);
+    (void)hipFree(p.d_eig); (void)hipFree(p.d_rates); (void)hipFree(p.d_blen); (void)hipFree(p.d_EV);
+    (void)hipFree(p.d_pm); (void)hipFree(p.d_w); (void)hipFree(p.d_lnl); (void)hipFree(p.d_sums);
+    plfx_ctx_destroy(p.ctx);
+  }
   return std::isfinite(lnl) ? 0 : 3;
 }
 
@@ -218,7 +275,7 @@ int run(const Opts &o) {
 int main(int argc, char **argv) {
   if (argc < 4)
     die("usage: plfx_tree <taxa (power of 2)> <sites> <sweeps> [--dtype f32|f64] [--tips] "
-        "[--alpha A] [--seed S] [--quiet] [--states 4|20] [--fma]");
+        "[--alpha A] [--seed S] [--quiet] [--states 4|20] [--fma] [--devices D0,D1,...]");
   Opts o;
   try {
     o.taxa = std::stoi(argv[1]);
@@ -251,6 +308,20 @@ int main(int argc, char **argv) {
       if (o.states != 4 && o.states != 20) die("states must be 4 or 20");
     } else if (a == "--fma") {
       o.fma = true;
+    } else if (a == "--devices") {
+      o.devices.clear();
+      const std::string v = next();
+      size_t p = 0;
+      while (p <= v.size()) {
+        const size_t q = std::min(v.find(',', p), v.size());
+        try {
+          o.devices.push_back(std::stoi(v.substr(p, q - p)));
+        } catch (const std::exception &) {
+          die("bad device list " + v);
+        }
+        if (o.devices.back() < 0) die("bad device list " + v);
+        p = q + 1;
+      }
     } else {
       die("unknown option " + a);
     }

@@ -522,7 +522,8 @@ def test_tree_driver_end_to_end(oracle):
     """The C++ tree driver (host/plfx_tree.cpp: model -> device P -> fused
     traversal -> root lnL): its lnL equals an independent numpy pruning of the
     same inputs within 1e-10; dense tips, coded tips and PLFX_FUSE=0 give the
-    bit-identical lnL; f32 within 1e-4."""
+    bit-identical lnL; f32 within 1e-4; --devices (sites split over a GPU
+    list) within 1e-12 of one GPU."""
     import os
     import subprocess
     from pathlib import Path
@@ -546,6 +547,14 @@ def test_tree_driver_end_to_end(oracle):
     assert abs(float(dense) - expect) <= 1e-10 * abs(expect)
     f32 = float(lnl("--dtype", "f32", "--tips"))
     assert abs(f32 - expect) <= 1e-4 * abs(expect)
+    # sites split over a GPU list (one context per entry; two on the box's one
+    # GPU, three blocks of 1000 sites): per-block lnLs summed in list order
+    for extra in (["--devices", "0,0"], ["--tips", "--devices", "0,0,0"]):
+        split = float(lnl(*extra))
+        assert abs(split - float(dense)) <= 1e-12 * abs(float(dense))
+        assert abs(split - expect) <= 1e-10 * abs(expect)
+    prot = [float(lnl("--states", "20", "--fma", "--tips", *d)) for d in ([], ["--devices", "0,0"])]
+    assert abs(prot[1] - prot[0]) <= 1e-12 * abs(prot[0])
 
 
 def _random_tree_ops(rng, ntips, recycle):
