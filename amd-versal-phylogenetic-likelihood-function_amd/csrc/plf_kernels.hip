@@ -372,8 +372,9 @@ hipError_t launch_deep_t(const dev::DeepDesc &d, const T *EV, const int32_t *wgt
   // 2^20-site f64 pass (same process: 3358 -> 3116 us,
   // profiles/r03_tune_deep_dyn.log; bench tree64 f64 --tips 1688 -> 1643 us,
   // f32 --tips 875 -> 861, f32 dense equal, profiles/r03_ab_deep_dyn.log)
-  if (ws) return launch_deep_k<D, T, kSum, U, kThreads, kTips, true>(d, EV, wgt, n, ws, max_blocks, s, tipvec);
-  return launch_deep_k<D, T, kSum, U, kThreads, kTips, false>(d, EV, wgt, n, ws, max_blocks, s, tipvec);
+  // (the traversal always has a stream workspace when it launches a pass)
+  if (!ws) return hipErrorInvalidValue;
+  return launch_deep_k<D, T, kSum, U, kThreads, kTips, true>(d, EV, wgt, n, ws, max_blocks, s, tipvec);
 }
 
 }  // namespace

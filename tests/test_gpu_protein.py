@@ -533,50 +533,120 @@ def test_protein_root_lnl_tiles(ctx, oracle, dtype):
     assert abs(float(out.item()) - exp) <= 1e-12 * abs(exp)
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("with_sum", [True, False])
 @pytest.mark.parametrize("warm", [False, True])
-def test_protein_tiptip_in_graph_capture(ctx, oracle, warm):
+def test_protein_tiptip_in_graph_capture(ctx, oracle, dtype, fma, with_sum, warm):
     """A tip/tip protein node captured in a HIP graph: on a stream whose
     combination tables do not exist yet (cold) the node takes the direct
-    kernel (no allocation inside a capture); on a warmed stream the capture
-    holds the combination-table launch and the gather.  Replays are
-    bit-identical to the oracle either way."""
+    tip/tip kernel of its mode (no allocation inside a capture); on a warmed
+    stream the capture holds the combination-table launch and the gather.
+    Replays are bit-identical to the oracle either way, with and without the
+    weighted sum."""
     import torch
 
     n = 5003
     rng = np.random.default_rng(31)
-    _, _, EV, left, right, w = gen(n, np.float64, 12)
+    _, _, EV, left, right, w = gen(n, dtype, 12)
+    left = (left * 1e-11).astype(dtype)  # a mix of rescaled sites
     c1, c2 = oracle.random_protein_codes(rng, n, 0.3), oracle.random_protein_codes(rng, n, 0.3)
-    e1, e2 = oracle.expand_protein_tips(c1, np.float64), oracle.expand_protein_tips(c2, np.float64)
-    f3, fsc, finc = oracle.plf_generic(S, CAT, e1, e2, EV, left, right, w)
+    e1, e2 = oracle.expand_protein_tips(c1, dtype), oracle.expand_protein_tips(c2, dtype)
+    f3, fsc, finc = oracle.plf_generic(S, CAT, e1, e2, EV, left, right, w, fma=fma)
+    assert 0 < fsc.sum() < n
     t = [dev(a) for a in (c1, c2, EV, left, right, w)]
-    x3 = torch.empty(V * n, dtype=torch.float64, device="cuda")
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    x3 = torch.empty(V * n, dtype=tt, device="cuda")
     sc = torch.empty(n, dtype=torch.uint8, device="cuda")
-    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    s = torch.zeros(1, dtype=torch.int64, device="cuda") if with_sum else None
     st = torch.cuda.Stream()
 
     def call():
         ctx.plf_tips_dev(x3, t[2], n, t[3], t[4], tip1=t[0], tip2=t[1], wgt=t[5], scaler=sc,
-                         scaler_sum=s, states=S, stream=st)
+                         scaler_sum=s, states=S, fma=fma, stream=st)
 
     torch.cuda.synchronize()
     if warm:
         call()
     else:  # the stream's workspace exists, its combination tables do not
-        xd = dev(np.zeros(V * n))
+        xd = dev(np.zeros(V * n, dtype))
         ctx.plf_tips_dev(x3, t[2], n, t[3], t[4], tip1=t[0], x2=xd, wgt=t[5], scaler=sc,
-                         scaler_sum=s, states=S, stream=st)
+                         scaler_sum=s, states=S, fma=fma, stream=st)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=st):
         call()
-    for _ in range(3):
+    for _ in range(2):
         x3.zero_()
-        s.zero_()
+        if s is not None:
+            s.zero_()
         torch.cuda.synchronize()
         g.replay()
         torch.cuda.synchronize()
         assert np.array_equal(bits(x3.cpu().numpy()), bits(f3))
-        assert np.array_equal(sc.cpu().numpy(), fsc) and int(s.item()) == finc
+        assert np.array_equal(sc.cpu().numpy(), fsc)
+        assert s is None or int(s.item()) == finc
+    del g
+    ctx.release_stream(st)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("with_sum", [True, False])
+def test_protein_tiptip_level_in_graph_capture(ctx, oracle, dtype, fma, with_sum):
+    """A 16-taxon all-coded protein tree traversed inside a capture on a
+    stream without combination tables: its first level (8 tip/tip nodes) runs
+    the direct batched tip/tip kernels.  Replays equal a sequential oracle
+    evaluation in the same mode bit for bit (CLVs, scaler bytes, sums)."""
+    import torch
+
+    n, ntips = 900, 16
+    rng = np.random.default_rng(61)
+    ops = oracle.balanced_tree_ops(ntips)
+    nops, nslots = ops.shape[0], ntips + ops.shape[0]
+    codes = [oracle.random_protein_codes(rng, n, 0.2) for _ in range(ntips)]
+    pm = (rng.random(nops * 2 * CAT * S * S) * 0.05).astype(dtype)
+    EV = (rng.random(S * S) * 0.05).astype(dtype)
+    wgt = rng.integers(1, 4, n).astype(np.int32)
+    host = [oracle.expand_protein_tips(c, dtype) for c in codes] + [None] * nops
+    M = CAT * S * S
+    escal, einc = [], []
+    for parent, a, b, p in ops:
+        x3, sc, inc = oracle.plf_generic(S, CAT, host[a], host[b], EV, pm[2 * p * M:(2 * p + 1) * M],
+                                         pm[(2 * p + 1) * M:(2 * p + 2) * M], wgt, fma=fma)
+        host[parent] = x3
+        escal.append(sc)
+        einc.append(inc)
+    assert sum(einc) > 0
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    clv = [None] * ntips + [torch.zeros(V * n, dtype=tt, device="cuda") for _ in range(nops)]
+    tips = [dev(c) for c in codes] + [None] * nops
+    sums = torch.zeros(nops, dtype=torch.int64, device="cuda") if with_sum else None
+    scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+    pmd, EVd, wd = dev(pm), dev(EV), dev(wgt)
+    st = torch.cuda.Stream()
+    # the stream's workspace, without tables: one tip/dense node first
+    xd = torch.zeros(V * n, dtype=tt, device="cuda")
+    ctx.plf_tips_dev(clv[ntips], EVd, n, pmd[:M], pmd[M:2 * M], tip1=tips[0], x2=xd, wgt=wd,
+                     states=S, fma=fma, stream=st)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        ctx.traverse(ops, clv, pmd, EVd, n, wd, scal, sums, tips=tips, states=S, fma=fma, stream=st)
+    for _ in range(2):
+        for x in clv[ntips:]:
+            x.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        for s_ in range(ntips, nslots):
+            assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
+        for j in range(nops):
+            assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+        if sums is not None:
+            assert sums.cpu().tolist() == einc
+    del g
+    ctx.release_stream(st)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
