@@ -231,13 +231,16 @@ hipError_t launch_prot_mfma_t(const DnaArgs &a, int max_blocks, hipStream_t s,
   // profiles/r03_tune_protein_dyn.log)
   auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, kTips, false>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
-  const bool dyn = kTips < 2 && a.ws && (a.n + 63) / 64 >= 32 * gx;
-  auto dyn_kernel = &dev::plf_prot_mfma_kernel<kSum, 2, kTips, true>;
-  hipLaunchKernelGGL(dyn ? dyn_kernel : kernel, dim3((unsigned)gx),
-                     dim3(kBlock), 0, s, (const double *)a.x1, (const double *)a.x2, (double *)a.x3,
-                     (const double *)a.EV, (const double *)a.left, (const double *)a.right, a.wgt,
-                     a.scaler, a.n, a.ws, a.scaler_sum, tipvec);
-  return hipGetLastError();
+  auto launch = [&](auto k) {
+    hipLaunchKernelGGL(k, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
+                       (const double *)a.x2, (double *)a.x3, (const double *)a.EV,
+                       (const double *)a.left, (const double *)a.right, a.wgt, a.scaler, a.n, a.ws,
+                       a.scaler_sum, tipvec);
+    return hipGetLastError();
+  };
+  if constexpr (kTips < 2)  // the queue form exists for dense and tip/inner nodes only
+    if (a.ws && (a.n + 63) / 64 >= 32 * gx) return launch(&dev::plf_prot_mfma_kernel<kSum, 2, kTips, true>);
+  return launch(kernel);
 }
 
 template <bool kSum, int kTips>

@@ -38,18 +38,21 @@ def _dna_tree(oracle, ntips, n, dtype, coded, seed):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-@pytest.mark.parametrize("leaves", ["dense", "coded", "mixed"])
+@pytest.mark.parametrize("leaves", ["dense", "coded", "mixed", "left"])
 @pytest.mark.parametrize("ntips,fuse", [(16, "3"), (32, "3"), (64, "3"), (64, "2"), (64, "1"), (64, "0")])
 def test_dna_traverse_without_sums(oracle, dtype, leaves, ntips, fuse, monkeypatch):
     """DNA traversals with scaler bytes but no scaler sums, under every
     schedule: six-, five- and four-level passes (PLFX_FUSE=3 at 64, 32 and 16
     taxa), three-level passes (2), level pairs (1) and level batches (0);
-    dense, coded or mixed leaves (tip/tip, tip/inner and inner/inner nodes)."""
+    dense, coded, mixed or left-coded leaves (tip/tip, tip/inner and
+    inner/inner nodes; left-coded: every leaf node tip/inner, so the
+    three-level passes take coded leaves)."""
     import plfx
     import torch
 
     n = 2049
-    coded = [{"dense": False, "coded": True, "mixed": t % 3 != 1}[leaves] for t in range(ntips)]
+    coded = [{"dense": False, "coded": True, "mixed": t % 3 != 1, "left": t % 2 == 0}[leaves]
+             for t in range(ntips)]
     ops, nslots, codes, dense, pm, EV, wgt, host = _dna_tree(oracle, ntips, n, dtype, coded, 30 + ntips)
     esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
     assert esums.sum() > 0
@@ -67,7 +70,7 @@ def test_dna_traverse_without_sums(oracle, dtype, leaves, ntips, fuse, monkeypat
         torch.cuda.synchronize()
     finally:
         c.close()
-    if fuse == "3" and leaves != "mixed":
+    if fuse == "3" and leaves in ("dense", "coded"):
         depth = {16: "deep4", 32: "deep5", 64: "deep6"}[ntips]
         assert sched[depth] == 1, sched
     for s in range(ntips, nslots):
@@ -188,3 +191,40 @@ def test_protein_traverse_without_sums(ctx, oracle, dtype, fma, with_sum):
         assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
     if with_sum:
         assert sums.cpu().tolist() == einc
+
+
+@pytest.mark.parametrize("kind", ["dense", "tip1"])
+def test_protein_fma_queue_without_sum(ctx, oracle, kind):
+    """The f64 FMA protein kernel's device-wide tile queue (from 32 tiles per
+    block: 2^20 sites) without a sum, dense and tip/dense: windows at the
+    start, middle and end checked bit for bit against the oracle's fused
+    restatement on those sites (sites are independent)."""
+    import torch
+
+    n = (1 << 20) + 37
+    rng = np.random.default_rng(20)
+    x1 = rng.random(V * n)
+    x1.reshape(n, V)[0::4] *= 1e-14
+    x2 = rng.random(V * n)
+    EV = rng.random(S * S) - 0.25
+    L, R = rng.random(CAT * S * S), rng.random(CAT * S * S)
+    if kind == "tip1":
+        L = L * 1e-11
+    w = rng.integers(0, 4, n).astype(np.int32)
+    c1 = oracle.random_protein_codes(rng, n, 0.3)
+    x3 = torch.empty(V * n, dtype=torch.float64, device="cuda")
+    sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    if kind == "dense":
+        ctx.plf_dev_gen(dev(x1), dev(x2), x3, dev(EV), dev(L), dev(R), S, dev(w), sc, None, fma=True)
+    else:
+        ctx.plf_tips_dev(x3, dev(EV), n, dev(L), dev(R), tip1=dev(c1), x2=dev(x2), wgt=dev(w), scaler=sc,
+                         scaler_sum=None, states=S, fma=True)
+    torch.cuda.synchronize()
+    g3, gsc = x3.cpu().numpy(), sc.cpu().numpy()
+    for lo in (0, n // 2 - 2048, n - 4096):
+        win = slice(lo, lo + 4096)
+        e1 = oracle.expand_protein_tips(c1[win]) if kind == "tip1" else x1[V * lo:V * (lo + 4096)]
+        f3, fsc, _ = oracle.plf_generic(S, CAT, e1, x2[V * lo:V * (lo + 4096)], EV, L, R, w[win], fma=True)
+        assert np.array_equal(bits(g3[V * lo:V * (lo + 4096)]), bits(f3)), lo
+        assert np.array_equal(gsc[win], fsc), lo
+    assert 0 < int(gsc.sum()) < n

@@ -537,13 +537,15 @@ def test_protein_root_lnl_tiles(ctx, oracle, dtype):
 @pytest.mark.parametrize("fma", [False, True])
 @pytest.mark.parametrize("with_sum", [True, False])
 @pytest.mark.parametrize("warm", [False, True])
-def test_protein_tiptip_in_graph_capture(ctx, oracle, dtype, fma, with_sum, warm):
+def test_protein_tiptip_in_graph_capture(oracle, dtype, fma, with_sum, warm):
     """A tip/tip protein node captured in a HIP graph: on a stream whose
     combination tables do not exist yet (cold) the node takes the direct
     tip/tip kernel of its mode (no allocation inside a capture); on a warmed
     stream the capture holds the combination-table launch and the gather.
     Replays are bit-identical to the oracle either way, with and without the
-    weighted sum."""
+    weighted sum.  A context of its own: a released stream's pool entry keeps
+    its tables, so a stream of the shared context may start with them."""
+    import plfx
     import torch
 
     n = 5003
@@ -560,6 +562,7 @@ def test_protein_tiptip_in_graph_capture(ctx, oracle, dtype, fma, with_sum, warm
     sc = torch.empty(n, dtype=torch.uint8, device="cuda")
     s = torch.zeros(1, dtype=torch.int64, device="cuda") if with_sum else None
     st = torch.cuda.Stream()
+    ctx = plfx.Context(0)
 
     def call():
         ctx.plf_tips_dev(x3, t[2], n, t[3], t[4], tip1=t[0], tip2=t[1], wgt=t[5], scaler=sc,
@@ -588,16 +591,19 @@ def test_protein_tiptip_in_graph_capture(ctx, oracle, dtype, fma, with_sum, warm
         assert s is None or int(s.item()) == finc
     del g
     ctx.release_stream(st)
+    ctx.close()
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("fma", [False, True])
 @pytest.mark.parametrize("with_sum", [True, False])
-def test_protein_tiptip_level_in_graph_capture(ctx, oracle, dtype, fma, with_sum):
+def test_protein_tiptip_level_in_graph_capture(oracle, dtype, fma, with_sum):
     """A 16-taxon all-coded protein tree traversed inside a capture on a
     stream without combination tables: its first level (8 tip/tip nodes) runs
     the direct batched tip/tip kernels.  Replays equal a sequential oracle
-    evaluation in the same mode bit for bit (CLVs, scaler bytes, sums)."""
+    evaluation in the same mode bit for bit (CLVs, scaler bytes, sums).  A
+    context of its own, whose pool entries have no tables yet."""
+    import plfx
     import torch
 
     n, ntips = 900, 16
@@ -625,6 +631,7 @@ def test_protein_tiptip_level_in_graph_capture(ctx, oracle, dtype, fma, with_sum
     scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
     pmd, EVd, wd = dev(pm), dev(EV), dev(wgt)
     st = torch.cuda.Stream()
+    ctx = plfx.Context(0)
     # the stream's workspace, without tables: one tip/dense node first
     xd = torch.zeros(V * n, dtype=tt, device="cuda")
     ctx.plf_tips_dev(clv[ntips], EVd, n, pmd[:M], pmd[M:2 * M], tip1=tips[0], x2=xd, wgt=wd,
@@ -647,6 +654,7 @@ def test_protein_tiptip_level_in_graph_capture(ctx, oracle, dtype, fma, with_sum
             assert sums.cpu().tolist() == einc
     del g
     ctx.release_stream(st)
+    ctx.close()
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
