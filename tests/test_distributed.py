@@ -67,7 +67,7 @@ def test_combine_ranks_single():
 
 # --- BASELINE configs[3] on the CPU: real nodes, the product's partition, the
 # one all-reduce, the oracle's plf() + root lnL as each rank's "GPU" ---------
-TOTAL_NODES, SITES = 11, 301
+TOTAL_NODES, SITES = 64, 301  # 64: the ceil split is defined for 2, 3 and 8 ranks
 
 
 def _node_inputs(oracle, j):
@@ -100,9 +100,9 @@ def _nodes_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_nodes_partition_lnl_allreduce_equals_single_process(oracle, world):
-    """configs[3] at world 2 and 3 (gloo): ranks take the reference's ceil
+    """configs[3] at world 2, 3 and 8 (gloo): ranks take the reference's ceil
     split of the nodes, evaluate their nodes (oracle plf + root lnL), and one
     all-reduce gives every rank the per-node lnL vector, the job lnL and the
     scaler totals of the single-process run -- bit for bit (so well inside the
@@ -187,7 +187,7 @@ def _tree_shard_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_tree_site_shards_equal_single_process(oracle, world):
     """Each rank's block sweep + the one lnL all-reduce = the whole-alignment
     tree lnL (1e-12 relative: only the summation order differs) and exactly
