@@ -138,3 +138,31 @@ def test_nodes512_full_size_windows(oracle):
         assert wl.sums.cpu().tolist() == [n // 4] * 512
         del wl
     torch.cuda.empty_cache()
+
+
+def test_eight_ranks_gloo_rehearsal():
+    """The driver's N = 8 layout rehearsed on the box's one GPU: 8 ranks under
+    torch.distributed.run (gloo, every rank's device folded onto GPU 0) for the
+    default node workload and for nodes512 with 16 nodes (2 per rank): one JSON
+    line, every rank's lnL in the one all-reduce, the scaler totals exact, and
+    the nodes512 job lnL equal to one rank's bit for bit."""
+    def run(nproc, *args):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
+               "--gpus", str(nproc), "--steps", "3", "--warmup", "1", "--no-cpu-baseline", *args]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT),
+                           env={**os.environ, "PLFX_DIST_BACKEND": "gloo", "OMP_NUM_THREADS": "2"})
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        return json.loads(lines[0])
+
+    d = run(8, "--sites", "65536", "--buffer-sets", "2")
+    assert d["n_gpus"] == 8 and d["check"] == "ok" and len(d["config"]["lnl_per_rank"]) == 8
+    assert d["config"]["scaler_events_all_ranks"] == 8 * (65536 // 4)
+    e8 = run(8, "--workload", "nodes512", "--nodes", "16", "--sites", "4099")
+    e1 = run(1, "--workload", "nodes512", "--nodes", "16", "--sites", "4099")
+    assert e8["check"] == e1["check"] == "ok" and e8["scaling"] == "strong"
+    k = "lnl_all_nodes_all_ranks"
+    assert e8["config"][k] == e1["config"][k]
+    assert e8["config"]["scaler_events_all_ranks"] == e1["config"]["scaler_events_all_ranks"] == 16 * ((4099 + 3) // 4)
