@@ -573,6 +573,26 @@ hipError_t launch_prot_tiptip_gather(int dtype, const ProtGatherDescH *d, int co
                  : launch_gather_t<float, false>(b, count, wgt, n, ws, max_blocks, s);
 }
 
+hipError_t launch_prot_tab_batch(const ProtTabDescH *d, int count, const double *EV, const int32_t *wgt,
+                                 int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s) {
+  if (count < 1 || count > kMaxBatch) return hipErrorInvalidValue;
+  dev::ProtTabBatch b{};
+  bool any_sum = false;
+  for (int i = 0; i < count; i++) {
+    static_assert(sizeof(b.d[0]) == sizeof(d[0]), "layout");
+    __builtin_memcpy(&b.d[i], &d[i], sizeof(d[i]));
+    any_sum |= d[i].scaler_sum != nullptr;
+  }
+  auto launch = [&](auto kernel, int &cache) {
+    const int64_t gx = grid_x((const void *)kernel, cache, 1, n, 64, 1, max_blocks);  // full grid per node
+    hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt, n, ws);
+    return hipGetLastError();
+  };
+  static int c_sum = 0, c_nosum = 0;
+  return any_sum ? launch(&dev::plf_prot_mfma_tab_batch_kernel<true>, c_sum)
+                 : launch(&dev::plf_prot_mfma_tab_batch_kernel<false>, c_nosum);
+}
+
 hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s,
                            int tips, const void *tipvec) {
   switch (tips) {

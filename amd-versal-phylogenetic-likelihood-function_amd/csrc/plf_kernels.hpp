@@ -61,6 +61,19 @@ constexpr int kProtCombos = 24 * 24;
 hipError_t launch_prot_tiptip_gather(int dtype, const ProtGatherDescH *d, int count, const int32_t *wgt,
                                      int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s);
 
+// f64 FMA protein nodes whose two children are tip/tip nodes held in
+// combination tables (plf_prot.hpp ProtTabDesc), batched as above.
+struct ProtTabDescH {
+  const void *tab1, *tab2;
+  const uint8_t *c1a, *c1b, *c2a, *c2b;
+  void *x3;
+  const void *left, *right;
+  uint8_t *scaler;
+  int64_t *scaler_sum;
+};
+hipError_t launch_prot_tab_batch(const ProtTabDescH *d, int count, const double *EV, const int32_t *wgt,
+                                 int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s);
+
 // Protein (S = 20) nodes batched the same way; fma as launch_plf_prot.
 hipError_t launch_plf_prot_batch(int dtype, bool fma, const NodeDescH *nodes, int count, const void *EV,
                                  const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,

@@ -543,13 +543,47 @@ struct ProtQueue {
   }
 };
 
-template <bool kSum, int kTips, bool kDyn>
+// A child tile gathered from its combination table by code pair (kTab below):
+// chunk j of the tile is site j / 40's row chunk j % 40, as tile_fetch.
+__device__ __forceinline__ void tab_fetch(const double *__restrict__ x, const uint8_t *__restrict__ ca,
+                                          const uint8_t *__restrict__ cb, int64_t b, int64_t n,
+                                          f64x2 (&pf)[ProtTile<double>::kChunks / kBlock]) {
+  using PT = ProtTile<double>;
+  const f64x2 *tab = reinterpret_cast<const f64x2 *>(x);
+  // lane l reads site l's two codes (one byte load per array for the whole
+  // tile), each chunk takes its site's code pair from that lane (the kernel
+  // runs at its 256-VGPR bound: per-chunk code loads spilled)
+  const int lane = threadIdx.x & 63;
+  const int lim = (int)(n - b < 64 ? n - b : 64);
+  const int ls = lane < lim ? lane : lim - 1;
+  const int mine = prot_code(ca[b + ls]) * kProtCodes + prot_code(cb[b + ls]);
+#pragma unroll
+  for (int i = 0; i < PT::kChunks / kBlock; i++) {
+    const int j = threadIdx.x + i * kBlock;
+    const int sl = j / PT::kChunksPerSite, q = j - sl * PT::kChunksPerSite;
+    const int combo = __shfl(mine, sl < lim ? sl : lim - 1);
+    pf[i] = sl < lim ? tab[(unsigned)(combo * PT::kChunksPerSite + q)] : f64x2{};
+  }
+}
+
+// kTab: both children are tip/tip nodes of the same traversal whose values
+// sit in their combination tables (prot_tiptip_gather_kernel below): x1 / x2
+// point at the two tables (576 code pairs x 80), t1a/t1b and t2a/t2b at each
+// child's two tip-code arrays, and a child tile is gathered from its table by
+// code pair (L2-resident, 368 KB) instead of read back from HBM.  The values
+// are the ones the gather wrote to the children's CLVs, so results are
+// bit-identical.
+template <bool kSum, int kTips, bool kDyn, bool kTab = false>
 __device__ __forceinline__ void prot_mfma_body(const double *__restrict__ x1, const double *__restrict__ x2,
                                                double *__restrict__ x3, const double *__restrict__ EV,
                                                const double *__restrict__ left, const double *__restrict__ right,
                                                const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler,
                                                int64_t n, unsigned long long *ws, int64_t *scaler_sum,
-                                               const double *__restrict__ tipvec) {
+                                               const double *__restrict__ tipvec,
+                                               const uint8_t *__restrict__ t1a = nullptr,
+                                               const uint8_t *__restrict__ t1b = nullptr,
+                                               const uint8_t *__restrict__ t2a = nullptr,
+                                               const uint8_t *__restrict__ t2b = nullptr) {
   constexpr int S = 20;
   // tips (kTips 1: x1, 2: both): the child's U^T comes from its LDS table in the
   // accumulator layout (lane: rows g + 4r and 16 + g of site lo16), no MFMA, no tile
@@ -562,8 +596,13 @@ __device__ __forceinline__ void prot_mfma_body(const double *__restrict__ x1, co
   const int lo16 = lane & 15, g = lane >> 4;
   f64x2 pf[K];
   const int64_t stride = (int64_t)gridDim.x * 64;
-  if constexpr (!T2)  // the first dense child's first tile, before the matrix fragments
-    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
+  if constexpr (!T2) {  // the first dense child's first tile, before the matrix fragments
+    if constexpr (kTab) {
+      if ((int64_t)blockIdx.x * 64 < n) tab_fetch(x1, t1a, t1b, (int64_t)blockIdx.x * 64, n, pf);
+    } else {
+      if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
+    }
+  }
   // A fragments: [0][s] -> lane holds M[row = lo16][col = 4s + g];
   // [1][s] -> M[row = 16 + lane%4][col = 4s + g] (the 4x4x4_4b form)
   double AL[2][5], AR[2][5], AE[2][5];
@@ -615,7 +654,8 @@ __device__ __forceinline__ void prot_mfma_body(const double *__restrict__ x1, co
       tile_put<double>(tile, pf);
       __syncthreads();
       if constexpr (kDyn) next = qslot;
-      tile_fetch<double>(x2, base, n, pf);
+      if constexpr (kTab) tab_fetch(x2, t2a, t2b, base, n, pf);
+      else tile_fetch<double>(x2, base, n, pf);
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         double bv[5];
@@ -650,7 +690,11 @@ __device__ __forceinline__ void prot_mfma_body(const double *__restrict__ x1, co
       __syncthreads();
       if constexpr (kDyn && T1) next = qslot;
       // next trip's first dense child: x1, or x2 when x1 is a tip
-      if (next < n) tile_fetch<double>(T1 ? x2 : x1, next, n, pf);
+      if constexpr (kTab) {
+        if (next < n) tab_fetch(x1, t1a, t1b, next, n, pf);
+      } else {
+        if (next < n) tile_fetch<double>(T1 ? x2 : x1, next, n, pf);
+      }
       if constexpr (kDyn) pq.dequeue();
 #pragma unroll
       for (int t = 0; t < 4; t++) {
@@ -769,6 +813,31 @@ plf_prot_mfma_batch_kernel(const NodeBatch nodes, const double *__restrict__ EV,
   prot_mfma_body<kSum, kTips, false>((const double *)d.x1, (const double *)d.x2, (double *)d.x3, EV,
                                      (const double *)d.left, (const double *)d.right, wgt, d.scaler, n,
                                      ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, tipvec);
+}
+
+// Batched f64 FMA protein nodes whose children are both tip/tip nodes held in
+// combination tables (kTab above): the parents of a coded tree's first level.
+struct ProtTabDesc {
+  const void *tab1, *tab2;               // the children's tables (576 x 80 f64)
+  const uint8_t *c1a, *c1b, *c2a, *c2b;  // each child's two tip-code arrays
+  void *x3;
+  const void *left, *right;
+  uint8_t *scaler;
+  int64_t *scaler_sum;
+};
+struct ProtTabBatch {
+  ProtTabDesc d[kMaxBatch];
+};
+
+template <bool kSum>
+__global__ void __launch_bounds__(kBlock, 2)
+plf_prot_mfma_tab_batch_kernel(const ProtTabBatch b, const double *__restrict__ EV,
+                               const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
+  const ProtTabDesc &d = b.d[blockIdx.y];
+  prot_mfma_body<kSum, 0, false, true>((const double *)d.tab1, (const double *)d.tab2, (double *)d.x3, EV,
+                                       (const double *)d.left, (const double *)d.right, wgt, d.scaler, n,
+                                       ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, nullptr, d.c1a,
+                                       d.c1b, d.c2a, d.c2b);
 }
 
 

@@ -381,13 +381,24 @@ int check_node(plfx_ctx *ctx, const plfx_node &d, int tips, int64_t n, int i) {
   return PLFX_OK;
 }
 
+// A tip/tip protein node whose values sit in its stream's combination tables
+// after batch_impl: its CLV (x3), its table and its two tip-code arrays.
+struct TabRef {
+  const void *x3;
+  const void *tab;
+  const uint8_t *ca, *cb;
+};
+
 // Nodes of one kind (tips = number of tip children, tip child first) in
 // launches of kMaxBatch.  A tip child is a uint8 code array (no alignment rule).
-// *launches counts the kernel launches issued (may be NULL).
+// *launches counts the kernel launches issued (may be NULL).  *tabs (may be
+// NULL) receives the tip/tip protein nodes whose tables are still in the
+// stream's workspace afterwards (the last launch group's).
 int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, const void *EV,
                int64_t n, const int32_t *wgt, hipStream_t s, int tips,
                const void *tipvec = nullptr, int states = 4, int flags = PLFX_EXACT,
-               int *launches = nullptr) {
+               int *launches = nullptr, std::vector<TabRef> *tabs = nullptr) {
+  if (tabs) tabs->clear();
   if (count < 0 || n < 0 || (count > 0 && (!nodes || !EV)))
     return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
   for (int i = 0; i < count; i++) {
@@ -422,6 +433,12 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
         e = plfx::launch_prot_tiptip_gather(dtype, g, c, wgt, n, w->ws, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot tip/tip gather");
         if (launches) *launches += 2;
+        if (tabs) {  // this group's tables stay until the next group overwrites them
+          tabs->clear();
+          for (int i = 0; i < c; i++)
+            tabs->push_back(TabRef{nodes[j + i].x3, comb[i].x3, static_cast<const uint8_t *>(nodes[j + i].x1),
+                                   static_cast<const uint8_t *>(nodes[j + i].x2)});
+        }
       }
       return PLFX_OK;
     }
@@ -937,6 +954,13 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   std::vector<plfx_node> batch[3];  // by number of tip children
   std::vector<plfx::TripleDescH> tb[3];
   std::vector<plfx::SeptetDescH> sb[3];
+  // f64 FMA protein: the previous level's tip/tip nodes still in their
+  // combination tables; a node of this level whose two children are among them
+  // stages its child tiles from the tables (plf_prot.hpp kTab) instead of
+  // reading the children's CLVs back from HBM.  Only for the next level: later
+  // levels may overwrite the tables or the children's slots.
+  std::vector<TabRef> prev_tabs, cur_tabs;
+  const bool tab_mode = states == 20 && dtype == PLFX_F64 && (flags & PLFX_FMA) && n > 0;
   for (int lv = 0; lv < nlev; lv++) {
     for (int k = 0; k < 3; k++) {
       batch[k].clear();
@@ -1043,11 +1067,41 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         if (e != hipSuccess) return hip_fail(ctx, e, "fused level-pair launch");
         sched[6]++;
       }
+      if (k == 0 && tab_mode && !prev_tabs.empty() && !batch[0].empty()) {
+        auto find = [&](const void *x) -> const TabRef * {
+          for (const TabRef &t : prev_tabs)
+            if (t.x3 == x) return &t;
+          return nullptr;
+        };
+        std::vector<plfx::ProtTabDescH> tab;
+        std::vector<plfx_node> rest;
+        for (const plfx_node &nd : batch[0]) {
+          const TabRef *a = find(nd.x1), *b = find(nd.x2);
+          if (!a || !b) {
+            rest.push_back(nd);
+            continue;
+          }
+          const int rc = check_node(ctx, nd, 0, n, (int)tab.size());
+          if (rc != PLFX_OK) return rc;
+          tab.push_back(plfx::ProtTabDescH{a->tab, b->tab, a->ca, a->cb, b->ca, b->cb, nd.x3, nd.left,
+                                           nd.right, nd.scaler, nd.scaler_sum});
+        }
+        for (size_t i = 0; i < tab.size(); i += plfx::kMaxBatch) {
+          const int c = (int)std::min<size_t>(plfx::kMaxBatch, tab.size() - i);
+          hipError_t e = plfx::launch_prot_tab_batch(tab.data() + i, c, static_cast<const double *>(EV), wgt,
+                                                     n, ws, ctx->max_blocks, s);
+          if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot table-children launch");
+          sched[6]++;
+        }
+        batch[0].swap(rest);
+      }
       if (batch[k].empty()) continue;
       int rc = batch_impl(ctx, dtype, batch[k].data(), (int)batch[k].size(), EV, n, wgt, s, k,
-                          tipvec, states, flags, &sched[6]);
+                          tipvec, states, flags, &sched[6], k == 2 && tab_mode ? &cur_tabs : nullptr);
       if (rc != PLFX_OK) return rc;
     }
+    prev_tabs.swap(cur_tabs);
+    cur_tabs.clear();
   }
   for (int i = 0; i < PLFX_SCHED_COUNTS; i++) ctx->sched[i] = sched[i];
   return PLFX_OK;

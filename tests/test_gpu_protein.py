@@ -723,3 +723,46 @@ def test_protein_traverse_all_coded_128(ctx, oracle, dtype):
     assert np.array_equal(sums.cpu().numpy(), esums)
     for j in range(nops):
         assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+
+
+@pytest.mark.parametrize("with_sum", [True, False])
+@pytest.mark.parametrize("ntips", [32, 128])
+def test_protein_coded_tree_table_children(ctx, oracle, with_sum, ntips):
+    """f64 FMA protein tree, every leaf coded: the second level's nodes stage
+    their children's tiles from the first level's combination tables
+    (plf_prot_mfma_tab_batch_kernel) -- at 128 taxa only the second table
+    group's parents can (the first group's tables are overwritten), the rest
+    read the children's CLVs.  Every CLV, scaler byte and sum equals a
+    sequential evaluation by the oracle's fused loop bit for bit."""
+    import torch
+
+    n = 1500
+    rng = np.random.default_rng(ntips + 3)
+    ops = oracle.balanced_tree_ops(ntips)
+    nops, nslots = ops.shape[0], ntips + ops.shape[0]
+    codes = [oracle.random_protein_codes(rng, n, 0.2) for _ in range(ntips)]
+    pm = rng.random(nops * 2 * CAT * S * S) * 0.05
+    EV = rng.random(S * S) * 0.05
+    wgt = rng.integers(1, 4, n).astype(np.int32)
+    host = [oracle.expand_protein_tips(c, np.float64) for c in codes] + [None] * nops
+    M = CAT * S * S
+    escal, einc = [], []
+    for parent, a, b, p in ops:
+        x3, sc, inc = oracle.plf_generic(S, CAT, host[a], host[b], EV, pm[2 * p * M:(2 * p + 1) * M],
+                                         pm[(2 * p + 1) * M:(2 * p + 2) * M], wgt, fma=True)
+        host[parent] = x3
+        escal.append(sc)
+        einc.append(inc)
+    assert sum(einc) > 0
+    clv = [None] * ntips + [torch.zeros(V * n, dtype=torch.float64, device="cuda") for _ in range(nops)]
+    tips = [dev(c) for c in codes] + [None] * nops
+    sums = torch.full((nops,), -1, dtype=torch.int64, device="cuda") if with_sum else None
+    scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+    ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips, states=S, fma=True)
+    torch.cuda.synchronize()
+    for s_ in range(ntips, nslots):
+        assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
+    for j in range(nops):
+        assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
+    if with_sum:
+        assert sums.cpu().tolist() == einc
