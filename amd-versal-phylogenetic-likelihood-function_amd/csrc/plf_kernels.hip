@@ -573,7 +573,7 @@ hipError_t launch_prot_tiptip_gather(int dtype, const ProtGatherDescH *d, int co
                  : launch_gather_t<float, false>(b, count, wgt, n, ws, max_blocks, s);
 }
 
-hipError_t launch_prot_tab_batch(const ProtTabDescH *d, int count, const double *EV, const int32_t *wgt,
+hipError_t launch_prot_tab_batch(int dtype, const ProtTabDescH *d, int count, const void *EV, const int32_t *wgt,
                                  int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s) {
   if (count < 1 || count > kMaxBatch) return hipErrorInvalidValue;
   dev::ProtTabBatch b{};
@@ -583,14 +583,19 @@ hipError_t launch_prot_tab_batch(const ProtTabDescH *d, int count, const double 
     __builtin_memcpy(&b.d[i], &d[i], sizeof(d[i]));
     any_sum |= d[i].scaler_sum != nullptr;
   }
-  auto launch = [&](auto kernel, int &cache) {
+  auto launch = [&](auto kernel, int &cache, auto ev) {
     const int64_t gx = grid_x((const void *)kernel, cache, 1, n, 64, 1, max_blocks);  // full grid per node
-    hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt, n, ws);
+    hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, ev, wgt, n, ws);
     return hipGetLastError();
   };
-  static int c_sum = 0, c_nosum = 0;
-  return any_sum ? launch(&dev::plf_prot_mfma_tab_batch_kernel<true>, c_sum)
-                 : launch(&dev::plf_prot_mfma_tab_batch_kernel<false>, c_nosum);
+  static int c64 = 0, c64n = 0, c32 = 0, c32n = 0;
+  const double *E64 = static_cast<const double *>(EV);
+  const float *E32 = static_cast<const float *>(EV);
+  if (dtype == 1)
+    return any_sum ? launch(&dev::plf_prot_mfma_tab_batch_kernel<true>, c64, E64)
+                   : launch(&dev::plf_prot_mfma_tab_batch_kernel<false>, c64n, E64);
+  return any_sum ? launch(&dev::plf_prot_mfma32_tab_batch_kernel<true>, c32, E32)
+                 : launch(&dev::plf_prot_mfma32_tab_batch_kernel<false>, c32n, E32);
 }
 
 hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s,

@@ -545,11 +545,13 @@ struct ProtQueue {
 
 // A child tile gathered from its combination table by code pair (kTab below):
 // chunk j of the tile is site j / 40's row chunk j % 40, as tile_fetch.
-__device__ __forceinline__ void tab_fetch(const double *__restrict__ x, const uint8_t *__restrict__ ca,
+template <typename T>
+__device__ __forceinline__ void tab_fetch(const T *__restrict__ x, const uint8_t *__restrict__ ca,
                                           const uint8_t *__restrict__ cb, int64_t b, int64_t n,
-                                          f64x2 (&pf)[ProtTile<double>::kChunks / kBlock]) {
-  using PT = ProtTile<double>;
-  const f64x2 *tab = reinterpret_cast<const f64x2 *>(x);
+                                          typename ProtTile<T>::V (&pf)[ProtTile<T>::kChunks / kBlock]) {
+  using PT = ProtTile<T>;
+  using V = typename PT::V;
+  const V *tab = reinterpret_cast<const V *>(x);
   // lane l reads site l's two codes (one byte load per array for the whole
   // tile), each chunk takes its site's code pair from that lane (the kernel
   // runs at its 256-VGPR bound: per-chunk code loads spilled)
@@ -562,7 +564,7 @@ __device__ __forceinline__ void tab_fetch(const double *__restrict__ x, const ui
     const int j = threadIdx.x + i * kBlock;
     const int sl = j / PT::kChunksPerSite, q = j - sl * PT::kChunksPerSite;
     const int combo = __shfl(mine, sl < lim ? sl : lim - 1);
-    pf[i] = sl < lim ? tab[(unsigned)(combo * PT::kChunksPerSite + q)] : f64x2{};
+    pf[i] = sl < lim ? tab[(unsigned)(combo * PT::kChunksPerSite + q)] : V{};
   }
 }
 
@@ -598,7 +600,7 @@ __device__ __forceinline__ void prot_mfma_body(const double *__restrict__ x1, co
   const int64_t stride = (int64_t)gridDim.x * 64;
   if constexpr (!T2) {  // the first dense child's first tile, before the matrix fragments
     if constexpr (kTab) {
-      if ((int64_t)blockIdx.x * 64 < n) tab_fetch(x1, t1a, t1b, (int64_t)blockIdx.x * 64, n, pf);
+      if ((int64_t)blockIdx.x * 64 < n) tab_fetch<double>(x1, t1a, t1b, (int64_t)blockIdx.x * 64, n, pf);
     } else {
       if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
     }
@@ -654,7 +656,7 @@ __device__ __forceinline__ void prot_mfma_body(const double *__restrict__ x1, co
       tile_put<double>(tile, pf);
       __syncthreads();
       if constexpr (kDyn) next = qslot;
-      if constexpr (kTab) tab_fetch(x2, t2a, t2b, base, n, pf);
+      if constexpr (kTab) tab_fetch<double>(x2, t2a, t2b, base, n, pf);
       else tile_fetch<double>(x2, base, n, pf);
 #pragma unroll
       for (int t = 0; t < 4; t++) {
@@ -691,7 +693,7 @@ __device__ __forceinline__ void prot_mfma_body(const double *__restrict__ x1, co
       if constexpr (kDyn && T1) next = qslot;
       // next trip's first dense child: x1, or x2 when x1 is a tip
       if constexpr (kTab) {
-        if (next < n) tab_fetch(x1, t1a, t1b, next, n, pf);
+        if (next < n) tab_fetch<double>(x1, t1a, t1b, next, n, pf);
       } else {
         if (next < n) tile_fetch<double>(T1 ? x2 : x1, next, n, pf);
       }
@@ -840,6 +842,11 @@ plf_prot_mfma_tab_batch_kernel(const ProtTabBatch b, const double *__restrict__ 
                                        d.c1b, d.c2a, d.c2b);
 }
 
+template <bool kSum>
+__global__ void __launch_bounds__(kBlock, 3)
+plf_prot_mfma32_tab_batch_kernel(const ProtTabBatch b, const float *__restrict__ EV,
+                                 const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws);
+
 
 // ---------------------------------------------------------------------------
 // FMA mode on the matrix cores, f32: v_mfma_f32_16x16x4_f32 is exact f32, a
@@ -889,13 +896,18 @@ __device__ __forceinline__ void transpose_groups44(unsigned (&v)[4]) {
   }
 }
 
-template <bool kSum, int kTips>
+// kTab: as prot_mfma_body's (children staged from their combination tables).
+template <bool kSum, int kTips, bool kTab = false>
 __device__ __forceinline__ void prot_mfma32_body(const float *__restrict__ x1, const float *__restrict__ x2,
                                                  float *__restrict__ x3, const float *__restrict__ EV,
                                                  const float *__restrict__ left, const float *__restrict__ right,
                                                  const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler,
                                                  int64_t n, unsigned long long *ws, int64_t *scaler_sum,
-                                                 const float *__restrict__ tipvec) {
+                                                 const float *__restrict__ tipvec,
+                                                 const uint8_t *__restrict__ t1a = nullptr,
+                                                 const uint8_t *__restrict__ t1b = nullptr,
+                                                 const uint8_t *__restrict__ t2a = nullptr,
+                                                 const uint8_t *__restrict__ t2b = nullptr) {
   constexpr int S = 20;
   constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
   using PT = ProtTile<float>;
@@ -907,8 +919,13 @@ __device__ __forceinline__ void prot_mfma32_body(const float *__restrict__ x1, c
   const int64_t stride = (int64_t)gridDim.x * 64;
   f32x4 pf[K];
   // the first dense child's first tile, before the matrix fragments
-  if constexpr (!(T1 && T2))
-    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<float>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
+  if constexpr (!(T1 && T2)) {
+    if constexpr (kTab) {
+      if ((int64_t)blockIdx.x * 64 < n) tab_fetch<float>(x1, t1a, t1b, (int64_t)blockIdx.x * 64, n, pf);
+    } else {
+      if ((int64_t)blockIdx.x * 64 < n) tile_fetch<float>(T1 ? x2 : x1, (int64_t)blockIdx.x * 64, n, pf);
+    }
+  }
   float AL[2][5], AR[2][5], AE[2][5];
 #pragma unroll
   for (int mt = 0; mt < 2; mt++)
@@ -1009,7 +1026,8 @@ __device__ __forceinline__ void prot_mfma32_body(const float *__restrict__ x1, c
       if constexpr (T2) {
         if (base + stride < n) tile_fetch<float>(x1, base + stride, n, pf);
       } else {
-        tile_fetch<float>(x2, base, n, pf);
+        if constexpr (kTab) tab_fetch<float>(x2, t2a, t2b, base, n, pf);
+        else tile_fetch<float>(x2, base, n, pf);
       }
       product(AL, QL, P, Q, false, td);
       __syncthreads();
@@ -1026,7 +1044,11 @@ __device__ __forceinline__ void prot_mfma32_body(const float *__restrict__ x1, c
     } else {
       tile_put<float>(tile, pf);
       __syncthreads();
-      if (base + stride < n) tile_fetch<float>(T1 ? x2 : x1, base + stride, n, pf);
+      if constexpr (kTab) {
+        if (base + stride < n) tab_fetch<float>(x1, t1a, t1b, base + stride, n, pf);
+      } else {
+        if (base + stride < n) tile_fetch<float>(T1 ? x2 : x1, base + stride, n, pf);
+      }
       product(AR, QR, P, Q, true, td);
       __syncthreads();  // every wave is done reading x2: the tile takes X3 now
     }
@@ -1139,6 +1161,17 @@ plf_prot_mfma32_batch_kernel(const NodeBatch nodes, const float *__restrict__ EV
   prot_mfma32_body<kSum, kTips>((const float *)d.x1, (const float *)d.x2, (float *)d.x3, EV,
                                 (const float *)d.left, (const float *)d.right, wgt, d.scaler, n,
                                 ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, tipvec);
+}
+
+template <bool kSum>
+__global__ void __launch_bounds__(kBlock, 3)
+plf_prot_mfma32_tab_batch_kernel(const ProtTabBatch b, const float *__restrict__ EV,
+                                 const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws) {
+  const ProtTabDesc &d = b.d[blockIdx.y];
+  prot_mfma32_body<kSum, 0, true>((const float *)d.tab1, (const float *)d.tab2, (float *)d.x3, EV,
+                                  (const float *)d.left, (const float *)d.right, wgt, d.scaler, n,
+                                  ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, nullptr, d.c1a, d.c1b,
+                                  d.c2a, d.c2b);
 }
 
 // ---------------------------------------------------------------------------

@@ -725,10 +725,11 @@ def test_protein_traverse_all_coded_128(ctx, oracle, dtype):
         assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("with_sum", [True, False])
 @pytest.mark.parametrize("ntips", [32, 128])
-def test_protein_coded_tree_table_children(ctx, oracle, with_sum, ntips):
-    """f64 FMA protein tree, every leaf coded: the second level's nodes stage
+def test_protein_coded_tree_table_children(ctx, oracle, dtype, with_sum, ntips):
+    """FMA-mode protein tree (f64, f32), every leaf coded: the second level's nodes stage
     their children's tiles from the first level's combination tables
     (plf_prot_mfma_tab_batch_kernel) -- at 128 taxa only the second table
     group's parents can (the first group's tables are overwritten), the rest
@@ -741,10 +742,10 @@ def test_protein_coded_tree_table_children(ctx, oracle, with_sum, ntips):
     ops = oracle.balanced_tree_ops(ntips)
     nops, nslots = ops.shape[0], ntips + ops.shape[0]
     codes = [oracle.random_protein_codes(rng, n, 0.2) for _ in range(ntips)]
-    pm = rng.random(nops * 2 * CAT * S * S) * 0.05
-    EV = rng.random(S * S) * 0.05
+    pm = (rng.random(nops * 2 * CAT * S * S) * 0.05).astype(dtype)
+    EV = (rng.random(S * S) * 0.05).astype(dtype)
     wgt = rng.integers(1, 4, n).astype(np.int32)
-    host = [oracle.expand_protein_tips(c, np.float64) for c in codes] + [None] * nops
+    host = [oracle.expand_protein_tips(c, dtype) for c in codes] + [None] * nops
     M = CAT * S * S
     escal, einc = [], []
     for parent, a, b, p in ops:
@@ -754,7 +755,8 @@ def test_protein_coded_tree_table_children(ctx, oracle, with_sum, ntips):
         escal.append(sc)
         einc.append(inc)
     assert sum(einc) > 0
-    clv = [None] * ntips + [torch.zeros(V * n, dtype=torch.float64, device="cuda") for _ in range(nops)]
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    clv = [None] * ntips + [torch.zeros(V * n, dtype=tt, device="cuda") for _ in range(nops)]
     tips = [dev(c) for c in codes] + [None] * nops
     sums = torch.full((nops,), -1, dtype=torch.int64, device="cuda") if with_sum else None
     scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
