@@ -296,7 +296,10 @@ int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const
  * per code pair (24 x 24) into tables of the stream's workspace (about 11.8 MB,
  * allocated on that stream's first such call, freed with the context) and
  * gathered per site: the same values as the direct computation; a capture on
- * a stream without the tables yet runs the direct kernel. */
+ * a stream without the tables yet runs the direct kernel.  In a traversal in
+ * FMA mode, a node whose two children are such nodes of the level before
+ * stages its children from their tables instead of reading their CLVs back
+ * (the CLVs are still written; the results are the same). */
 int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const plfx_trav_op *ops,
                        int nops, void *const *clv, const uint8_t *const *tips, int nslots,
                        const void *pmats,
