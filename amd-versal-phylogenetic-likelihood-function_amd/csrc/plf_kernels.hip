@@ -573,8 +573,9 @@ hipError_t launch_prot_tiptip_gather(int dtype, const ProtGatherDescH *d, int co
                  : launch_gather_t<float, false>(b, count, wgt, n, ws, max_blocks, s);
 }
 
-hipError_t launch_prot_tab_batch(int dtype, const ProtTabDescH *d, int count, const void *EV, const int32_t *wgt,
-                                 int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s) {
+hipError_t launch_prot_tab_batch(int dtype, bool fma, const ProtTabDescH *d, int count, const void *EV,
+                                 const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                                 hipStream_t s) {
   if (count < 1 || count > kMaxBatch) return hipErrorInvalidValue;
   dev::ProtTabBatch b{};
   bool any_sum = false;
@@ -588,9 +589,16 @@ hipError_t launch_prot_tab_batch(int dtype, const ProtTabDescH *d, int count, co
     hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, ev, wgt, n, ws);
     return hipGetLastError();
   };
-  static int c64 = 0, c64n = 0, c32 = 0, c32n = 0;
+  static int c64 = 0, c64n = 0, c32 = 0, c32n = 0, x64 = 0, x64n = 0, x32 = 0, x32n = 0;
   const double *E64 = static_cast<const double *>(EV);
   const float *E32 = static_cast<const float *>(EV);
+  if (!fma) {  // the exact bodies' shapes (launch_prot_t / launch_prot_exact64_t)
+    if (dtype == 1)
+      return any_sum ? launch(&dev::plf_prot_lds_tab_batch_kernel<double, true, 10, true>, x64, E64)
+                     : launch(&dev::plf_prot_lds_tab_batch_kernel<double, false, 10, true>, x64n, E64);
+    return any_sum ? launch(&dev::plf_prot_lds_tab_batch_kernel<float, true, 4, false>, x32, E32)
+                   : launch(&dev::plf_prot_lds_tab_batch_kernel<float, false, 4, false>, x32n, E32);
+  }
   if (dtype == 1)
     return any_sum ? launch(&dev::plf_prot_mfma_tab_batch_kernel<true>, c64, E64)
                    : launch(&dev::plf_prot_mfma_tab_batch_kernel<false>, c64n, E64);

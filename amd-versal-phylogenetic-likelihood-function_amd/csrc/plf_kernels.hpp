@@ -61,7 +61,7 @@ constexpr int kProtCombos = 24 * 24;
 hipError_t launch_prot_tiptip_gather(int dtype, const ProtGatherDescH *d, int count, const int32_t *wgt,
                                      int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s);
 
-// FMA-mode protein nodes (f64, f32) whose two children are tip/tip nodes held in
+// Protein nodes (f64, f32; FMA or exact) whose two children are tip/tip nodes held in
 // combination tables (plf_prot.hpp ProtTabDesc), batched as above.
 struct ProtTabDescH {
   const void *tab1, *tab2;
@@ -71,8 +71,9 @@ struct ProtTabDescH {
   uint8_t *scaler;
   int64_t *scaler_sum;
 };
-hipError_t launch_prot_tab_batch(int dtype, const ProtTabDescH *d, int count, const void *EV, const int32_t *wgt,
-                                 int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s);
+hipError_t launch_prot_tab_batch(int dtype, bool fma, const ProtTabDescH *d, int count, const void *EV,
+                                 const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
+                                 hipStream_t s);
 
 // Protein (S = 20) nodes batched the same way; fma as launch_plf_prot.
 hipError_t launch_plf_prot_batch(int dtype, bool fma, const NodeDescH *nodes, int count, const void *EV,

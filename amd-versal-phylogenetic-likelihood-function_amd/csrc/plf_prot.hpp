@@ -211,6 +211,31 @@ __device__ __forceinline__ void pin_chains(T (&u)[R]) {
   }
 }
 
+// A child tile gathered from its combination table by code pair (kTab in the bodies below):
+// chunk j of the tile is site j / 40's row chunk j % 40, as tile_fetch.
+template <typename T>
+__device__ __forceinline__ void tab_fetch(const T *__restrict__ x, const uint8_t *__restrict__ ca,
+                                          const uint8_t *__restrict__ cb, int64_t b, int64_t n,
+                                          typename ProtTile<T>::V (&pf)[ProtTile<T>::kChunks / kBlock]) {
+  using PT = ProtTile<T>;
+  using V = typename PT::V;
+  const V *tab = reinterpret_cast<const V *>(x);
+  // lane l reads site l's two codes (one byte load per array for the whole
+  // tile), each chunk takes its site's code pair from that lane (the kernel
+  // runs at its 256-VGPR bound: per-chunk code loads spilled)
+  const int lane = threadIdx.x & 63;
+  const int lim = (int)(n - b < 64 ? n - b : 64);
+  const int ls = lane < lim ? lane : lim - 1;
+  const int mine = prot_code(ca[b + ls]) * kProtCodes + prot_code(cb[b + ls]);
+#pragma unroll
+  for (int i = 0; i < PT::kChunks / kBlock; i++) {
+    const int j = threadIdx.x + i * kBlock;
+    const int sl = j / PT::kChunksPerSite, q = j - sl * PT::kChunksPerSite;
+    const int combo = __shfl(mine, sl < lim ? sl : lim - 1);
+    pf[i] = sl < lim ? tab[(unsigned)(combo * PT::kChunksPerSite + q)] : V{};
+  }
+}
+
 // The LDS-matrix protein kernel (exact mode, f64 and f32): the matrices live
 // in LDS (P_L and P_R of the 4 categories and EV; 28.8 KB f64) and every value
 // is a wave-uniform ds_read_b128 broadcast, where a register-distributed form
@@ -233,13 +258,18 @@ __device__ __forceinline__ void pin_chains(T (&u)[R]) {
 // phase 1, the next trip's first dense child during phases 2 and 3.
 // kE3S: phase 3's EV rows by scalar loads (SGPR operands) instead of LDS
 // broadcasts: 145.8 vs 148.8 us at 2^18 f64 (profiles/r02_tune_protein_exact_rows.log).
-template <typename T, bool kSum, int kTips, int kRows, bool kE3S>
+// kTab: as prot_mfma_body's (children staged from their combination tables).
+template <typename T, bool kSum, int kTips, int kRows, bool kE3S, bool kTab = false>
 __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T *__restrict__ x2,
                                               T *__restrict__ x3, const T *__restrict__ EV,
                                               const T *__restrict__ left, const T *__restrict__ right,
                                               const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler,
                                               int64_t n, unsigned long long *ws, int64_t *scaler_sum,
-                                              const T *__restrict__ tipvec) {
+                                              const T *__restrict__ tipvec,
+                                              const uint8_t *__restrict__ t1a = nullptr,
+                                              const uint8_t *__restrict__ t1b = nullptr,
+                                              const uint8_t *__restrict__ t2a = nullptr,
+                                              const uint8_t *__restrict__ t2b = nullptr) {
   constexpr int S = 20;
   constexpr bool T1 = kTips >= 1, T2 = kTips == 2;
   using PT = ProtTile<T>;
@@ -315,8 +345,11 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
   const int64_t stride = (int64_t)gridDim.x * 64;
   constexpr int K = PT::kChunks / kBlock;
   V pf[K];  // unused (and eliminated) when both children are tips
-  if constexpr (kAnyDense)
+  if constexpr (kTab) {
+    if ((int64_t)blockIdx.x * 64 < n) tab_fetch<T>(x1, t1a, t1b, (int64_t)blockIdx.x * 64, n, pf);
+  } else if constexpr (kAnyDense) {
     if ((int64_t)blockIdx.x * 64 < n) tile_fetch<T>(FD, (int64_t)blockIdx.x * 64, n, pf);
+  }
   for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
     int off = 0;
     asm volatile("" : "+v"(off));
@@ -335,7 +368,12 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
     auto stage = [&](const T *next, int64_t nbase) {
       tile_put<T>(tile, pf);
       __syncthreads();
-      if (nbase < n) tile_fetch<T>(next, nbase, n, pf);
+      if constexpr (kTab) {
+        const bool one = next == x1;
+        if (nbase < n) tab_fetch<T>(next, one ? t1a : t2a, one ? t1b : t2b, nbase, n, pf);
+      } else {
+        if (nbase < n) tile_fetch<T>(next, nbase, n, pf);
+      }
     };
     if constexpr (T1) {  // tip: U from the table row of the site's code
       const T *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
@@ -542,31 +580,6 @@ struct ProtQueue {
     }
   }
 };
-
-// A child tile gathered from its combination table by code pair (kTab below):
-// chunk j of the tile is site j / 40's row chunk j % 40, as tile_fetch.
-template <typename T>
-__device__ __forceinline__ void tab_fetch(const T *__restrict__ x, const uint8_t *__restrict__ ca,
-                                          const uint8_t *__restrict__ cb, int64_t b, int64_t n,
-                                          typename ProtTile<T>::V (&pf)[ProtTile<T>::kChunks / kBlock]) {
-  using PT = ProtTile<T>;
-  using V = typename PT::V;
-  const V *tab = reinterpret_cast<const V *>(x);
-  // lane l reads site l's two codes (one byte load per array for the whole
-  // tile), each chunk takes its site's code pair from that lane (the kernel
-  // runs at its 256-VGPR bound: per-chunk code loads spilled)
-  const int lane = threadIdx.x & 63;
-  const int lim = (int)(n - b < 64 ? n - b : 64);
-  const int ls = lane < lim ? lane : lim - 1;
-  const int mine = prot_code(ca[b + ls]) * kProtCodes + prot_code(cb[b + ls]);
-#pragma unroll
-  for (int i = 0; i < PT::kChunks / kBlock; i++) {
-    const int j = threadIdx.x + i * kBlock;
-    const int sl = j / PT::kChunksPerSite, q = j - sl * PT::kChunksPerSite;
-    const int combo = __shfl(mine, sl < lim ? sl : lim - 1);
-    pf[i] = sl < lim ? tab[(unsigned)(combo * PT::kChunksPerSite + q)] : V{};
-  }
-}
 
 // kTab: both children are tip/tip nodes of the same traversal whose values
 // sit in their combination tables (prot_tiptip_gather_kernel below): x1 / x2
@@ -840,6 +853,18 @@ plf_prot_mfma_tab_batch_kernel(const ProtTabBatch b, const double *__restrict__ 
                                        (const double *)d.left, (const double *)d.right, wgt, d.scaler, n,
                                        ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, nullptr, d.c1a,
                                        d.c1b, d.c2a, d.c2b);
+}
+
+// exact mode (the LDS-matrix body), f64 and f32
+template <typename T, bool kSum, int kRows, bool kE3S>
+__global__ void __launch_bounds__(kBlock, 2)
+plf_prot_lds_tab_batch_kernel(const ProtTabBatch b, const T *__restrict__ EV, const int32_t *__restrict__ wgt,
+                              int64_t n, unsigned long long *ws) {
+  const ProtTabDesc &d = b.d[blockIdx.y];
+  prot_lds_body<T, kSum, 0, kRows, kE3S, true>((const T *)d.tab1, (const T *)d.tab2, (T *)d.x3, EV,
+                                               (const T *)d.left, (const T *)d.right, wgt, d.scaler, n,
+                                               ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, nullptr,
+                                               d.c1a, d.c1b, d.c2a, d.c2b);
 }
 
 template <bool kSum>

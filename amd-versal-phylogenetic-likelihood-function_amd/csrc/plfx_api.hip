@@ -954,13 +954,13 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   std::vector<plfx_node> batch[3];  // by number of tip children
   std::vector<plfx::TripleDescH> tb[3];
   std::vector<plfx::SeptetDescH> sb[3];
-  // protein FMA mode: the previous level's tip/tip nodes still in their
+  // protein: the previous level's tip/tip nodes still in their
   // combination tables; a node of this level whose two children are among them
   // stages its child tiles from the tables (plf_prot.hpp kTab) instead of
   // reading the children's CLVs back from HBM.  Only for the next level: later
   // levels may overwrite the tables or the children's slots.
   std::vector<TabRef> prev_tabs, cur_tabs;
-  const bool tab_mode = states == 20 && (flags & PLFX_FMA) && n > 0;
+  const bool tab_mode = states == 20 && n > 0;
   for (int lv = 0; lv < nlev; lv++) {
     for (int k = 0; k < 3; k++) {
       batch[k].clear();
@@ -1088,8 +1088,8 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         }
         for (size_t i = 0; i < tab.size(); i += plfx::kMaxBatch) {
           const int c = (int)std::min<size_t>(plfx::kMaxBatch, tab.size() - i);
-          hipError_t e = plfx::launch_prot_tab_batch(dtype, tab.data() + i, c, EV, wgt, n, ws,
-                                                     ctx->max_blocks, s);
+          hipError_t e = plfx::launch_prot_tab_batch(dtype, (flags & PLFX_FMA) != 0, tab.data() + i, c, EV,
+                                                     wgt, n, ws, ctx->max_blocks, s);
           if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot table-children launch");
           sched[6]++;
         }

@@ -726,10 +726,11 @@ def test_protein_traverse_all_coded_128(ctx, oracle, dtype):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("fma", [True, False])
 @pytest.mark.parametrize("with_sum", [True, False])
 @pytest.mark.parametrize("ntips", [32, 128])
-def test_protein_coded_tree_table_children(ctx, oracle, dtype, with_sum, ntips):
-    """FMA-mode protein tree (f64, f32), every leaf coded: the second level's nodes stage
+def test_protein_coded_tree_table_children(ctx, oracle, dtype, fma, with_sum, ntips):
+    """Protein tree (f64, f32; FMA or exact), every leaf coded: the second level's nodes stage
     their children's tiles from the first level's combination tables
     (plf_prot_mfma_tab_batch_kernel) -- at 128 taxa only the second table
     group's parents can (the first group's tables are overwritten), the rest
@@ -750,7 +751,7 @@ def test_protein_coded_tree_table_children(ctx, oracle, dtype, with_sum, ntips):
     escal, einc = [], []
     for parent, a, b, p in ops:
         x3, sc, inc = oracle.plf_generic(S, CAT, host[a], host[b], EV, pm[2 * p * M:(2 * p + 1) * M],
-                                         pm[(2 * p + 1) * M:(2 * p + 2) * M], wgt, fma=True)
+                                         pm[(2 * p + 1) * M:(2 * p + 2) * M], wgt, fma=fma)
         host[parent] = x3
         escal.append(sc)
         einc.append(inc)
@@ -760,7 +761,7 @@ def test_protein_coded_tree_table_children(ctx, oracle, dtype, with_sum, ntips):
     tips = [dev(c) for c in codes] + [None] * nops
     sums = torch.full((nops,), -1, dtype=torch.int64, device="cuda") if with_sum else None
     scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
-    ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips, states=S, fma=True)
+    ctx.traverse(ops, clv, dev(pm), dev(EV), n, dev(wgt), scal, sums, tips=tips, states=S, fma=fma)
     torch.cuda.synchronize()
     for s_ in range(ntips, nslots):
         assert np.array_equal(bits(clv[s_].cpu().numpy()), bits(host[s_])), s_
