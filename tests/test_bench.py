@@ -1,0 +1,123 @@
+"""CPU tests of bench.py's host logic: the self-contained `--gpus N` entry
+(torch.distributed.run started as a child when no launcher set WORLD_SIZE,
+fail-fast when too few GPUs are visible for RCCL)."""
+import os
+import subprocess
+import sys
+import time
+
+from conftest import ROOT
+
+sys.path.insert(0, str(ROOT))
+
+import bench  # noqa: E402
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "PLFX_DIST_BACKEND")}
+    env.update(kw)
+    return env
+
+
+def test_gpus_n_fails_fast_without_enough_gpus():
+    """--gpus 2 under the default nccl backend on a host with fewer than 2
+    visible GPUs (this container has none): a clear message and a non-zero
+    exit before any rank is started, no traceback."""
+    t0 = time.time()
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300, env=_env(),
+                       cwd=str(ROOT))
+    assert r.returncode != 0
+    assert "needs 2 visible GPUs" in r.stderr and "PLFX_DIST_BACKEND=gloo" in r.stderr
+    assert "Traceback" not in r.stderr and r.stdout == ""
+    assert time.time() - t0 < 120
+
+
+def test_self_launch_command_is_the_drivers():
+    """The child command is the driver's own N > 1 invocation: one node,
+    N ranks, 127.0.0.1 rendezvous, bench.py with the same arguments."""
+    argv = ["--gpus", "8", "--workload", "nodes512", "--steps", "5"]
+    cmd = bench.self_launch_cmd(8, argv, 29511)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=8" in cmd
+    i = cmd.index("--master-addr")
+    assert cmd[i + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29511"
+    assert cmd[-len(argv) - 1].endswith("bench.py") and cmd[-len(argv):] == argv
+
+
+def test_launched_rank_does_not_relaunch(monkeypatch):
+    """Under a launcher (WORLD_SIZE set) bench.py must not start another one:
+    main() goes straight to the rank path (checked here up to the
+    --gpus/WORLD_SIZE consistency exit, before any GPU work)."""
+    monkeypatch.setenv("WORLD_SIZE", "3")
+    called = []
+    monkeypatch.setattr(bench, "self_launch", lambda *a: called.append(a))
+    try:
+        bench.main(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    except SystemExit as e:
+        assert "WORLD_SIZE=3" in str(e.code)
+    assert called == []
+
+
+class _WL:
+    bytes_per_step = 12345
+
+
+def _record(tmp_path, tag, code, val=4.0e8, sites=1 << 20):
+    import json
+
+    rec = {"kernel": "plf_dna_f64_pair_kernel", "sites": sites, "dtype": "f64",
+           "hbm_bytes_per_launch": val}
+    if code is not None:
+        rec["code"] = code
+    p = tmp_path / f"{tag}_node_pmc_traffic.json"
+    p.write_text(json.dumps(rec))
+    return p
+
+
+def test_traffic_record_tied_to_code(tmp_path):
+    """roofline.traffic comes only from a PMC record whose code stamp (sha256
+    of the counted kernel's gfx950 machine code) matches the library being
+    timed: a mismatched or unstamped record is refused (traffic null,
+    traffic_stale true, traffic_source naming it); an older record that still
+    matches the code is used instead of a newer stale one."""
+    from plfx import codeobj
+
+    lib = codeobj.default_lib()
+    good = codeobj.stamp(["plf_dna_f64_pair_kernel"], lib)
+    assert len(good["plf_dna_f64_pair_kernel"]) == 64
+    a = bench.parse(["--traffic-json", str(tmp_path / "x.json")])
+
+    t = bench.traffic_record(a, _WL(), lib)
+    assert t["traffic"] is None and not t["traffic_stale"] and t["traffic_source"] is None
+
+    _record(tmp_path, "r05", {"plf_dna_f64_pair_kernel": "0" * 64}, val=1.0)
+    t = bench.traffic_record(a, _WL(), lib)
+    assert t["traffic"] is None and t["traffic_stale"]
+    assert t["traffic_source"].endswith("r05_node_pmc_traffic.json")
+    assert "plf_dna_f64_pair_kernel" in t["traffic_note"]
+
+    _record(tmp_path, "r04", None, val=2.0)  # unstamped: refused too
+    assert bench.traffic_record(a, _WL(), lib)["traffic"] is None
+
+    _record(tmp_path, "r03", good, val=3.0)
+    t = bench.traffic_record(a, _WL(), lib)
+    assert t["traffic"] == 3.0 and not t["traffic_stale"]
+    assert t["traffic_source"].endswith("r03_node_pmc_traffic.json")
+
+    _record(tmp_path, "r06", good, val=6.0, sites=4096)  # another configuration: ignored
+    assert bench.traffic_record(a, _WL(), lib)["traffic"] == 3.0
+
+
+def test_code_hash_names_kernels_exactly():
+    """The stamp hashes every instantiation of exactly the named kernel."""
+    from plfx import codeobj
+
+    lib = codeobj.default_lib()
+    inst = codeobj.kernel_instantiations(lib, "plf_dna_kernel")
+    assert inst and all("14plf_dna_kernel" in s for s in inst)
+    assert codeobj.kernel_code_sha256(lib, "plf_dna_kernel") != codeobj.kernel_code_sha256(
+        lib, "plf_dna_f64_pair_kernel")
+    ok, why = codeobj.check_stamp({"no_such_kernel": "0" * 64}, lib)
+    assert not ok and "no_such_kernel" in why

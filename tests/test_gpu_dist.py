@@ -105,6 +105,26 @@ def test_nodes_three_ranks_ragged_split():
     assert d["config"]["scaler_events_all_ranks"] == 2 * (65536 // 4)
 
 
+def test_bench_gpus_two_without_outer_launcher():
+    """`python bench.py --gpus 2` as the driver may invoke it, with NO outer
+    torch.distributed.run: bench.py starts the launcher as a child, and the
+    relayed stdout is exactly one JSON line from two ranks (gloo on the
+    one-GPU box: both ranks fold onto GPU 0)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PLFX_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--sites", "65536", "--steps", "3",
+           "--warmup", "1", "--no-cpu-baseline", "--buffer-sets", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT), env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["check"] == "ok" and len(d["config"]["lnl_per_rank"]) == 2
+    assert d["config"]["launcher"] == "torch.distributed.run started by bench.py"
+    assert d["config"]["distributed"] == "gloo"
+    assert d["config"]["scaler_events_all_ranks"] == 2 * (65536 // 4)
+
+
 def test_nodes512_full_size_windows(oracle):
     """BASELINE configs[3] at full size on one GPU, as bench.py times it: the
     512 nodes x 2^20 f64 sites of bench.NodesWorkload (201 GB of CLVs) in its

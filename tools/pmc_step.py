@@ -15,6 +15,11 @@ import argparse
 import collections
 import csv
 import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "amd-versal-phylogenetic-likelihood-function_amd"))
+from plfx import codeobj  # noqa: E402
 import statistics as st
 
 
@@ -57,6 +62,8 @@ def main():
            "correction": "FETCH_SIZE x1024 x2, WRITE_SIZE x1024 (MI355X_MICROARCH.md, HBM section)"}
     if a.key:
         rec["key"] = a.key
+    # ties the record to the machine code it was counted on (bench.py checks it)
+    rec["code"] = codeobj.stamp([r["kernel"] for r in rows])
     json.dump(rec, open(a.out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 

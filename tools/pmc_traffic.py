@@ -10,6 +10,11 @@ usage: tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON --sites N --dtype f64
 import argparse
 import csv
 import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "amd-versal-phylogenetic-likelihood-function_amd"))
+from plfx import codeobj  # noqa: E402
 import statistics as st
 
 
@@ -51,6 +56,8 @@ def main():
         "correction": "FETCH_SIZE x1024 x2 (gfx950 half-count on 16-B/lane streaming reads), "
                       "WRITE_SIZE x1024 (MI355X_MICROARCH.md, HBM section)",
     }
+    # ties the record to the machine code it was counted on (bench.py checks it)
+    rec["code"] = codeobj.stamp([a.kernel])
     json.dump(rec, open(a.out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
