@@ -608,10 +608,12 @@ hipError_t launch_prot_tab_batch(int dtype, bool fma, const ProtTabDescH *d, int
 
 hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s,
                            int tips, const void *tipvec) {
+  // tip/tip nodes (tips == 2) always go through the combination tables of the
+  // stream's workspace (launch_plf_prot_batch over the 576 code pairs, then
+  // launch_prot_tiptip_gather), never a one-node kernel
   switch (tips) {
     case 0: return launch_prot_tips<0>(dtype, fma, a, max_blocks, s, tipvec);
     case 1: return launch_prot_tips<1>(dtype, fma, a, max_blocks, s, tipvec);
-    case 2: return launch_prot_tips<2>(dtype, fma, a, max_blocks, s, tipvec);
     default: return hipErrorInvalidValue;
   }
 }

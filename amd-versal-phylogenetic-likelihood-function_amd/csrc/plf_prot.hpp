@@ -830,8 +830,11 @@ plf_prot_mfma_batch_kernel(const NodeBatch nodes, const double *__restrict__ EV,
                                      ws + (size_t)blockIdx.y * kWsWords, d.scaler_sum, tipvec);
 }
 
-// Batched f64 FMA protein nodes whose children are both tip/tip nodes held in
+// Batched protein nodes whose children are both tip/tip nodes held in
 // combination tables (kTab above): the parents of a coded tree's first level.
+// One kernel per mode and dtype: f64 FMA (matrix cores, below), exact f64 and
+// f32 (the LDS-matrix body), f32 FMA (matrix cores) -- the traversal uses the
+// tables in every mode (plfx_api.hip tab_mode).
 struct ProtTabDesc {
   const void *tab1, *tab2;               // the children's tables (576 x 80 f64)
   const uint8_t *c1a, *c1b, *c2a, *c2b;  // each child's two tip-code arrays

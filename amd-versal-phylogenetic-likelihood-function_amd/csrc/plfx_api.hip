@@ -34,15 +34,19 @@ constexpr int kHostChunksMax = 16;
 // (handle, thread).  Entries come from a pool allocated and zeroed with the
 // context (no allocation on a call path for the first kWsPool streams, so a
 // stream's first use may be inside a graph capture); plfx_ctx_release_stream
-// returns an entry to the pool.
+// returns an entry to the pool -- unless a graph was captured through it: the
+// graph's replays keep using the entry's words, so it is retired (never handed
+// to another stream) and the context waits for the device when destroyed.
 struct StreamWs {
   hipStream_t stream = nullptr;
   std::thread::id tid;               // owning thread for hipStreamPerThread, else none
   bool in_use = false;
+  bool captured = false;             // used while its stream was capturing
+  bool retired = false;              // released after a capture, or its thread exited
   unsigned long long *ws = nullptr;  // kWsRegions x kWsWords u64
   double *lnl_partials = nullptr;    // kLnlMaxGrid doubles
   unsigned long long *lnl_ticket = nullptr;
-  void *tt = nullptr;  // tip/tip protein combination tables (kTtBytes, on first use; stays with the entry)
+  char *tt = nullptr;  // tip/tip protein combination tables (kTtEntryBytes, allocated with the entry)
 };
 constexpr int kWsPool = PLFX_WS_POOL;
 
@@ -54,6 +58,7 @@ struct plfx_ctx {
                  // level pairs, 1 level pairs, 0 none (PLFX_FUSE)
   std::deque<StreamWs> wss;         // per-stream workspaces (stable addresses)
   std::vector<void *> ws_blocks;    // their allocations (the pool's, then one per extra entry)
+  uint8_t *tt_codes = nullptr;      // the tip/tip tables' two constant 576-code arrays (kTtCodeBytes)
   int sched[PLFX_SCHED_COUNTS] = {};  // schedule of the last traverse
   // grow-only staging for the synchronous host entry points
   void *d_buf = nullptr;
@@ -126,6 +131,42 @@ hipStream_t pick(plfx_ctx *, void *stream) { return reinterpret_cast<hipStream_t
 
 constexpr size_t kWsEntryBytes = kWsBytes + kLnlPartialBytes + kLnlTicketBytes;
 
+// Tip/tip protein combination tables (plf_prot.hpp prot_tiptip_gather_kernel):
+// per node of a launch group, a 576 x 80 table of the node's dtype and 576
+// scaler bytes, in every workspace entry (written by the table kernel before
+// each use, so never zeroed), and the two constant 576-code arrays (combo
+// k = code1 * 24 + code2) once per context.  Allocated with the entries, so
+// a stream's first tip/tip call -- also inside a capture -- takes the tables.
+constexpr size_t kTtCodeBytes = 2048;
+constexpr size_t kTtTabBytes = (size_t)plfx::kProtCombos * 80 * sizeof(double);
+constexpr size_t kTtScBytes = 1024;
+constexpr size_t kTtEntryBytes = (size_t)plfx::kMaxBatch * (kTtTabBytes + kTtScBytes);
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  return s && hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+}
+
+// Threads that took a hipStreamPerThread workspace of a live context: when
+// such a thread exits without releasing it, its entry is retired (its stream
+// is gone with the thread, so nothing may wait on it) and reclaimed, after a
+// device synchronisation, when the context runs out of entries.
+std::mutex g_live_mu;
+std::vector<plfx_ctx *> g_live;  // contexts not yet destroyed
+
+void orphan_thread_entries(plfx_ctx *ctx, std::thread::id tid);
+
+struct PerThreadEntries {
+  std::vector<plfx_ctx *> ctxs;
+  ~PerThreadEntries() {
+    std::lock_guard<std::mutex> l(g_live_mu);
+    for (plfx_ctx *c : ctxs)
+      if (std::find(g_live.begin(), g_live.end(), c) != g_live.end())
+        orphan_thread_entries(c, std::this_thread::get_id());
+  }
+};
+thread_local PerThreadEntries t_entries;
+
 // the key thread of a stream handle: the calling thread for hipStreamPerThread
 std::thread::id ws_thread(hipStream_t s) {
   return s == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
@@ -134,107 +175,114 @@ std::thread::id ws_thread(hipStream_t s) {
 StreamWs *ws_find(plfx_ctx *ctx, hipStream_t s) {
   const std::thread::id tid = ws_thread(s);
   for (StreamWs &w : ctx->wss)
-    if (w.in_use && w.stream == s && w.tid == tid) return &w;
+    if (w.in_use && !w.retired && w.stream == s && w.tid == tid) return &w;
   return nullptr;
 }
 
-void ws_carve(StreamWs &w, void *base) {
+void orphan_thread_entries(plfx_ctx *ctx, std::thread::id tid) {
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  for (StreamWs &w : ctx->wss)
+    if (w.in_use && !w.retired && w.stream == hipStreamPerThread && w.tid == tid) {
+      w.retired = true;
+      w.stream = nullptr;
+      w.tid = std::thread::id();
+    }
+}
+
+void ws_carve(StreamWs &w, void *base, void *tt) {
   char *b = static_cast<char *>(base);
   w.ws = reinterpret_cast<unsigned long long *>(b);
   w.lnl_partials = reinterpret_cast<double *>(b + kWsBytes);
   w.lnl_ticket = reinterpret_cast<unsigned long long *>(b + kWsBytes + kLnlPartialBytes);
+  w.tt = static_cast<char *>(tt);
+}
+
+// An entry taken by stream s: keyed to it, marked if s is capturing, and for
+// hipStreamPerThread remembered by the calling thread (retired at its exit).
+StreamWs *ws_take(plfx_ctx *ctx, StreamWs &w, hipStream_t s) {
+  w.in_use = true;
+  w.retired = false;
+  w.captured = false;
+  w.stream = s;
+  w.tid = ws_thread(s);
+  if (s == hipStreamPerThread &&
+      std::find(t_entries.ctxs.begin(), t_entries.ctxs.end(), ctx) == t_entries.ctxs.end())
+    t_entries.ctxs.push_back(ctx);
+  return &w;
 }
 
 // The workspace of stream s: its own, else a free pool entry (zero at rest),
-// else a new allocation (zeroed in order on s) -- not inside a stream capture,
-// where the allocation would not be part of the graph.
+// else a retired per-thread entry reclaimed after a device synchronisation,
+// else a new allocation (zeroed in order on s) -- neither of the last two
+// inside a stream capture.  An entry used while s is capturing is marked: the
+// graph keeps using it after the capture.
 StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
-  if (StreamWs *w = ws_find(ctx, s)) return w;
   *rc = PLFX_OK;
-  for (StreamWs &w : ctx->wss)
-    if (!w.in_use) {
-      w.in_use = true;
-      w.stream = s;
-      w.tid = ws_thread(s);
-      return &w;
+  const bool cap = capturing(s);
+  StreamWs *got = ws_find(ctx, s);
+  if (!got)
+    for (StreamWs &w : ctx->wss)
+      if (!w.in_use) {
+        got = ws_take(ctx, w, s);
+        break;
+      }
+  if (!got && !cap) {
+    // entries of exited threads' per-thread streams (not captured: those
+    // stay retired): their last launches must be done before reuse
+    bool any = false;
+    for (StreamWs &w : ctx->wss) any |= w.in_use && w.retired && !w.captured;
+    if (any) {
+      hipError_t e = hipDeviceSynchronize();
+      if (e != hipSuccess) {
+        *rc = hip_fail(ctx, e, "reclaiming workspaces of exited threads");
+        return nullptr;
+      }
+      for (StreamWs &w : ctx->wss)
+        if (w.in_use && w.retired && !w.captured) w.in_use = false;
+      for (StreamWs &w : ctx->wss)
+        if (!w.in_use) {
+          got = ws_take(ctx, w, s);
+          break;
+        }
     }
+  }
+  if (got) {
+    got->captured = got->captured || cap;
+    return got;
+  }
   if ((int)ctx->wss.size() >= PLFX_MAX_STREAMS) {
     *rc = fail(ctx, PLFX_ERR_INVALID,
                "more than %d streams in use with one context (release idle ones with "
                "plfx_ctx_release_stream)", PLFX_MAX_STREAMS);
     return nullptr;
   }
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (s && hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
+  if (cap) {
     *rc = fail(ctx, PLFX_ERR_INVALID,
                "more than %d streams in use and this one is being captured: issue one call on "
                "the stream before capturing (its reduction workspace is allocated then)", kWsPool);
     return nullptr;
   }
+  // stream-ordered on s: usable by s's next launch with no host wait (and
+  // freed stream-ordered at destroy, which a plain hipFree would turn into a
+  // wait for the whole device)
   void *block = nullptr;
-  hipError_t e = hipMalloc(&block, kWsEntryBytes);
+  hipError_t e = hipMallocAsync(&block, kWsEntryBytes + kTtEntryBytes, s);
   if (e != hipSuccess) {
-    *rc = fail(ctx, PLFX_ERR_NOMEM, "workspace hipMalloc(%zu): %s", kWsEntryBytes, hipGetErrorString(e));
+    *rc = fail(ctx, PLFX_ERR_NOMEM, "workspace hipMallocAsync(%zu): %s", kWsEntryBytes + kTtEntryBytes,
+               hipGetErrorString(e));
     return nullptr;
   }
   e = hipMemsetAsync(block, 0, kWsEntryBytes, s);
-  if (e == hipSuccess && !s) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
-    (void)hipFree(block);
+    (void)hipFreeAsync(block, s);
     *rc = hip_fail(ctx, e, "workspace memset");
     return nullptr;
   }
   ctx->ws_blocks.push_back(block);
   StreamWs w;
-  w.stream = s;
-  w.tid = ws_thread(s);
-  w.in_use = true;
-  ws_carve(w, block);
+  ws_carve(w, block, static_cast<char *>(block) + kWsEntryBytes);
   ctx->wss.push_back(w);
-  return &ctx->wss.back();
-}
-
-// Tip/tip protein combination tables of one stream entry: the two constant
-// 576-code arrays (combo k = code1 * 24 + code2) and, per node of a batch, a
-// 576 x 80 table of the node's dtype and 576 scaler bytes (plf_prot.hpp
-// prot_tiptip_gather_kernel).  Allocated on the entry's first tip/tip protein
-// call (not inside a capture: the caller then takes the direct kernel).
-constexpr size_t kTtCodeBytes = 2048;
-constexpr size_t kTtTabBytes = (size_t)plfx::kProtCombos * 80 * sizeof(double);
-constexpr size_t kTtScBytes = 1024;
-constexpr size_t kTtBytes = kTtCodeBytes + (size_t)plfx::kMaxBatch * (kTtTabBytes + kTtScBytes);
-
-void *tt_for(plfx_ctx *ctx, StreamWs *w, hipStream_t s) {
-  if (w->tt) return w->tt;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (s && hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) return nullptr;
-  struct Codes {
-    uint8_t v[kTtCodeBytes] = {};
-    Codes() {
-      for (int k = 0; k < plfx::kProtCombos; k++) {
-        v[k] = (uint8_t)(k / 24);
-        v[1024 + k] = (uint8_t)(k % 24);
-      }
-    }
-  };
-  static const Codes codes;  // thread-safe one-time initialisation
-
-  // on failure the caller takes the direct kernel; the error is cleared so
-  // that the launch check after it does not report it
-  void *b = nullptr;
-  if (hipMalloc(&b, kTtBytes) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  if (hipMemcpyAsync(b, codes.v, kTtCodeBytes, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess) {
-    (void)hipGetLastError();
-    (void)hipFree(b);
-    return nullptr;
-  }
-  ctx->ws_blocks.push_back(b);  // freed with the context
-  w->tt = b;
-  return b;
+  return ws_take(ctx, ctx->wss.back(), s);
 }
 
 // the workspace of stream s as `out`; returns from the caller on failure
@@ -246,8 +294,18 @@ void *tt_for(plfx_ctx *ctx, StreamWs *w, hipStream_t s) {
     if (!out) return wrc_;                        \
   } while (0)
 
+// [a, a + na) and [b, b + nb) share a byte
+bool overlap(const void *a, size_t na, const void *b, size_t nb) {
+  const uintptr_t pa = reinterpret_cast<uintptr_t>(a), pb = reinterpret_cast<uintptr_t>(b);
+  return na > 0 && nb > 0 && pa < pb + nb && pb < pa + na;
+}
+
+// clv_bytes: bytes of one CLV of the call (n * 4 categories * states * element
+// size); a tip child is n code bytes.  The parent may not share a byte with
+// either child: every site's children are read by other blocks than the one
+// writing that site's parent.
 int check_dev_args(plfx_ctx *ctx, const void *x1, const void *x2, const void *x3, const void *EV,
-                   int64_t n, const void *left, const void *right) {
+                   int64_t n, const void *left, const void *right, size_t clv_bytes) {
   if (!ctx) return PLFX_ERR_INVALID;
   if (n < 0) return fail(ctx, PLFX_ERR_INVALID, "n < 0 (%lld)", (long long)n);
   if (n == 0) return PLFX_OK;
@@ -255,7 +313,8 @@ int check_dev_args(plfx_ctx *ctx, const void *x1, const void *x2, const void *x3
     return fail(ctx, PLFX_ERR_INVALID, "null CLV/matrix pointer");
   if (!aligned16(x1) || !aligned16(x2) || !aligned16(x3))
     return fail(ctx, PLFX_ERR_INVALID, "CLV pointers must be 16-byte aligned");
-  if (x3 == x1 || x3 == x2) return fail(ctx, PLFX_ERR_INVALID, "x3 may not alias x1/x2");
+  if (overlap(x3, clv_bytes, x1, clv_bytes) || overlap(x3, clv_bytes, x2, clv_bytes))
+    return fail(ctx, PLFX_ERR_INVALID, "x3 may not overlap x1/x2");
   return PLFX_OK;
 }
 
@@ -263,7 +322,7 @@ template <typename T>
 int plf_dev(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int64_t n, const T *left,
             const T *right, const int32_t *wgt, uint8_t *scaler, int64_t *scaler_sum,
             void *stream) {
-  int rc = check_dev_args(ctx, x1, x2, x3, EV, n, left, right);
+  int rc = check_dev_args(ctx, x1, x2, x3, EV, n, left, right, (size_t)n * 16 * sizeof(T));
   if (rc != PLFX_OK) return rc;
   hipStream_t s = pick(ctx, stream);
   if (n == 0) {
@@ -282,12 +341,12 @@ int ensure_dbuf(plfx_ctx *ctx, size_t bytes) {
   if (bytes <= ctx->d_cap) return PLFX_OK;
   if (ctx->d_buf) {
     PLFX_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    PLFX_HIP(ctx, hipFree(ctx->d_buf));
+    PLFX_HIP(ctx, hipFreeAsync(ctx->d_buf, ctx->stream));
     ctx->d_buf = nullptr;
     ctx->d_cap = 0;
   }
-  hipError_t e = hipMalloc(&ctx->d_buf, bytes);
-  if (e != hipSuccess) return fail(ctx, PLFX_ERR_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  hipError_t e = hipMallocAsync(&ctx->d_buf, bytes, ctx->stream);
+  if (e != hipSuccess) return fail(ctx, PLFX_ERR_NOMEM, "hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
   ctx->d_cap = bytes;
   return PLFX_OK;
 }
@@ -369,16 +428,23 @@ int plf_host(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int n,
   return PLFX_OK;
 }
 
-// One node of a kind (tips = number of tip children, tip child first).
-int check_node(plfx_ctx *ctx, const plfx_node &d, int tips, int64_t n, int i) {
+// One node of a kind (tips = number of tip children, tip child first); i
+// names it in the message (the op index in a traversal); clv_bytes as
+// check_dev_args.
+int check_node(plfx_ctx *ctx, const plfx_node &d, int tips, int64_t n, int i, size_t clv_bytes) {
   if (n <= 0) return PLFX_OK;
   if (!d.x1 || !d.x2 || !d.x3 || !d.left || !d.right)
     return fail(ctx, PLFX_ERR_INVALID, "node %d: null CLV/tip/matrix pointer", i);
   if ((tips < 1 && !aligned16(d.x1)) || (tips < 2 && !aligned16(d.x2)) || !aligned16(d.x3))
     return fail(ctx, PLFX_ERR_INVALID, "node %d: CLV pointers must be 16-byte aligned", i);
-  if (d.x3 == d.x1 || d.x3 == d.x2)
-    return fail(ctx, PLFX_ERR_INVALID, "node %d: x3 may not alias a child", i);
+  const size_t b1 = tips >= 1 ? (size_t)n : clv_bytes, b2 = tips >= 2 ? (size_t)n : clv_bytes;
+  if (overlap(d.x3, clv_bytes, d.x1, b1) || overlap(d.x3, clv_bytes, d.x2, b2))
+    return fail(ctx, PLFX_ERR_INVALID, "node %d: x3 may not overlap a child", i);
   return PLFX_OK;
+}
+
+size_t clv_bytes_of(int dtype, int states, int64_t n) {
+  return (size_t)(n > 0 ? n : 0) * 4 * states * (dtype == PLFX_F32 ? 4 : 8);
 }
 
 // A tip/tip protein node whose values sit in its stream's combination tables
@@ -397,13 +463,14 @@ struct TabRef {
 int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, const void *EV,
                int64_t n, const int32_t *wgt, hipStream_t s, int tips,
                const void *tipvec = nullptr, int states = 4, int flags = PLFX_EXACT,
-               int *launches = nullptr, std::vector<TabRef> *tabs = nullptr) {
+               int *launches = nullptr, std::vector<TabRef> *tabs = nullptr,
+               const int *ids = nullptr) {
   if (tabs) tabs->clear();
   if (count < 0 || n < 0 || (count > 0 && (!nodes || !EV)))
     return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
   for (int i = 0; i < count; i++) {
     const plfx_node &d = nodes[i];
-    int rc = check_node(ctx, d, tips, n, i);
+    int rc = check_node(ctx, d, tips, n, ids ? ids[i] : i, clv_bytes_of(dtype, states, n));
     if (rc != PLFX_OK) return rc;
     if (n == 0 && d.scaler_sum) PLFX_HIP(ctx, hipMemsetAsync(d.scaler_sum, 0, sizeof(int64_t), s));
   }
@@ -413,15 +480,16 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
     // both children coded tips: the node's 576 code pairs through its own
     // kernel, then x3 / scaler / sum gathered by code pair (a write stream;
     // the direct kernel is compute-bound: 77 us f64, 95 us f32 per 2^18 sites)
-    if (char *tt = static_cast<char *>(tt_for(ctx, w, s))) {
-      const uint8_t *cc1 = reinterpret_cast<const uint8_t *>(tt), *cc2 = cc1 + 1024;
+    {
+      char *tt = w->tt;
+      const uint8_t *cc1 = ctx->tt_codes, *cc2 = cc1 + 1024;
       for (int j = 0; j < count; j += plfx::kMaxBatch) {
         const int c = std::min(count - j, plfx::kMaxBatch);
         plfx::NodeDescH comb[plfx::kMaxBatch];
         plfx::ProtGatherDescH g[plfx::kMaxBatch];
         for (int i = 0; i < c; i++) {
           const plfx_node &d = nodes[j + i];
-          char *tab = tt + kTtCodeBytes + (size_t)i * (kTtTabBytes + kTtScBytes);
+          char *tab = tt + (size_t)i * (kTtTabBytes + kTtScBytes);
           uint8_t *tsc = reinterpret_cast<uint8_t *>(tab + kTtTabBytes);
           comb[i] = plfx::NodeDescH{cc1, cc2, tab, d.left, d.right, tsc, nullptr};
           g[i] = plfx::ProtGatherDescH{static_cast<const uint8_t *>(d.x1), static_cast<const uint8_t *>(d.x2),
@@ -522,25 +590,40 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
     if (v > 0) ctx->max_blocks = v;
   }
   if (const char *env = std::getenv("PLFX_FUSE")) ctx->fuse = std::atoi(env);
-  // the workspace pool: kWsPool entries in one allocation, zeroed before return
-  void *pool = nullptr;
-  if (hipMalloc(&pool, kWsPool * kWsEntryBytes) != hipSuccess) {
+  // the workspace pool: kWsPool entries (reduction words zeroed before return,
+  // tip/tip tables), and the tables' constant code arrays
+  auto undo = [&](int code) {
+    for (void *b : ctx->ws_blocks) (void)hipFreeAsync(b, ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
-    return PLFX_ERR_NOMEM;
+    return code;
+  };
+  void *pool = nullptr, *tabs = nullptr, *codes = nullptr;
+  if (hipMallocAsync(&pool, kWsPool * kWsEntryBytes, ctx->stream) != hipSuccess) return undo(PLFX_ERR_NOMEM);
+  ctx->ws_blocks.push_back(pool);
+  if (hipMallocAsync(&tabs, kWsPool * kTtEntryBytes, ctx->stream) != hipSuccess) return undo(PLFX_ERR_NOMEM);
+  ctx->ws_blocks.push_back(tabs);
+  if (hipMallocAsync(&codes, kTtCodeBytes, ctx->stream) != hipSuccess) return undo(PLFX_ERR_NOMEM);
+  ctx->ws_blocks.push_back(codes);
+  uint8_t cc[kTtCodeBytes] = {};
+  for (int k = 0; k < plfx::kProtCombos; k++) {
+    cc[k] = (uint8_t)(k / 24);
+    cc[1024 + k] = (uint8_t)(k % 24);
   }
   if (hipMemsetAsync(pool, 0, kWsPool * kWsEntryBytes, ctx->stream) != hipSuccess ||
-      hipStreamSynchronize(ctx->stream) != hipSuccess) {
-    (void)hipFree(pool);
-    (void)hipStreamDestroy(ctx->stream);
-    delete ctx;
-    return PLFX_ERR_HIP;
-  }
-  ctx->ws_blocks.push_back(pool);
+      hipMemcpyAsync(codes, cc, kTtCodeBytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess)
+    return undo(PLFX_ERR_HIP);
+  ctx->tt_codes = static_cast<uint8_t *>(codes);
   for (int i = 0; i < kWsPool; i++) {
     StreamWs w;
-    ws_carve(w, static_cast<char *>(pool) + i * kWsEntryBytes);
+    ws_carve(w, static_cast<char *>(pool) + i * kWsEntryBytes, static_cast<char *>(tabs) + i * kTtEntryBytes);
     ctx->wss.push_back(w);
+  }
+  {
+    std::lock_guard<std::mutex> l(g_live_mu);
+    g_live.push_back(ctx);
   }
   *out = ctx;
   return PLFX_OK;
@@ -549,24 +632,40 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
 int plfx_ctx_destroy(plfx_ctx *ctx) {
   if (!ctx) return PLFX_OK;
   {
+    // no exiting thread may retire entries of this context from here on
+    std::lock_guard<std::mutex> l(g_live_mu);
+    g_live.erase(std::remove(g_live.begin(), g_live.end(), ctx), g_live.end());
+  }
+  {
     DeviceGuard guard(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->d_buf) (void)hipFree(ctx->d_buf);
+    // all device memory of the context is stream-ordered (hipMallocAsync):
+    // freed on its stream below, since hipFree would wait for the whole device
+    if (ctx->d_buf) (void)hipFreeAsync(ctx->d_buf, ctx->stream);
     if (ctx->d2h_stream) {
       (void)hipStreamSynchronize(ctx->d2h_stream);
       (void)hipStreamDestroy(ctx->d2h_stream);
     }
     for (hipEvent_t e : ctx->chunk_done)
       if (e) (void)hipEventDestroy(e);
-    // other streams' workspaces: their last launches must be done before the
-    // free.  A stream still holding one may already be destroyed (HIP does not
-    // validate handles), so it is never touched here: streams released with
-    // plfx_ctx_release_stream cost nothing, any other holder makes destroy wait
-    // for the device (plfx.h, "Streams and the scaler-sum workspace").
-    bool held = false;
-    for (StreamWs &w : ctx->wss) held |= w.in_use && w.stream != ctx->stream;
-    if (held) (void)hipDeviceSynchronize();
-    for (void *b : ctx->ws_blocks) (void)hipFree(b);
+    // Workspace entries still held: their last launches must be done before
+    // the free.  A stream holding one is waited for (it must still exist,
+    // plfx.h); the device is waited for only when no stream can stand for the
+    // entry's work -- an entry used under a capture (the graph may be
+    // replaying on any stream), a retired one, or another thread's
+    // hipStreamPerThread (this thread cannot name that stream).
+    bool device_wide = false;
+    const std::thread::id me = std::this_thread::get_id();
+    for (StreamWs &w : ctx->wss) {
+      if (!w.in_use) continue;
+      if (w.captured || w.retired || (w.stream == hipStreamPerThread && w.tid != me))
+        device_wide = true;
+      else if (w.stream != ctx->stream)
+        (void)hipStreamSynchronize(w.stream);
+    }
+    if (device_wide) (void)hipDeviceSynchronize();
+    for (void *b : ctx->ws_blocks) (void)hipFreeAsync(b, ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -598,10 +697,15 @@ int plfx_ctx_release_stream(plfx_ctx *ctx, void *stream) {
   hipStream_t s = pick(ctx, stream);
   StreamWs *w = ws_find(ctx, s);
   if (!w) return PLFX_OK;  // no workspace held: nothing to release
+  if (capturing(s))  // a wait on a capturing stream would invalidate the capture
+    return fail(ctx, PLFX_ERR_INVALID, "stream is being captured: release it after the capture ends");
   // the stream's last sum-producing launch must be done before another stream
   // may take the entry (it is zero again once that launch has finished)
   PLFX_HIP(ctx, hipStreamSynchronize(s));
-  w->in_use = false;
+  // a graph captured through the entry keeps using its words (sum tickets,
+  // queue heads, tip/tip tables): retired, never handed to another stream
+  if (w->captured) w->retired = true;
+  else w->in_use = false;
   w->stream = nullptr;
   w->tid = std::thread::id();
   return PLFX_OK;
@@ -651,7 +755,8 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
                                  (const double *)right, wgt, scaler, scaler_sum, stream);
   }
   if (states != 20) return fail(ctx, PLFX_ERR_UNSUPPORTED, "states=%d not built (4, 20)", states);
-  int rc = check_dev_args(ctx, x1, x2, x3, EV, n, left, right);
+  int rc = check_dev_args(ctx, x1, x2, x3, EV, n, left, right,
+                          (size_t)n * 80 * (dtype == PLFX_F32 ? 4 : 8));
   if (rc != PLFX_OK) return rc;
   hipStream_t s = pick(ctx, stream);
   if (n == 0) {
@@ -789,6 +894,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
     return fail(ctx, PLFX_ERR_INVALID, "bad traverse arguments");
   const size_t es = dtype == PLFX_F32 ? 4 : 8;
   const size_t mat = (size_t)states * states * 4;  // C*S*S values per matrix
+  const size_t cb = clv_bytes_of(dtype, states, n);
   auto is_tip = [&](int sl) { return tips && tips[sl]; };
   // dependency levels: RAW on children (cdep), WAR/WAW on the parent slot (pdep)
   std::vector<int> level(nops, 0), pdep(nops, 0), w1(nops, -1), w2(nops, -1);
@@ -952,6 +1058,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   sched[4] = (int)triples.size();
   for (int j = 0; j < nops; j++) sched[5] += used[j] ? 0 : 1;
   std::vector<plfx_node> batch[3];  // by number of tip children
+  std::vector<int> bop[3];           // the op index of each batch entry
   std::vector<plfx::TripleDescH> tb[3];
   std::vector<plfx::SeptetDescH> sb[3];
   // protein: the previous level's tip/tip nodes still in their
@@ -964,6 +1071,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   for (int lv = 0; lv < nlev; lv++) {
     for (int k = 0; k < 3; k++) {
       batch[k].clear();
+      bop[k].clear();
       tb[k].clear();
       sb[k].clear();
     }
@@ -975,7 +1083,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         const int j = t.ops[q];
         const plfx_trav_op &o = ops[j];
         int kq;
-        const int rc = check_node(ctx, node_of(j, &kq), kq, n, j);
+        const int rc = check_node(ctx, node_of(j, &kq), kq, n, j, cb);
         if (rc != PLFX_OK) return rc;
         if (q < leaf_ops) {  // level 1: the leaves (CLVs or tip codes), child1 then child2
           d.g[2 * q] = t.tips ? (const void *)tips[o.child1] : clv[o.child1];
@@ -1004,7 +1112,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
       for (int q = 0; q < 7; q++) {
         int kq;
         const plfx_node nd = node_of(id[q], &kq);
-        const int rc = check_node(ctx, nd, kq, n, id[q]);
+        const int rc = check_node(ctx, nd, kq, n, id[q], cb);
         if (rc != PLFX_OK) return rc;
         if (q < 4) {
           d.g[2 * q] = nd.x1;
@@ -1022,8 +1130,8 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
       if (level[t.a] != lv) continue;
       int ka, kb, kp;
       const plfx_node A = node_of(t.a, &ka), B = node_of(t.b, &kb), P = node_of(t.p, &kp);
-      for (int rc : {check_node(ctx, A, ka, n, t.a), check_node(ctx, B, kb, n, t.b),
-                     check_node(ctx, P, kp, n, t.p)})
+      for (int rc : {check_node(ctx, A, ka, n, t.a, cb), check_node(ctx, B, kb, n, t.b, cb),
+                     check_node(ctx, P, kp, n, t.p, cb)})
         if (rc != PLFX_OK) return rc;
       // P's children as op P names them: child1 = A's slot or B's slot
       const bool a_first = ops[t.p].child1 == ops[t.a].parent;
@@ -1039,6 +1147,7 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
       int kind;
       const plfx_node nd = node_of(j, &kind);
       batch[kind].push_back(nd);
+      bop[kind].push_back(j);
     }
     for (int k = 0; k < 3; k++) {
       for (size_t i = 0; i < sb[k].size(); i += plfx::kMaxSeptets) {
@@ -1075,13 +1184,17 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
         };
         std::vector<plfx::ProtTabDescH> tab;
         std::vector<plfx_node> rest;
-        for (const plfx_node &nd : batch[0]) {
+        std::vector<int> rest_op;
+        for (size_t q = 0; q < batch[0].size(); q++) {
+          const plfx_node &nd = batch[0][q];
           const TabRef *a = find(nd.x1), *b = find(nd.x2);
           if (!a || !b) {
             rest.push_back(nd);
+            rest_op.push_back(bop[0][q]);
             continue;
           }
-          const int rc = check_node(ctx, nd, 0, n, (int)tab.size());
+          // these nodes do not go through batch_impl's checks: checked here
+          const int rc = check_node(ctx, nd, 0, n, bop[0][q], cb);
           if (rc != PLFX_OK) return rc;
           tab.push_back(plfx::ProtTabDescH{a->tab, b->tab, a->ca, a->cb, b->ca, b->cb, nd.x3, nd.left,
                                            nd.right, nd.scaler, nd.scaler_sum});
@@ -1094,10 +1207,12 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
           sched[6]++;
         }
         batch[0].swap(rest);
+        bop[0].swap(rest_op);
       }
       if (batch[k].empty()) continue;
       int rc = batch_impl(ctx, dtype, batch[k].data(), (int)batch[k].size(), EV, n, wgt, s, k,
-                          tipvec, states, flags, &sched[6], k == 2 && tab_mode ? &cur_tabs : nullptr);
+                          tipvec, states, flags, &sched[6], k == 2 && tab_mode ? &cur_tabs : nullptr,
+                          bop[k].data());
       if (rc != PLFX_OK) return rc;
     }
     prev_tabs.swap(cur_tabs);

@@ -61,13 +61,21 @@
  * inside hipStreamBeginCapture: issue one call on it before capturing).
  * plfx_ctx_release_stream() waits for a stream and returns its workspace to
  * the pool -- call it before destroying a stream used with the context, or
- * when rotating through many streams.  A captured graph keeps the workspace
- * of the stream it was captured on, so its replays must not overlap other
- * work on that stream's workspace, and must not outlive the context.
- * plfx_ctx_destroy() synchronises the context's stream; if any other stream
- * still holds a workspace it waits for the whole device (hipDeviceSynchronize,
- * which must not overlap a global-mode capture in another thread), so release
- * streams first to keep destroy local.
+ * when rotating through many streams (not while the stream is being captured:
+ * PLFX_ERR_INVALID).  A captured graph keeps the workspace of the stream it
+ * was captured on, so its replays must not overlap other work on that
+ * workspace, and must not outlive the context; releasing such a stream retires
+ * its workspace (no other stream is ever given it) instead of returning it to
+ * the pool.  A hipStreamPerThread workspace whose thread exits without
+ * releasing it is retired too, and reclaimed (after a device-wide wait, not
+ * inside a capture) when the context runs out of workspaces.
+ * plfx_ctx_destroy() waits for the context's stream and for every other
+ * stream still holding a workspace -- so such streams must still exist at
+ * destroy; release them first otherwise -- and waits for the whole device
+ * (hipDeviceSynchronize, which must not overlap a global-mode capture in
+ * another thread) only when a workspace was used under a capture, is retired,
+ * or belongs to another thread's hipStreamPerThread.  Graph replays still in
+ * flight must finish before destroy.
  * The same workspace also holds the tile/chunk queues of the protein f64 FMA
  * kernel (from 2^20 sites) and of the fused six-level tree passes: blocks or
  * waves that run ahead take more of the alignment instead of a fixed share
@@ -79,7 +87,11 @@
  * cannot check it cheaply and leave it to the caller.
  *
  * No allocation happens per call after warm-up (the host entry points keep
- * grow-only staging buffers in the context).
+ * grow-only staging buffers in the context).  Each workspace also holds the
+ * protein tip/tip combination tables (about 11.8 MB; the pool's
+ * PLFX_WS_POOL of them are allocated with the context).
+ * Every entry point rejects a parent CLV x3 that shares any byte with a child
+ * it reads (PLFX_ERR_INVALID).
  *
  * Timing note: after an idle gap of ~0.3 s or more the MI355X lowers its
  * shader clock to ~1.8-2.0 GHz for the first ~10-15 ms of renewed load
@@ -293,13 +305,13 @@ int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const
  * plfx_plf_dev_gen (PLFX_FMA: protein nodes on the f64 / f32 matrix cores;
  * DNA is always exact).  plfx_traverse == flags PLFX_EXACT, no tips, no tipvec.
  * Protein tip/tip nodes (here and in plfx_plf_tips_dev_gen) are evaluated once
- * per code pair (24 x 24) into tables of the stream's workspace (about 11.8 MB,
- * allocated on that stream's first such call, freed with the context) and
- * gathered per site: the same values as the direct computation; a capture on
- * a stream without the tables yet runs the direct kernel.  In a traversal in
- * FMA mode, a node whose two children are such nodes of the level before
- * stages its children from their tables instead of reading their CLVs back
- * (the CLVs are still written; the results are the same). */
+ * per code pair (24 x 24) into tables of the stream's workspace (allocated
+ * with the workspace, so also a stream's first call inside a capture uses
+ * them) and gathered per site: the same values as the direct computation.  In
+ * a traversal (exact and FMA modes, f64 and f32), a node whose two children
+ * are such nodes of the level before stages its children from their tables
+ * instead of reading their CLVs back (the CLVs are still written; the results
+ * are the same). */
 int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const plfx_trav_op *ops,
                        int nops, void *const *clv, const uint8_t *const *tips, int nslots,
                        const void *pmats,

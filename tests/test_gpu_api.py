@@ -4,6 +4,8 @@ benchmarked sizes: protein FMA at 2^18 sites (BASELINE configs[4]) and 64
 batched nodes x 2^20 sites (configs[3]'s per-GPU shard).  Bar: CLVs, scaler
 bytes and sums bit-exact against the oracle; protein FMA also within 1e-12
 (relative to the site's largest value) of the unfused loop."""
+import time
+
 import numpy as np
 import pytest
 
@@ -269,7 +271,7 @@ def test_release_stream_recycles_workspaces(oracle):
     PLFX_MAX_STREAMS streams used one after another work when each is released;
     without releases the (MAX_STREAMS+1)-th is refused until one is released.
     Destroying the context with streams still holding workspaces waits for
-    the device, so the sums are complete after close()."""
+    those streams, so the sums are complete after close()."""
     import plfx
     import torch
 
@@ -460,3 +462,228 @@ def test_binding_rejects_host_or_mistyped_tensors(ctx):
     ctx.scaler_sum(sc, None, s, n=n)
     torch.cuda.synchronize()
     assert int(s.item()) == 0
+
+
+def _kernel_nodes(g):
+    """Kernel nodes of a captured torch graph (made with keep_graph=True)."""
+    import ctypes
+
+    hip = _hip()
+    graph = ctypes.c_void_p(int(g.raw_cuda_graph()))
+    n = ctypes.c_size_t(0)
+    assert hip.hipGraphGetNodes(graph, None, ctypes.byref(n)) == 0
+    nodes = (ctypes.c_void_p * n.value)()
+    assert hip.hipGraphGetNodes(graph, nodes, ctypes.byref(n)) == 0
+    k = 0
+    for nd in nodes:
+        t = ctypes.c_int(-1)
+        assert hip.hipGraphNodeGetType(ctypes.c_void_p(nd), ctypes.byref(t)) == 0
+        k += t.value == 0  # hipGraphNodeTypeKernel
+    return k
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_tiptip_tables_on_a_first_call_inside_capture(oracle, dtype):
+    """the tip/tip combination tables come with the
+    workspace, so the FIRST call of a fresh context on a fresh stream, made
+    inside a graph capture, takes the table path (2 kernels: the 576 code-pair
+    tables, then the per-site gather) -- no allocation, no wait on the
+    caller's stream.  Replays are bit-exact against the oracle."""
+    import plfx
+    import torch
+
+    S, n = 20, 3001
+    rng = np.random.default_rng(5)
+    EV = (rng.random(S * S) - 0.25).astype(dtype)
+    left = (rng.random(4 * S * S) * 1e-11).astype(dtype)
+    right = rng.random(4 * S * S).astype(dtype)
+    w = rng.integers(1, 5, n).astype(np.int32)
+    c1, c2 = oracle.random_protein_codes(rng, n, 0.3), oracle.random_protein_codes(rng, n, 0.3)
+    e1, e2 = oracle.expand_protein_tips(c1, dtype), oracle.expand_protein_tips(c2, dtype)
+    f3, fsc, finc = oracle.plf_generic(S, 4, e1, e2, EV, left, right, w, fma=True)
+    assert 0 < fsc.sum() < n
+    t = [dev(a) for a in (c1, c2, EV, left, right, w)]
+    x3 = torch.empty(4 * S * n, dtype=t[2].dtype, device="cuda")
+    sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with plfx.Context(0) as c:
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.graph(g, stream=st):
+            c.plf_tips_dev(x3, t[2], n, t[3], t[4], tip1=t[0], tip2=t[1], wgt=t[5], scaler=sc,
+                           scaler_sum=s, states=S, fma=True, stream=st)
+        assert _kernel_nodes(g) == 2
+        g.instantiate()
+        for _ in range(2):
+            x3.zero_()
+            s.zero_()
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            assert np.array_equal(bits(x3.cpu().numpy()), bits(f3))
+            assert np.array_equal(sc.cpu().numpy(), fsc) and int(s.item()) == finc
+        del g
+
+
+def test_x3_partial_overlap_rejected(ctx):
+    """a parent CLV sharing ANY byte with a child is
+    refused (PLFX_ERR_INVALID) on every device entry point -- not only
+    x3 == x1 -- while an adjacent, non-overlapping x3 is accepted."""
+    import plfx
+    import torch
+
+    n = 1000
+    for dt, V, states in ((torch.float64, 16, 4), (torch.float32, 16, 4), (torch.float64, 80, 20),
+                          (torch.float32, 80, 20)):
+        buf = torch.rand(V * (3 * n + 8), dtype=dt, device="cuda")
+        x1, x2 = buf[:V * n], buf[V * n:2 * V * n]
+        EV, P = torch.rand(states * states, dtype=dt, device="cuda"), torch.rand(4 * states * states, dtype=dt, device="cuda")
+        step = 16 // buf.element_size()  # the smallest 16-B-aligned shift
+        for x3 in (buf[step:step + V * n], buf[V * n - step:2 * V * n - step],   # into x1's tail
+                   buf[2 * V * n - V * n // 2:3 * V * n - V * n // 2]):          # half into x2
+            with pytest.raises(plfx.PlfxError) as ei:
+                ctx.plf_dev_gen(x1, x2, x3, EV, P, P, states, n=n)
+            assert ei.value.code == plfx.ERR_INVALID and "overlap" in str(ei.value)
+            with pytest.raises(plfx.PlfxError) as ei:
+                ctx.plf_batch_dev([dict(x1=x1, x2=x2, x3=x3, left=P, right=P)] * 2, EV, n, states=states)
+            assert ei.value.code == plfx.ERR_INVALID and "overlap" in str(ei.value)
+        ctx.plf_dev_gen(x1, x2, buf[2 * V * n:3 * V * n], EV, P, P, states, n=n)  # adjacent: fine
+        if states == 4:
+            x3 = buf[step:step + V * n]
+            with pytest.raises(plfx.PlfxError) as ei:
+                ctx.plf_dev(x1, x2, x3, EV, P, P, n=n)
+            assert ei.value.code == plfx.ERR_INVALID
+            # a coded tip child (one byte per site) inside the parent's bytes
+            codes = buf[2 * V * n:3 * V * n].view(torch.uint8)[64:64 + n]
+            with pytest.raises(plfx.PlfxError) as ei:
+                ctx.plf_tips_dev(buf[2 * V * n:3 * V * n], EV, n, P, P, tip1=codes, x2=x2)
+            assert ei.value.code == plfx.ERR_INVALID
+    torch.cuda.synchronize()
+
+
+def test_destroy_waits_for_its_streams_not_the_device(oracle):
+    """plfx_ctx_destroy waits for the streams holding the
+    context's workspaces, not for the whole device -- a long kernel on an
+    unrelated stream is still running when close() returns -- and the work of
+    a stream that still holds a workspace is complete after close()."""
+    import plfx
+    import torch
+
+    n = 1 << 18
+    d = oracle.gen_hostmem(n, np.float64, 50)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    _, _, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+    other, mine = torch.cuda.Stream(), torch.cuda.Stream()
+    o3 = torch.empty_like(t["x1"])
+    s = torch.zeros(4, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    c = plfx.Context(0)
+    for i in range(4):
+        c.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s[i:i + 1],
+                  stream=mine)
+    # calibrate torch's spin kernel, then keep `other` busy for ~1.5 s
+    t0 = time.perf_counter()
+    torch.cuda._sleep(50_000_000)
+    torch.cuda.synchronize()
+    rate = 50_000_000 / max(time.perf_counter() - t0, 1e-4)
+    with torch.cuda.stream(other):
+        torch.cuda._sleep(int(1.5 * rate))
+        busy = torch.cuda.Event()
+        busy.record(other)
+    t0 = time.perf_counter()
+    c.close()  # `mine` still holds its workspace (not released)
+    dt = time.perf_counter() - t0
+    assert not busy.query(), "close() waited for an unrelated stream"
+    assert dt < 0.5
+    assert s.tolist() == [einc] * 4  # mine's launches were complete
+    torch.cuda.synchronize()
+
+
+def test_release_after_capture_retires_the_workspace(oracle):
+    """releasing a stream whose workspace a graph was
+    captured through must not hand that workspace to another stream -- the
+    graph's replays keep using its self-resetting sum words.  Capture on A,
+    release A, then replay the graph on A while stream B makes sum-producing
+    calls of its own: every sum exact.  Releasing a stream while it is being
+    captured is refused."""
+    import plfx
+    import torch
+
+    n = 1 << 18
+    d = oracle.gen_hostmem(n, np.float64, 51)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    _, _, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+    A, B = torch.cuda.Stream(), torch.cuda.Stream()
+    oa, ob = torch.empty_like(t["x1"]), torch.empty_like(t["x1"])
+    sa = torch.zeros(1, dtype=torch.int64, device="cuda")
+    sb = torch.zeros(16, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    with plfx.Context(0) as c:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=A):
+            c.plf_dev(t["x1"], t["x2"], oa, t["EV"], t["left"], t["right"], t["wgt"], None, sa, stream=A)
+            with pytest.raises(plfx.PlfxError) as ei:
+                c.release_stream(A)
+            assert ei.value.code == plfx.ERR_INVALID
+        c.release_stream(A)  # retires A's workspace: the graph still uses it
+        torch.cuda.synchronize()
+        with torch.cuda.stream(A):
+            for _ in range(8):
+                g.replay()
+        for i in range(16):  # B's first call takes a fresh pool entry
+            c.plf_dev(t["x1"], t["x2"], ob, t["EV"], t["left"], t["right"], t["wgt"], None, sb[i:i + 1],
+                      stream=B)
+        torch.cuda.synchronize()
+        assert int(sa.item()) == einc
+        assert sb.tolist() == [einc] * 16
+        c.release_stream(B)
+        del g
+
+
+def test_exited_threads_per_thread_workspaces_are_reclaimed(oracle):
+    """a thread that used hipStreamPerThread and exits without
+    releasing its workspace must not use up the context: PLFX_MAX_STREAMS + 6
+    short-lived threads, one after another, each making one sum-producing
+    call on its per-thread stream and exiting, all succeed with exact sums
+    (the exited threads' entries are retired and reclaimed)."""
+    import threading
+
+    import plfx
+    import torch
+
+    n = 4099
+    d = oracle.gen_hostmem(n, np.float64, 52)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    _, _, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+    k = plfx.MAX_STREAMS + 6
+    sums = torch.zeros(k, dtype=torch.int64, device="cuda")
+    o3 = torch.empty_like(t["x1"])
+    torch.cuda.synchronize()
+    errs = []
+    with plfx.Context(0) as c:
+        def worker(i):
+            try:
+                c.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None,
+                          sums[i:i + 1], stream=plfx.STREAM_PER_THREAD)
+                torch.cuda.current_stream().synchronize()
+                hip = _hip()
+                assert hip.hipStreamSynchronize(ctypes_stream_per_thread()) == 0
+            except Exception as e:  # reported on the main thread
+                errs.append(e)
+
+        for i in range(k):
+            th = threading.Thread(target=worker, args=(i,))
+            th.start()
+            th.join(timeout=60)
+    assert not errs, errs[:3]
+    torch.cuda.synchronize()
+    assert sums.tolist() == [einc] * k
+
+
+def ctypes_stream_per_thread():
+    import ctypes
+
+    import plfx
+
+    return ctypes.c_void_p(plfx.STREAM_PER_THREAD)

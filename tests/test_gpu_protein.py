@@ -538,13 +538,12 @@ def test_protein_root_lnl_tiles(ctx, oracle, dtype):
 @pytest.mark.parametrize("with_sum", [True, False])
 @pytest.mark.parametrize("warm", [False, True])
 def test_protein_tiptip_in_graph_capture(oracle, dtype, fma, with_sum, warm):
-    """A tip/tip protein node captured in a HIP graph: on a stream whose
-    combination tables do not exist yet (cold) the node takes the direct
-    tip/tip kernel of its mode (no allocation inside a capture); on a warmed
-    stream the capture holds the combination-table launch and the gather.
-    Replays are bit-identical to the oracle either way, with and without the
-    weighted sum.  A context of its own: a released stream's pool entry keeps
-    its tables, so a stream of the shared context may start with them."""
+    """A tip/tip protein node captured in a HIP graph: whether or not the
+    stream made a tip/tip call before (warm / cold), the capture holds the
+    combination-table launch and the gather (2 kernel nodes: the tables come
+    with the stream's workspace, nothing is allocated or waited for inside the
+    capture).  Replays are bit-identical to the oracle, with and without the
+    weighted sum."""
     import plfx
     import torch
 
@@ -576,9 +575,13 @@ def test_protein_tiptip_in_graph_capture(oracle, dtype, fma, with_sum, warm):
         ctx.plf_tips_dev(x3, t[2], n, t[3], t[4], tip1=t[0], x2=xd, wgt=t[5], scaler=sc,
                          scaler_sum=s, states=S, fma=fma, stream=st)
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
+    g = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(g, stream=st):
         call()
+    from test_gpu_api import _kernel_nodes
+
+    assert _kernel_nodes(g) == 2
+    g.instantiate()
     for _ in range(2):
         x3.zero_()
         if s is not None:
@@ -599,10 +602,11 @@ def test_protein_tiptip_in_graph_capture(oracle, dtype, fma, with_sum, warm):
 @pytest.mark.parametrize("with_sum", [True, False])
 def test_protein_tiptip_level_in_graph_capture(oracle, dtype, fma, with_sum):
     """A 16-taxon all-coded protein tree traversed inside a capture on a
-    stream without combination tables: its first level (8 tip/tip nodes) runs
-    the direct batched tip/tip kernels.  Replays equal a sequential oracle
-    evaluation in the same mode bit for bit (CLVs, scaler bytes, sums).  A
-    context of its own, whose pool entries have no tables yet."""
+    stream whose only earlier call was a tip/dense node: its first level (8
+    tip/tip nodes) goes through the combination tables of the stream's
+    workspace (allocated with it) and the second level stages its children
+    from them.  Replays equal a sequential oracle evaluation in the same mode
+    bit for bit (CLVs, scaler bytes, sums)."""
     import plfx
     import torch
 
@@ -632,7 +636,7 @@ def test_protein_tiptip_level_in_graph_capture(oracle, dtype, fma, with_sum):
     pmd, EVd, wd = dev(pm), dev(EV), dev(wgt)
     st = torch.cuda.Stream()
     ctx = plfx.Context(0)
-    # the stream's workspace, without tables: one tip/dense node first
+    # the stream's workspace: one tip/dense node first
     xd = torch.zeros(V * n, dtype=tt, device="cuda")
     ctx.plf_tips_dev(clv[ntips], EVd, n, pmd[:M], pmd[M:2 * M], tip1=tips[0], x2=xd, wgt=wd,
                      states=S, fma=fma, stream=st)
