@@ -1130,7 +1130,7 @@ plf_dna_f64_septet_kernel(const SeptetBatch sb, const double *__restrict__ EV,
 // node just in time; each node's weighted scaler sum collects in an LDS
 // counter (a wave reduction + atomic per node and 8-site block, only where a
 // site scaled) and is published by the per-region ticket at the end.  Results
-// are bit-identical to 63 separate updates.  (Measured, tools/gpu_deep.sh,
+// are bit-identical to 63 separate updates.  (Measured, tools/gpu_deep.sh@f9b3af3,
 // profiles/r01_deep.log: 256/512/768-thread blocks, U = 1/2, next-group
 // prefetch.)
 // kTips = 2: every leaf is a tip (one uint8 state code per site, see
@@ -1153,7 +1153,7 @@ __device__ constexpr int deep_off(int l) {
 // Wave-level chunk queue of the deep passes (kDyn).  Their waves run the
 // grid stride independently (no block barriers), and with a fixed stride the
 // launch ends when the slowest wave ends: a per-wave timeline of the 2^20-site
-// six-level pass (tools/tune_deep_dyn.hip) shows wave exits from 2.61 to
+// six-level pass (tools/tune_deep_dyn.hip@f9b3af3) shows wave exits from 2.61 to
 // 3.36 ms.  Chunk = one wave trip (8U f64 / 16U f32 sites); trip 0 takes
 // chunk `wave`, trip 1 W + wave (W = waves in the grid), trip i >= 2 2W + d,
 // d from a returning atomic add on the head word that lane 0 issues in trip

@@ -40,7 +40,7 @@ static_assert(kMaxSeptets == dev::kMaxSeptets, "septet batch size");
 static_assert(kDeepQueueRegion == dev::kDeepQueueRegion, "deep queue region");
 static_assert(sizeof(DeepDescH) == sizeof(dev::DeepDesc), "deep descriptor mismatch");
 
-// Tuned on MI355X (tools/tune_plf.hip, profiles/r01_tune.log):
+// Tuned on MI355X (tools/tune_plf.hip@f9b3af3, profiles/r01_tune.log):
 // f64 lane-pair kernel, 2 x 16-site steps per trip, non-temporal CLV loads
 // and stores, grid = resident blocks.
 constexpr int kU64 = 2, kU32 = 4;
@@ -49,12 +49,12 @@ constexpr bool kNt = true;   // f32: NT CLV loads (74.8% vs 70.2% of HBM peak, r
 constexpr bool kNtl64 = true;
 constexpr int kMinWaves = 1;
 constexpr int kBlocksPerCu32 = 2;  // f32 node kernel grid (launch_cat)
-constexpr int kTripleU = 1;  // fused level pairs: 16 sites per trip (tools/tune_triple.hip)
+constexpr int kTripleU = 1;  // fused level pairs: 16 sites per trip (tools/tune_triple.hip@f9b3af3)
 constexpr int kTripleUTips = 2;  // with coded tips: 32 sites per trip (+13-19 % for 2 tip
                                  // children, equal for 1; profiles/r01_ab_fused_tips.log)
 constexpr int kTripleU32 = 2;
 // fused three-level subtrees: 2 x 8-site blocks per trip, matrices re-read from
-// LDS, next trip's loads in flight (tools/tune_septet.hip, r01_tune_septet.log)
+// LDS, next trip's loads in flight (tools/tune_septet.hip@f9b3af3, r01_tune_septet.log)
 constexpr int kSeptetU = 2;
 constexpr int kSeptetU32 = 2;  // f32 (lane = category): 2 x 16-site blocks per trip
 constexpr int kDeepU32 = 2;    // f32 six-level pass: 2 x 16-site blocks per trip
@@ -106,7 +106,7 @@ hipError_t launch_cat(const DnaArgs &a, int max_blocks, hipStream_t s) {
   // 2 blocks per CU rather than the 3 co-resident ones: at 2^20 sites U = 4
   // leaves 5.33 trips per wave at 3/CU (a sixth trip for a third of the waves)
   // and exactly 8 at 2/CU -- 35.4 vs 35.8 us, and 68.4 vs 69.2 us at 2^21
-  // (tools/ab_defer.hip, tools/tune_f32.hip; profiles/r02_tune_f32.log)
+  // (tools/ab_defer.hip@f9b3af3, tools/tune_f32.hip@f9b3af3; profiles/r02_tune_f32.log)
   const int64_t gx = grid_x((const void *)kernel, cache, kGridMul32, a.n, kWavesPerBlock * 16 * kU32,
                             1, max_blocks > 0 ? max_blocks : kBlocksPerCu32 * cu_count());
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
@@ -161,7 +161,7 @@ hipError_t launch_lnl_t(const T *x, int64_t n, const double *catw, const double 
   static int cache = 0;
   auto kernel = &dev::root_lnl_kernel<T, S, C>;
   // C steps of 64/C sites per wave trip; 2 blocks per CU (more trips per wave: the
-  // kernel is short and its ramp and final reduction weigh; tools/ab_lnl.hip)
+  // kernel is short and its ramp and final reduction weigh; tools/ab_lnl.hip@f9b3af3)
   int64_t gx = grid_x((const void *)kernel, cache, 1, n, kWavesPerBlock * 64, 1, 0);
   static int cus = 0;
   if (!cus) {
@@ -198,7 +198,7 @@ hipError_t launch_prot_t(const DnaArgs &a, int max_blocks, hipStream_t s, const 
   // rows 16..19 of the products and the back-transform on 4x4x1_16b, kQ = 2:
   // 52.4 -> 46.5 us at 2^18, profiles/r02_tune_protein_f32_q.log), exact mode
   // on the LDS-matrix kernel (4-row groups, tile prefetch)
-  // (tools/tune_prot32.hip, profiles/r02_tune_protein_f32.log)
+  // (tools/tune_prot32.hip@f9b3af3, profiles/r02_tune_protein_f32.log)
   if constexpr (kFma) {
     static int cache = 0;
     auto kernel = &dev::plf_prot_mfma32_kernel<kSum, 3, kTips>;
@@ -222,12 +222,12 @@ hipError_t launch_prot_mfma_t(const DnaArgs &a, int max_blocks, hipStream_t s,
                               const double *tipvec) {
   static int cache = 0;
   // X3 to LDS through permuted back-transform rows (kX3 = 2: conflict-free
-  // b128 writes; 90.2 vs 91.2 us at 2^18, 342 vs 345 at 2^20, tools/tune_prot.hip,
+  // b128 writes; 90.2 vs 91.2 us at 2^18, 342 vs 345 at 2^20, tools/tune_prot.hip@f9b3af3,
   // profiles/r02_tune_protein_v3.log); first tile's loads before the matrix fragments.
   // From 32 tiles per block (2^20 sites at 512 blocks) on, tiles come from the
   // device-wide queue (kDyn, plf_prot.hpp ProtQueue): 2^20 -3..-5 %, 2^22 -10 %
   // dense, tip/inner -8 / -14 %; below that, and for tip/tip nodes at any size,
-  // the fixed stride is as fast or faster (tools/tune_prot64d.hip,
+  // the fixed stride is as fast or faster (tools/tune_prot64d.hip@f9b3af3,
   // profiles/r03_tune_protein_dyn.log)
   auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, kTips, false>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
@@ -247,7 +247,7 @@ template <bool kSum, int kTips>
 hipError_t launch_prot_exact64_t(const DnaArgs &a, int max_blocks, hipStream_t s,
                                  const double *tipvec) {
   static int cache = 0;
-  // 10-row groups + tile prefetch (tools/tune_prot.hip, profiles/r02_tune_protein_exact_rows.log)
+  // 10-row groups + tile prefetch (tools/tune_prot.hip@f9b3af3, profiles/r02_tune_protein_exact_rows.log)
   auto kernel = &dev::plf_prot_lds_kernel<double, kSum, 2, kTips, 10, true>;
   const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
@@ -337,7 +337,7 @@ hipError_t launch_septets32_t(const dev::SeptetBatch &b, int count, const float 
 
 // fused six-level subtrees: 512-thread blocks (one LDS copy of the 63 nodes'
 // matrices per 8 waves), 2 x 8-site blocks per trip, grid = co-resident blocks
-// (tools/gpu_deep.sh, profiles/r01_deep.log)
+// (tools/gpu_deep.sh@f9b3af3, profiles/r01_deep.log)
 template <int D, typename T, bool kSum, int U, int kThreads, int kTips, bool kDyn>
 hipError_t launch_deep_k(const dev::DeepDesc &d, const T *EV, const int32_t *wgt, int64_t n,
                          unsigned long long *ws, int max_blocks, hipStream_t s, const T *tipvec) {

@@ -22,7 +22,7 @@
 // (*_batch_kernel: node = blockIdx.y, plf_dna.hpp NodeBatch).
 // The measured-and-not-adopted forms and knobs (the round-1 readlane kernel,
 // ablations, swizzles, rings, SGPR operands, ...) live in the tuning copy
-// tools/plf_prot_tune.hpp; DESIGN.md section 3.3 has the measurements.
+// tools/plf_prot_tune.hpp@f9b3af3; DESIGN.md section 3.3 has the measurements.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -361,7 +361,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
     // inside the scaled-site branch, its wait also drained the next child tile
     // in flight (2^18: f64 142.2 -> 138.9 us, f32 76.5 -> 74.6 us; the FMA
     // kernels ran 1-2 % slower this way and keep the branch load,
-    // tools/tune_prot_wgt.hip, profiles/r03_tune_protein_wgt.log)
+    // tools/tune_prot_wgt.hip@f9b3af3, profiles/r03_tune_protein_wgt.log)
     const int wsite = kSum ? wgt_at(wgt, sq, ws) : 0;
     // stage a dense child's tile from the prefetch registers, then fetch the
     // next tile in the sequence
@@ -528,7 +528,7 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // Device-wide tile queue for the protein kernels (kDyn).  Why: with two or
 // three co-resident blocks per CU the oldest block's waves win the SIMD's issue
 // arbitration -- at 2^18 sites the first block on each CU finished its 8 fixed
-// trips at ~75 us, the second at ~83 us (tools/probes/prot_timeline.hip) -- so
+// trips at ~75 us, the second at ~83 us (tools/probes/prot_timeline.hip@f9b3af3) -- so
 // a fixed grid stride leaves CUs half idle at the end, more so the more trips a
 // block makes.  Tiles: trip 0 takes blockIdx.x, trip 1 G + blockIdx.x, trip
 // i >= 2 2G + d, d from a returning atomic add on a head word that thread 0

@@ -518,7 +518,7 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
     // previous node's last trips leave idle).  64-taxon tree at 2^18 sites per
     // sweep vs one launch per node: f64 FMA 5.67 -> 5.38 ms, f64 exact 8.45 ->
     // 8.02 ms, f32 FMA 2.94 -> 2.66 ms; splitting the resident grid over the
-    // nodes (the DNA batches' rule) gains only 1-3 % (tools/prot_batch_ab.py,
+    // nodes (the DNA batches' rule) gains only 1-3 % (tools/prot_batch_ab.py@f9b3af3,
     // profiles/r03_protein_batch_ab.log).
     const plfx::NodeDescH *all = reinterpret_cast<const plfx::NodeDescH *>(nodes);
     for (int j = 0; j < count; j += plfx::kMaxBatch) {
