@@ -57,6 +57,7 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
+#include <unistd.h>
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
@@ -249,6 +250,41 @@ int run(const Opts &o) {
                 (unsigned long long)tb.instance_elements_right(), (unsigned long long)(tb.instance_elements_right() * es));
     std::printf("| instance out:           | %16llu | %16llu | %16llu |\n", (unsigned long long)n0,
                 (unsigned long long)tb.instance_elements_out(), (unsigned long long)(tb.instance_elements_out() * es));
+    // host_mem.cpp:70-82: the instances' buffers together, and all plf calls
+    const unsigned long long P_ = o.instances, S_ = o.sites;
+    std::printf("----------------------------------------------------------------------------------\n");
+    std::printf("| buffer left:            | %16llu | %16llu | %16llu |\n", S_,
+                (unsigned long long)tb.instance_elements_left() * P_, (unsigned long long)(tb.instance_elements_left() * P_ * es));
+    std::printf("| buffer right:           | %16llu | %16llu | %16llu |\n", S_,
+                (unsigned long long)tb.instance_elements_right() * P_, (unsigned long long)(tb.instance_elements_right() * P_ * es));
+    std::printf("| buffer out:             | %16llu | %16llu | %16llu |\n", S_,
+                (unsigned long long)tb.instance_elements_out() * P_, (unsigned long long)(tb.instance_elements_out() * P_ * es));
+    std::printf("----------------------------------------------------------------------------------\n");
+    const unsigned long long data_el = (unsigned long long)tb.elements_per_instance() * P_ * o.calls;
+    std::printf("| total (%3u plf calls):  | %16llu | %16llu | %16llu |\n", o.calls, S_ * o.calls, data_el,
+                data_el * es);
+    std::printf("==================================================================================\n");
+    // host_mem.cpp:84-88: memory this run holds on the host and on the device
+    // (capacities from the machine and the GPU instead of the VCK5000's 256 / 12 GB)
+    const double host_b = (double)es * (2.0 * o.sites * 16 + (double)o.calls * o.sites * 16 +
+                                        (o.check ? o.sites * 16.0 : 0.0)) +
+                          (double)o.calls * o.sites + 4.0 * o.sites +
+                          (o.sw_emu ? 0.0 : (double)P_ * (tb.instance_elements_left() + tb.instance_elements_right()) * es);
+    const double host_cap = (double)sysconf(_SC_PHYS_PAGES) * (double)sysconf(_SC_PAGE_SIZE);
+    std::printf("| RAM usage (host):       | %14.6f GB of %7.1f GB (%12.6f %%)      |\n", host_b / 1e9, host_cap / 1e9,
+                host_cap > 0 ? 100.0 * host_b / host_cap : 0.0);
+    const double dev_b = (double)P_ * ((tb.instance_elements_left() + tb.instance_elements_right() +
+                                        tb.instance_elements_out()) * es + n0);
+    if (o.sw_emu) {
+      std::printf("| RAM usage (GPU):        | %54s |\n", "none (sw_emu: the instances run on the host)");
+    } else {
+      size_t free_b = 0, total_b = 0;
+      HIPCHK(hipSetDevice(o.devices[0]));
+      HIPCHK(hipMemGetInfo(&free_b, &total_b));
+      const double per_gpu = dev_b / (double)std::min<size_t>(o.devices.size(), P_);
+      std::printf("| RAM usage (GPU):        | %14.6f GB of %7.1f GB (%12.6f %%)      |\n", per_gpu / 1e9,
+                  (double)total_b / 1e9, total_b ? 100.0 * per_gpu / (double)total_b : 0.0);
+    }
     std::printf("==================================================================================\n");
   }
 

@@ -45,3 +45,27 @@ def ctx():
     c = plfx.Context(0)
     yield c
     c.close()
+
+
+def check_report_rows(out, n, calls, P, dtype, args):
+    """plfx_host's sizing rows equal testbench_info's arithmetic
+    (include.h:150-266 via plfx.Testbench): per instance, for all instances
+    (buffer rows) and for all calls (total row), in elements and bytes."""
+    import plfx
+
+    window = int(args[args.index("--window") + 1]) if "--window" in args else 8192
+    layout = plfx.LAYOUT_COMBINED if "comb" in args else plfx.LAYOUT_SEPARATE
+    aie = plfx.AIE_STREAM if "stream" in args else plfx.AIE_WINDOW
+    tb = plfx.Testbench(n, P, window, layout, aie)
+    es = np.dtype(dtype).itemsize
+    rows = {ln.split("|")[1].strip(): [int(v) for v in ln.split("|")[2:5]]
+            for ln in out.splitlines()
+            if ln.startswith("| instance ") or ln.startswith("| buffer ") or ln.startswith("| total (")}
+    n0 = tb.alignments_per_instance()
+    for side, el in (("left", tb.instance_elements_left()), ("right", tb.instance_elements_right()),
+                     ("out", tb.instance_elements_out())):
+        assert rows[f"instance {side}:"] == [n0, el, el * es]
+        assert rows[f"buffer {side}:"] == [n, el * P, el * P * es]
+    tot = tb.elements_per_instance() * P * calls
+    assert rows[f"total ({calls:3d} plf calls):"] == [n * calls, tot, tot * es]
+    assert "RAM usage (host):" in out

@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, PKG, golden
+from conftest import GOLDEN, PKG, golden, check_report_rows
 
 pytestmark = pytest.mark.gpu
 
@@ -392,6 +392,9 @@ def test_host_driver_end_to_end(oracle, tmp_path):
         for ln in lines[1:]:
             vals = [float(v) for v in ln.split(",")]
             assert len(vals) == len(lines[0].split(",")) and all(v >= 0 for v in vals)
+        # the report's sizing rows (host_mem.cpp:56-88): instances, buffers, all calls, memory
+        check_report_rows(r.stdout, n, calls, P, dtype, args)
+        assert "RAM usage (GPU):" in r.stdout and " GB of " in r.stdout.split("RAM usage (GPU):")[1]
         # the driver's own check (host_mem.cpp:403-442): CPU plf() vs the GPU, exact
         assert "Test result: Passed" in r.stdout
         assert "Reference (CPU plf" in r.stdout and "Speed up (excluding transfers)" in r.stdout
