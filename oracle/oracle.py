@@ -14,7 +14,9 @@ Contents
   (host_mem.cpp:384-388).
 * ctypes bindings to the reference's own ``plf()`` built into ``oracle/_ref``
   from /root/reference/app/src/plf.cpp (oracle/Makefile), used to pin the
-  restatement.
+  restatement, and ``ref_traverse``: a tree sweep as the composition of the
+  reference's own plf() calls, one per inner node in post-order, which pins
+  the traversal/fused-pass results of BASELINE configs[2]/[3].
 * ``testbench_*``: the instance sizing/partition arithmetic of
   ``testbench_info`` (/root/reference/app/src/include.h:150-266).
 * ``pack_instance``: the per-instance input buffers of host_mem.cpp:221-243.
@@ -28,9 +30,11 @@ Contents
   (aie/data/golden{0..3}.txt and their stimuli).
 
 Parity status: the float path is pinned (reference binary + AIE goldens +
-committed fixtures).  Double, protein (S=20), tree sweep and lnL are
-extensions the reference does not have: parity unpinned beyond being the same
-loop as the pinned float path.
+committed fixtures); double by the reference source's double instantiation;
+4-state tree sweeps (dense and state-coded tips) by the composition of the
+reference's plf() calls (tests/golden/tree64.npz, ref_traverse).  Protein
+(S=20) and the root lnL are extensions the reference does not have: parity
+unpinned beyond being the same loop as the pinned path.
 """
 from __future__ import annotations
 
@@ -317,6 +321,48 @@ def balanced_tree_ops(ntips):
     return np.array(ops, np.int32)
 
 
+TREE_GOLDEN_N = 257       # ragged: not a multiple of any kernel's trip
+TREE_GOLDEN_SEED = 6464
+
+
+def tree_golden_case(dtype, coded, n=TREE_GOLDEN_N, seed=TREE_GOLDEN_SEED):
+    """Inputs of the committed tree-sweep fixtures (tests/golden/tree64.npz):
+    BASELINE configs[2]'s 64-taxon balanced tree at a small ragged site count,
+    P and EV scaled by 0.25 so the deep levels underflow and the
+    scaler path runs.  coded: every tip is DNA state codes (20 % ambiguous),
+    expanded to the dense CLV plf() reads.  Returns dict(ops, tips (dense
+    CLVs), codes (None or per tip), pm, EV, wgt, n)."""
+    dt = np.dtype(dtype)
+    rng = np.random.default_rng(seed + (1 if coded else 0))
+    ops = balanced_tree_ops(64)
+    codes = [random_tip_codes(rng, n, 0.2) for _ in range(64)] if coded else None
+    tips = ([expand_tips(c, dt) for c in codes] if coded
+            else [rng.random(16 * n).astype(dt) for _ in range(64)])
+    pm = (rng.random(ops.shape[0] * 128) * 0.25).astype(dt)
+    EV = (rng.random(16) * 0.25).astype(dt)
+    wgt = rng.integers(1, 5, n).astype(np.int32)
+    return dict(ops=ops, tips=tips, codes=codes, pm=pm, EV=EV, wgt=wgt, n=n)
+
+
+def tree_case_digest(case):
+    """sha256 over a tree case's input bytes (tips, P, EV, weights): a fixture
+    is only compared when the inputs regenerate to the same bytes."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for t in case["tips"]:
+        h.update(np.ascontiguousarray(t).tobytes())
+    for k in ("pm", "EV", "wgt"):
+        h.update(np.ascontiguousarray(case[k]).tobytes())
+    return h.hexdigest()
+
+
+def clv_digest(a):
+    import hashlib
+
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
 def expand_tips(codes, dtype=np.float64, Ccat=4, tipvec=None):
     """Dense CLV of a tip stored as DNA state codes (bit s = state s possible,
     upper nibble ignored; the RAxML/PLL encoding): x[i][c][s] = (code_i >> s) & 1
@@ -383,6 +429,80 @@ def ref_plf(x1, x2, EV, left, right, wgt, opt="O0"):
     inc = L.plfref_plf(x1.copy(), x2.copy(), x3, EV.copy(), n, left.copy(), right.copy(),
                        np.ascontiguousarray(wgt, dtype=np.int32).copy())
     return x3, inc
+
+
+def _ref_call(dtype, opt="O0"):
+    """The reference plf() entry of one dtype over raw contiguous arrays:
+    f(x1, x2, x3, EV, n, left, right, wgt) -> scalerIncrement, or None."""
+    if np.dtype(dtype) == np.float32:
+        L = ref_lib(opt)
+        return None if L is None else L.plfref_plf
+    L = ref_lib_f64(opt)
+    return None if L is None else L.plfref_plf_f64
+
+
+def ref_available(dtype=np.float32, opt="O0") -> bool:
+    return _ref_call(dtype, opt) is not None
+
+
+def ref_scaled_sites(f, x1, x2, EV, left, right, n):
+    """Per-site scaler bytes of one reference plf() call (the reference returns
+    only the weighted sum): each half of a site range is called with unit
+    weights and split further only while its count is neither 0 nor its length,
+    so sparse and dense scaling cost O(scaled · log n) calls, not n."""
+    sc = np.zeros(n, np.uint8)
+    V = x1.size // n
+    ones = np.ones(n, np.int32)
+    x3 = np.empty_like(x1)
+
+    def count(lo, hi):
+        return f(x1[V * lo:V * hi], x2[V * lo:V * hi], x3[V * lo:V * hi], EV, hi - lo, left, right,
+                 ones[lo:hi])
+
+    stack = [(0, n, count(0, n))] if n else []
+    while stack:
+        lo, hi, c = stack.pop()
+        if c == 0:
+            continue
+        if c == hi - lo:
+            sc[lo:hi] = 1
+            continue
+        mid = (lo + hi) // 2
+        cl = count(lo, mid)
+        stack.append((lo, mid, cl))
+        stack.append((mid, hi, c - cl))
+    return sc
+
+
+def ref_traverse(ops, clv, pmats, EV, n, wgt=None, want_scalers=False, opt="O0"):
+    """A traversal as the reference would run it: the UNMODIFIED reference
+    plf() (/root/reference/app/src/plf.cpp:8-68, oracle/_ref; the f64 build is
+    the same source with float spelled double) called once per op in op order
+    -- parent = plf(child1, child2, P_left, P_right) -- exactly how a tree
+    likelihood code calls it per inner node.  ops = int32
+    (nops, 4) [parent, child1, child2, pmat]; clv = list of numpy CLVs (4-state,
+    written in place); pmats = flat 2·npmat 4×4×4 matrices; wgt None = 1.
+    Returns (scaler_sums int64[nops], scaler bytes per op or None).
+    Raises FileNotFoundError when oracle/_ref holds no build for the dtype."""
+    dt = clv[0].dtype
+    f = _ref_call(dt, opt)
+    if f is None:
+        raise FileNotFoundError("oracle/_ref was not built (no /root/reference here)")
+    ops = np.ascontiguousarray(ops, dtype=np.int32).reshape(-1, 4)
+    pm = np.ascontiguousarray(pmats, dt)
+    ev = np.ascontiguousarray(EV, dt)
+    w = np.ones(n, np.int32) if wgt is None else np.ascontiguousarray(wgt, np.int32)
+    sums = np.zeros(ops.shape[0], np.int64)
+    scal = [] if want_scalers else None
+    for j, (p, c1, c2, m) in enumerate(ops):
+        left, right = pm[128 * m:128 * m + 64], pm[128 * m + 64:128 * m + 128]
+        x1, x2 = clv[c1].copy(), clv[c2].copy()  # a parent may reuse a child's slot
+        out = np.empty(16 * n, dt)
+        sums[j] = f(x1, x2, out, ev, n, left, right, w) if n else 0
+        clv[p][:] = out
+        if want_scalers:
+            scal.append(ref_scaled_sites(f, x1, x2, ev, left, right, n))
+    return sums, scal
 
 
 def scaler_sum(scaler, wgt=None):

@@ -137,6 +137,33 @@ def make_edge():
                         wgt=wgt, x3=x3, scaler=sc, scalerIncrement=np.int64(incw))
 
 
+def make_tree64():
+    """BASELINE configs[2]'s 64-taxon post-order sweep, as the composition of
+    the reference's own plf() (oracle.ref_traverse: the unmodified plf.cpp,
+    float build and double instantiation, one call per inner node), dense and
+    state-coded tips: per op the sha256 of the parent CLV's bytes, the
+    per-site scaler bytes and the weighted scaler sum, plus the root CLV."""
+    d = {}
+    for dt in (np.float32, np.float64):
+        for coded in (False, True):
+            k = f"{'f32' if dt == np.float32 else 'f64'}_{'coded' if coded else 'dense'}"
+            c = O.tree_golden_case(dt, coded)
+            nops = c["ops"].shape[0]
+            clv = [t.copy() for t in c["tips"]] + [np.zeros(16 * c["n"], dt) for _ in range(nops)]
+            sums, scal = O.ref_traverse(c["ops"], clv, c["pm"], c["EV"], c["n"], c["wgt"], want_scalers=True)
+            assert sums.sum() > 0
+            d[f"{k}_inputs_sha256"] = np.array(O.tree_case_digest(c))
+            d[f"{k}_x3_sha256"] = np.array([O.clv_digest(clv[int(p)]) for p in c["ops"][:, 0]])
+            d[f"{k}_scaler"] = np.stack(scal)
+            d[f"{k}_sums"] = sums
+            d[f"{k}_root"] = clv[int(c["ops"][-1, 0])]
+    d["n"] = np.int64(O.TREE_GOLDEN_N)
+    d["seed"] = np.int64(O.TREE_GOLDEN_SEED)
+    d["source"] = np.array("reference plf() per inner node (oracle/_ref/libplfref_O0.so, "
+                           "libplfref_f64_O0.so), oracle.ref_traverse")
+    np.savez_compressed(OUT / "tree64.npz", **d)
+
+
 def main():
     if O.ref_lib("O0") is None:
         sys.exit("oracle/_ref/libplfref_O0.so missing: run `make -C oracle` where /root/reference exists")
@@ -147,6 +174,7 @@ def main():
     make_hostmem(4096, False)
     make_hash(65536)
     make_edge()
+    make_tree64()
     for f in sorted(OUT.iterdir()):
         print(f"{f.name:32s} {f.stat().st_size:9d} B")
 

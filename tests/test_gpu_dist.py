@@ -130,7 +130,8 @@ def test_nodes512_full_size_windows(oracle):
     512 nodes x 2^20 f64 sites of bench.NodesWorkload (201 GB of CLVs) in its
     16 interleaved 32-node launches.  A 1024-site window of every node is
     checked bit for bit against the oracle on that window (x3 and scaler
-    bytes), and every node's scaler sum is its N/4 rescaled sites."""
+    bytes; every 64th node also against the reference's own plf() in
+    double), and every node's scaler sum is its N/4 rescaled sites."""
     import torch
 
     import bench
@@ -155,6 +156,12 @@ def test_nodes512_full_size_windows(oracle):
                                     nd["right"].cpu().numpy(), ones)
             assert np.array_equal(h["x3"].view(np.uint64), e3.view(np.uint64)), j
             assert np.array_equal(nd["scaler"][lo:lo + 1024].cpu().numpy(), esc), j
+            if j % 64 == 0 and oracle.ref_available(np.float64):
+                # and through the reference's own plf() (its double build)
+                r3, rinc = oracle.ref_plf_f64(h["x1"], h["x2"], EV, nd["left"].cpu().numpy(),
+                                              nd["right"].cpu().numpy(), ones)
+                assert np.array_equal(h["x3"].view(np.uint64), r3.view(np.uint64)), j
+                assert rinc == int(esc.sum()), j
         assert wl.sums.cpu().tolist() == [n // 4] * 512
         del wl
     torch.cuda.empty_cache()

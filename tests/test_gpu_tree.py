@@ -1,9 +1,14 @@
 """GPU tests of the multi-node extensions (BASELINE configs 3 and 4): batched
 independent nodes, traversal descriptors with level scheduling, and the root
-log-likelihood.  The reference has none of these: parity is
-against the oracle's sequential restatement built on the pinned plf() loop --
-"parity unpinned" beyond that.  Bar: CLVs and scaler sums bit-exact; lnL within
-1e-12 relative (device log() and a different, fixed summation order)."""
+log-likelihood.  The reference has no traversal driver; on its
+side a sweep is its plf() called once per inner node, and that composition of
+the unmodified reference build pins the 4-state sweeps here
+(`test_tree64_reference_golden` against tests/golden/tree64.npz, the full-size
+window against oracle.ref_traverse).  The other tests check against the
+oracle's sequential restatement (itself pinned by the same fixture,
+tests/test_tree_golden.py).  The root lnL stays "parity unpinned".  Bar: CLVs
+and scaler sums bit-exact; lnL within 1e-12 relative (device log() and a
+different, fixed summation order)."""
 import numpy as np
 import pytest
 
@@ -170,14 +175,65 @@ def test_tree64_full_size_window(ctx, oracle):
     lo, m = 500_003, 4096
     win = [t[16 * lo:16 * (lo + m)].cpu().numpy().copy() for t in clv[:ntips]]
     win += [np.zeros(16 * m) for _ in range(nslots - ntips)]
+    rwin = [w.copy() for w in win]
     esums, escal = oracle.traverse(4, 4, ops, win, pm.cpu().numpy(), EV.cpu().numpy(), m, want_scalers=True)
     for s in range(ntips, nslots):
         assert np.array_equal(bits(clv[s][16 * lo:16 * (lo + m)].cpu().numpy()), bits(win[s])), s
     for j in range(ops.shape[0]):
         assert np.array_equal(scal[j][lo:lo + m].cpu().numpy(), escal[j])
+    if oracle.ref_available(np.float64):
+        # the same window through the reference's own plf(), one call per node
+        rsums, rscal = oracle.ref_traverse(ops, rwin, pm.cpu().numpy(), EV.cpu().numpy(), m, want_scalers=True)
+        for s in range(ntips, nslots):
+            assert np.array_equal(bits(rwin[s]), bits(win[s])), s
+        assert np.array_equal(rsums, esums)
+        for j in range(ops.shape[0]):
+            assert np.array_equal(rscal[j], escal[j])
     root = clv[-1].cpu().numpy()
     exp = oracle.root_lnl(4, 4, root, n, scaler_sums=gsums)
     assert abs(float(out.item()) - exp) <= LNL_RTOL * abs(exp)
+
+
+@pytest.mark.parametrize("fuse", ["3", "2", "1", "0"])
+@pytest.mark.parametrize("dtype,coded", [(np.float64, False), (np.float32, False), (np.float64, True),
+                                         (np.float32, True)])
+def test_tree64_reference_golden(oracle, dtype, coded, fuse, monkeypatch):
+    """configs[2] pinned by the reference itself: the 64-taxon sweep under
+    every schedule (PLFX_FUSE 3: one six-level pass; 2: three-level passes +
+    level pairs; 1: level pairs; 0: batched levels) reproduces
+    tests/golden/tree64.npz -- the unmodified reference plf() called per inner
+    node (oracle.ref_traverse) -- byte for byte: every parent CLV (sha256), the
+    per-site scaler bytes and the weighted sums, dense and state-coded tips."""
+    import plfx
+    import torch
+
+    g = np.load(__import__("conftest").GOLDEN / "tree64.npz", allow_pickle=False)
+    k = f"{'f32' if dtype == np.float32 else 'f64'}_{'coded' if coded else 'dense'}"
+    c = oracle.tree_golden_case(dtype, coded, int(g["n"]), int(g["seed"]))
+    assert oracle.tree_case_digest(c) == str(g[f"{k}_inputs_sha256"])
+    n, ops = c["n"], c["ops"]
+    nops = ops.shape[0]
+    monkeypatch.setenv("PLFX_FUSE", fuse)
+    ctx = plfx.Context(0)
+    try:
+        tt = torch.float64 if dtype == np.float64 else torch.float32
+        clv = [None if coded else dev(t) for t in c["tips"]]
+        clv += [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nops)]
+        tips = ([dev(cd) for cd in c["codes"]] if coded else [None] * 64) + [None] * nops
+        sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
+        scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+        ctx.traverse(ops, clv, dev(c["pm"]), dev(c["EV"]), n, dev(c["wgt"]), scal, sums, tips=tips)
+        torch.cuda.synchronize()
+        sched = ctx.last_schedule()
+    finally:
+        ctx.close()
+    if fuse == "3":
+        assert sched["deep6"] == 1, sched
+    got = [oracle.clv_digest(clv[int(p)].cpu().numpy()) for p in ops[:, 0]]
+    bad = [j for j, (a, b) in enumerate(zip(got, g[f"{k}_x3_sha256"])) if a != str(b)]
+    assert not bad, f"parent CLVs of ops {bad[:8]} differ from the reference composition ({sched})"
+    assert np.array_equal(sums.cpu().numpy(), g[f"{k}_sums"])
+    assert np.array_equal(np.stack([s.cpu().numpy() for s in scal]), g[f"{k}_scaler"])
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])

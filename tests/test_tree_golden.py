@@ -1,0 +1,88 @@
+"""CPU tests: the tree-sweep oracle pinned by the reference itself.
+
+BASELINE configs[2] (a 64-taxon post-order sweep) is, on the reference's side,
+nothing but its plf() (/root/reference/app/src/plf.cpp:8-68) called once per
+inner node with that node's children and P matrices.  tests/golden/tree64.npz
+holds that composition as produced by the unmodified reference build
+(oracle.ref_traverse over oracle/_ref; generator tests/golden/make_golden.py
+make_tree64): per op the sha256 of the parent CLV, the per-site scaler bytes,
+the weighted scaler sum, and the root CLV -- f32 and f64 (the reference source
+with float spelled double), dense and state-coded tips.
+
+Here the oracle's own sequential traversal (plf_oracle.c plfo_traverse, the
+checker of every GPU traversal test) must reproduce those bytes, and the live
+reference composition must too when oracle/_ref is present.  The GPU side of
+the same fixture is tests/test_gpu_tree.py::test_tree64_reference_golden.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+CASES = [(np.float32, False), (np.float32, True), (np.float64, False), (np.float64, True)]
+
+
+def key(dt, coded):
+    return f"{'f32' if dt == np.float32 else 'f64'}_{'coded' if coded else 'dense'}"
+
+
+def check_against_golden(oracle, g, k, case, clv, sums, scal):
+    ops = case["ops"]
+    digests = [oracle.clv_digest(clv[int(p)]) for p in ops[:, 0]]
+    bad = [j for j, (a, b) in enumerate(zip(digests, g[f"{k}_x3_sha256"])) if a != str(b)]
+    assert not bad, f"{k}: parent CLVs of ops {bad[:8]} differ from the reference composition"
+    assert np.array_equal(np.asarray(sums, np.int64), g[f"{k}_sums"])
+    assert np.array_equal(np.stack(scal), g[f"{k}_scaler"])
+    root = clv[int(ops[-1, 0])]
+    assert np.array_equal(root.view(np.uint8), g[f"{k}_root"].view(np.uint8))
+
+
+@pytest.mark.parametrize("dt,coded", CASES)
+def test_fixture_inputs_regenerate(oracle, dt, coded):
+    g = golden("tree64.npz")
+    c = oracle.tree_golden_case(dt, coded, int(g["n"]), int(g["seed"]))
+    assert oracle.tree_case_digest(c) == str(g[f"{key(dt, coded)}_inputs_sha256"])
+    assert g[f"{key(dt, coded)}_sums"].sum() > 0  # the scaler path is in the fixture
+
+
+@pytest.mark.parametrize("dt,coded", CASES)
+def test_oracle_traverse_matches_reference_composition(oracle, dt, coded):
+    g = golden("tree64.npz")
+    c = oracle.tree_golden_case(dt, coded, int(g["n"]), int(g["seed"]))
+    n, ops = c["n"], c["ops"]
+    clv = [t.copy() for t in c["tips"]] + [np.zeros(16 * n, dt) for _ in range(ops.shape[0])]
+    sums, scal = oracle.traverse(4, 4, ops, clv, c["pm"], c["EV"], n, c["wgt"], want_scalers=True)
+    check_against_golden(oracle, g, key(dt, coded), c, clv, sums, scal)
+
+
+@pytest.mark.parametrize("dt,coded", CASES)
+def test_live_reference_reproduces_fixture(oracle, dt, coded):
+    if not oracle.ref_available(dt):
+        pytest.skip("oracle/_ref not built (no /root/reference on this machine)")
+    g = golden("tree64.npz")
+    c = oracle.tree_golden_case(dt, coded, int(g["n"]), int(g["seed"]))
+    n, ops = c["n"], c["ops"]
+    clv = [t.copy() for t in c["tips"]] + [np.zeros(16 * n, dt) for _ in range(ops.shape[0])]
+    sums, scal = oracle.ref_traverse(ops, clv, c["pm"], c["EV"], n, c["wgt"], want_scalers=True)
+    check_against_golden(oracle, g, key(dt, coded), c, clv, sums, scal)
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_ref_scaled_sites_bisection(oracle, dt):
+    """ref_scaled_sites recovers per-site scaler bytes from the reference's
+    weighted sum alone: equal to the restatement's bytes on sparse, dense and
+    alternating scaling."""
+    if not oracle.ref_available(dt):
+        pytest.skip("oracle/_ref not built")
+    rng = np.random.default_rng(2)
+    n = 999
+    EV = rng.random(16).astype(dt)
+    L = rng.random(64).astype(dt)
+    R = rng.random(64).astype(dt)
+    f = oracle._ref_call(dt)
+    for pattern in (np.zeros(n, bool), np.ones(n, bool), np.arange(n) % 2 == 0, rng.random(n) < 0.01):
+        x1 = rng.random(16 * n).astype(dt)
+        x1.reshape(n, 16)[pattern] *= dt(1e-30) if dt == np.float64 else dt(1e-20)
+        x2 = rng.random(16 * n).astype(dt)
+        _, sc, _ = oracle.plf(x1, x2, EV, L, R, np.ones(n, np.int32))
+        assert np.array_equal(oracle.ref_scaled_sites(f, x1, x2, EV, L, R, n), sc)
