@@ -373,8 +373,8 @@ class Context:
                     raise PlfxError(ERR_INVALID, f"node {i}: {k} must be a contiguous {dt} device "
                                                  f"tensor >= {V}*n")
             for k in ("left", "right"):
-                if nd[k].dtype != dt or nd[k].numel() < M or not nd[k].is_cuda:
-                    raise PlfxError(ERR_INVALID, f"node {i}: {k} needs {M} device values")
+                if nd[k].dtype != dt or nd[k].numel() < M or not nd[k].is_cuda or not nd[k].is_contiguous():
+                    raise PlfxError(ERR_INVALID, f"node {i}: {k} needs {M} contiguous device values")
             try:
                 _check_aux(n, None, nd.get("scaler"), nd.get("scaler_sum"))
             except PlfxError as e:
@@ -382,8 +382,8 @@ class Context:
             arr[i] = Node(ptr(nd["x1"]), ptr(nd["x2"]), ptr(nd["x3"]), ptr(nd["left"]),
                           ptr(nd["right"]), ptr(nd.get("scaler")), ptr(nd.get("scaler_sum")))
         _check_aux(n, wgt, None, None)
-        if not EV.is_cuda:
-            raise PlfxError(ERR_INVALID, "EV must be a device tensor")
+        if not EV.is_cuda or not EV.is_contiguous() or EV.numel() < states * states:
+            raise PlfxError(ERR_INVALID, f"EV must be a contiguous device tensor of {states * states} values")
         self._check(self._L.plfx_plf_batch_dev(self.h, F32 if dt == torch.float32 else F64, states, arr,
                                                len(nodes), C.c_void_p(EV.data_ptr()), int(n),
                                                C.c_void_p(ptr(wgt)), _stream_handle(stream, self.device)))
@@ -454,11 +454,12 @@ class Context:
                                       or t.numel() < n):
                     raise PlfxError(ERR_INVALID, f"scaler of op {j} must be a contiguous uint8 "
                                                  f"device tensor of >= n elements")
-        if wgt is not None and (wgt.dtype != torch.int32 or wgt.numel() < n or not wgt.is_cuda):
-            raise PlfxError(ERR_INVALID, "wgt must be an int32 device tensor of >= n elements")
+        _check_aux(n, wgt, None, None)
         for t in (pmats, EV):
             if not t.is_cuda or not t.is_contiguous():
                 raise PlfxError(ERR_INVALID, "pmats and EV must be contiguous device tensors")
+        if EV.numel() < states * states:
+            raise PlfxError(ERR_INVALID, f"EV needs {states * states} values")
         top = (TravOp * nops)(*[TravOp(*map(int, r)) for r in ops])
         slots = (C.c_void_p * nslots)(*[None if t is None else t.data_ptr() for t in clv])
         tp = None
