@@ -325,19 +325,26 @@ TREE_GOLDEN_N = 257       # ragged: not a multiple of any kernel's trip
 TREE_GOLDEN_SEED = 6464
 
 
+TREE_GOLDEN_TIPS = ("dense", "coded", "mixed")
+
+
 def tree_golden_case(dtype, coded, n=TREE_GOLDEN_N, seed=TREE_GOLDEN_SEED):
     """Inputs of the committed tree-sweep fixtures (tests/golden/tree64.npz):
     BASELINE configs[2]'s 64-taxon balanced tree at a small ragged site count,
     P and EV scaled by 0.25 so the deep levels underflow and the
-    scaler path runs.  coded: every tip is DNA state codes (20 % ambiguous),
-    expanded to the dense CLV plf() reads.  Returns dict(ops, tips (dense
-    CLVs), codes (None or per tip), pm, EV, wgt, n)."""
+    scaler path runs.  coded: False / "dense" (every tip a dense CLV), True /
+    "coded" (every tip DNA state codes, 20 % ambiguous, expanded to the dense
+    CLV plf() reads) or "mixed" (tips 4j+1 and 4j+2 coded, the rest dense:
+    tip/tip, tip/inner and inner/inner nodes).  Returns dict(ops, tips (dense
+    CLVs), codes (per tip: codes or None), pm, EV, wgt, n)."""
+    mode = {False: "dense", True: "coded"}.get(coded, coded)
     dt = np.dtype(dtype)
-    rng = np.random.default_rng(seed + (1 if coded else 0))
+    rng = np.random.default_rng(seed + TREE_GOLDEN_TIPS.index(mode))
     ops = balanced_tree_ops(64)
-    codes = [random_tip_codes(rng, n, 0.2) for _ in range(64)] if coded else None
-    tips = ([expand_tips(c, dt) for c in codes] if coded
-            else [rng.random(16 * n).astype(dt) for _ in range(64)])
+    is_coded = [mode == "coded" or (mode == "mixed" and t % 4 in (1, 2)) for t in range(64)]
+    codes = [random_tip_codes(rng, n, 0.2) if c else None for c in is_coded]
+    dense = [None if c else rng.random(16 * n).astype(dt) for c in is_coded]
+    tips = [expand_tips(c, dt) if c is not None else d for c, d in zip(codes, dense)]
     pm = (rng.random(ops.shape[0] * 128) * 0.25).astype(dt)
     EV = (rng.random(16) * 0.25).astype(dt)
     wgt = rng.integers(1, 5, n).astype(np.int32)

@@ -140,14 +140,14 @@ def make_edge():
 def make_tree64():
     """BASELINE configs[2]'s 64-taxon post-order sweep, as the composition of
     the reference's own plf() (oracle.ref_traverse: the unmodified plf.cpp,
-    float build and double instantiation, one call per inner node), dense and
-    state-coded tips: per op the sha256 of the parent CLV's bytes, the
+    float build and double instantiation, one call per inner node), dense, state-coded and
+    mixed tips: per op the sha256 of the parent CLV's bytes, the
     per-site scaler bytes and the weighted scaler sum, plus the root CLV."""
     d = {}
     for dt in (np.float32, np.float64):
-        for coded in (False, True):
-            k = f"{'f32' if dt == np.float32 else 'f64'}_{'coded' if coded else 'dense'}"
-            c = O.tree_golden_case(dt, coded)
+        for mode in O.TREE_GOLDEN_TIPS:
+            k = f"{'f32' if dt == np.float32 else 'f64'}_{mode}"
+            c = O.tree_golden_case(dt, mode)
             nops = c["ops"].shape[0]
             clv = [t.copy() for t in c["tips"]] + [np.zeros(16 * c["n"], dt) for _ in range(nops)]
             sums, scal = O.ref_traverse(c["ops"], clv, c["pm"], c["EV"], c["n"], c["wgt"], want_scalers=True)

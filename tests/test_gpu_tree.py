@@ -195,21 +195,22 @@ def test_tree64_full_size_window(ctx, oracle):
 
 
 @pytest.mark.parametrize("fuse", ["3", "2", "1", "0"])
-@pytest.mark.parametrize("dtype,coded", [(np.float64, False), (np.float32, False), (np.float64, True),
-                                         (np.float32, True)])
-def test_tree64_reference_golden(oracle, dtype, coded, fuse, monkeypatch):
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("mode", ["dense", "coded", "mixed"])
+def test_tree64_reference_golden(oracle, dtype, mode, fuse, monkeypatch):
     """configs[2] pinned by the reference itself: the 64-taxon sweep under
     every schedule (PLFX_FUSE 3: one six-level pass; 2: three-level passes +
     level pairs; 1: level pairs; 0: batched levels) reproduces
     tests/golden/tree64.npz -- the unmodified reference plf() called per inner
     node (oracle.ref_traverse) -- byte for byte: every parent CLV (sha256), the
-    per-site scaler bytes and the weighted sums, dense and state-coded tips."""
+    per-site scaler bytes and the weighted sums; dense, state-coded and mixed
+    tips (tip/tip, tip/inner and inner/inner nodes)."""
     import plfx
     import torch
 
     g = np.load(__import__("conftest").GOLDEN / "tree64.npz", allow_pickle=False)
-    k = f"{'f32' if dtype == np.float32 else 'f64'}_{'coded' if coded else 'dense'}"
-    c = oracle.tree_golden_case(dtype, coded, int(g["n"]), int(g["seed"]))
+    k = f"{'f32' if dtype == np.float32 else 'f64'}_{mode}"
+    c = oracle.tree_golden_case(dtype, mode, int(g["n"]), int(g["seed"]))
     assert oracle.tree_case_digest(c) == str(g[f"{k}_inputs_sha256"])
     n, ops = c["n"], c["ops"]
     nops = ops.shape[0]
@@ -217,9 +218,9 @@ def test_tree64_reference_golden(oracle, dtype, coded, fuse, monkeypatch):
     ctx = plfx.Context(0)
     try:
         tt = torch.float64 if dtype == np.float64 else torch.float32
-        clv = [None if coded else dev(t) for t in c["tips"]]
+        clv = [None if cd is not None else dev(t) for t, cd in zip(c["tips"], c["codes"])]
         clv += [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nops)]
-        tips = ([dev(cd) for cd in c["codes"]] if coded else [None] * 64) + [None] * nops
+        tips = [None if cd is None else dev(cd) for cd in c["codes"]] + [None] * nops
         sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
         scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
         ctx.traverse(ops, clv, dev(c["pm"]), dev(c["EV"]), n, dev(c["wgt"]), scal, sums, tips=tips)
@@ -227,7 +228,7 @@ def test_tree64_reference_golden(oracle, dtype, coded, fuse, monkeypatch):
         sched = ctx.last_schedule()
     finally:
         ctx.close()
-    if fuse == "3":
+    if fuse == "3" and mode != "mixed":
         assert sched["deep6"] == 1, sched
     got = [oracle.clv_digest(clv[int(p)].cpu().numpy()) for p in ops[:, 0]]
     bad = [j for j, (a, b) in enumerate(zip(got, g[f"{k}_x3_sha256"])) if a != str(b)]

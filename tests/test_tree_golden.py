@@ -7,7 +7,7 @@ holds that composition as produced by the unmodified reference build
 (oracle.ref_traverse over oracle/_ref; generator tests/golden/make_golden.py
 make_tree64): per op the sha256 of the parent CLV, the per-site scaler bytes,
 the weighted scaler sum, and the root CLV -- f32 and f64 (the reference source
-with float spelled double), dense and state-coded tips.
+with float spelled double), dense, state-coded and mixed tips.
 
 Here the oracle's own sequential traversal (plf_oracle.c plfo_traverse, the
 checker of every GPU traversal test) must reproduce those bytes, and the live
@@ -19,11 +19,11 @@ import pytest
 
 from conftest import golden
 
-CASES = [(np.float32, False), (np.float32, True), (np.float64, False), (np.float64, True)]
+CASES = [(dt, mode) for dt in (np.float32, np.float64) for mode in ("dense", "coded", "mixed")]
 
 
-def key(dt, coded):
-    return f"{'f32' if dt == np.float32 else 'f64'}_{'coded' if coded else 'dense'}"
+def key(dt, mode):
+    return f"{'f32' if dt == np.float32 else 'f64'}_{mode}"
 
 
 def check_against_golden(oracle, g, k, case, clv, sums, scal):
@@ -37,34 +37,34 @@ def check_against_golden(oracle, g, k, case, clv, sums, scal):
     assert np.array_equal(root.view(np.uint8), g[f"{k}_root"].view(np.uint8))
 
 
-@pytest.mark.parametrize("dt,coded", CASES)
-def test_fixture_inputs_regenerate(oracle, dt, coded):
+@pytest.mark.parametrize("dt,mode", CASES)
+def test_fixture_inputs_regenerate(oracle, dt, mode):
     g = golden("tree64.npz")
-    c = oracle.tree_golden_case(dt, coded, int(g["n"]), int(g["seed"]))
-    assert oracle.tree_case_digest(c) == str(g[f"{key(dt, coded)}_inputs_sha256"])
-    assert g[f"{key(dt, coded)}_sums"].sum() > 0  # the scaler path is in the fixture
+    c = oracle.tree_golden_case(dt, mode, int(g["n"]), int(g["seed"]))
+    assert oracle.tree_case_digest(c) == str(g[f"{key(dt, mode)}_inputs_sha256"])
+    assert g[f"{key(dt, mode)}_sums"].sum() > 0  # the scaler path is in the fixture
 
 
-@pytest.mark.parametrize("dt,coded", CASES)
-def test_oracle_traverse_matches_reference_composition(oracle, dt, coded):
+@pytest.mark.parametrize("dt,mode", CASES)
+def test_oracle_traverse_matches_reference_composition(oracle, dt, mode):
     g = golden("tree64.npz")
-    c = oracle.tree_golden_case(dt, coded, int(g["n"]), int(g["seed"]))
+    c = oracle.tree_golden_case(dt, mode, int(g["n"]), int(g["seed"]))
     n, ops = c["n"], c["ops"]
     clv = [t.copy() for t in c["tips"]] + [np.zeros(16 * n, dt) for _ in range(ops.shape[0])]
     sums, scal = oracle.traverse(4, 4, ops, clv, c["pm"], c["EV"], n, c["wgt"], want_scalers=True)
-    check_against_golden(oracle, g, key(dt, coded), c, clv, sums, scal)
+    check_against_golden(oracle, g, key(dt, mode), c, clv, sums, scal)
 
 
-@pytest.mark.parametrize("dt,coded", CASES)
-def test_live_reference_reproduces_fixture(oracle, dt, coded):
+@pytest.mark.parametrize("dt,mode", CASES)
+def test_live_reference_reproduces_fixture(oracle, dt, mode):
     if not oracle.ref_available(dt):
         pytest.skip("oracle/_ref not built (no /root/reference on this machine)")
     g = golden("tree64.npz")
-    c = oracle.tree_golden_case(dt, coded, int(g["n"]), int(g["seed"]))
+    c = oracle.tree_golden_case(dt, mode, int(g["n"]), int(g["seed"]))
     n, ops = c["n"], c["ops"]
     clv = [t.copy() for t in c["tips"]] + [np.zeros(16 * n, dt) for _ in range(ops.shape[0])]
     sums, scal = oracle.ref_traverse(ops, clv, c["pm"], c["EV"], n, c["wgt"], want_scalers=True)
-    check_against_golden(oracle, g, key(dt, coded), c, clv, sums, scal)
+    check_against_golden(oracle, g, key(dt, mode), c, clv, sums, scal)
 
 
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
