@@ -172,6 +172,8 @@ def _destroy_streams(hs):
         assert hip.hipStreamDestroy(ctypes.c_void_p(h)) == 0
 
 
+# the rejected capture below ends with an empty graph, which torch warns about
+@pytest.mark.filterwarnings("ignore:The CUDA Graph is empty")
 def test_graph_capture_first_use_from_the_pool(oracle):
     """The first PLFX_WS_POOL streams take workspaces allocated with the
     context, so a stream's FIRST sum-producing call may be inside a capture;
