@@ -8,7 +8,7 @@ set -eu
 S=${1:?session dir under gpurun_out}; TAG=${2:-r03}
 O=gpurun_out/$S; P=profiles
 [ -f $O/pytest_gpu.log ] && tail -3 $O/pytest_gpu.log > $P/${TAG}_pytest_gpu.log
-for W in node node_f32 protein tree64 tree64_tips nodes512 prottree64 prottree64_tips; do
+for W in node node_f32 protein protein_exact protein_f32 tree64 tree64_tips nodes512 prottree64 prottree64_tips; do
   [ -f $O/$W/bench.log ] || continue
   tail -1 $O/$W/bench.log > $P/${TAG}_${W}_bench.json
   cp $O/$W/kernel_stats.csv $P/${TAG}_${W}_kernel_stats.csv

@@ -21,5 +21,7 @@ for w in $W; do
     nodes512) EXTRA_STEPS=1 bash tools/gpu_r03_measure.sh $T/nodes512 2 --workload nodes512 --steps 10 --warmup 2 || exit 1 ;;
     prottree64) bash tools/gpu_r03_measure.sh $T/prottree64 10 --workload prottree64 --steps 50 --warmup 5 || exit 1 ;;
     prottree64_tips) bash tools/gpu_r03_measure.sh $T/prottree64_tips 10 --workload prottree64 --tips --steps 50 --warmup 5 || exit 1 ;;
+    protein_exact) bash tools/gpu_r03_measure.sh $T/protein_exact 20 --workload protein --exact || exit 1 ;;
+    protein_f32) bash tools/gpu_r03_measure.sh $T/protein_f32 20 --workload protein --dtype f32 || exit 1 ;;
   esac
 done
