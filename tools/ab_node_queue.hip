@@ -1,0 +1,357 @@
+// A/B harness (not product code): the headline f64 node kernel
+// (plf_dna_f64_pair_kernel, csrc/plf_dna.hpp) against a variant whose wave
+// trips after the first kStatic come from per-pool dynamic chunk queues.
+//
+// Why: a per-wave timeline of the product kernel at 2^20 sites
+// (tools/probes/wave_timeline.hip, profiles/r01_probe_wave_timeline.log) has
+// wave exits p1 57 / p50 61-63 / p90 63.5-67 / max 67-73 us -- every wave makes
+// exactly 8 trips, so the launch ends with the waves the memory arbitration
+// served last.  The variant lets early waves take the late ones' trips.
+// Pools: blockIdx % kPools (blocks are dispatched round-robin over the 8
+// XCDs, so pool = XCD for kPools = 8 and the head words stay XCD-local), one
+// head word per pool in the stream workspace's second region; chunk = one
+// wave trip (16 U sites); trip i >= kStatic takes chunk kStatic*W + kPools*d +
+// pool, d from a returning atomic issued a trip ahead (WaveQueue's protocol,
+// plf_dna.hpp), the last wave out zeroes the words.  Every chunk is computed
+// exactly as in the product body, so x3, scaler bytes and sums must be
+// bit-identical (checked).
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//     -I amd-versal-phylogenetic-likelihood-function_amd/csrc tools/ab_node_queue.hip -o build/ab_node_queue
+//   build/ab_node_queue [log2 sites ...]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "plf_dna.hpp"
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      printf("%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                             \
+    }                                                                      \
+  } while (0)
+
+using namespace plfx::dev;
+
+// pooled queue words: head of pool p at q[16 p], exit count at q[16 kPools]
+template <int kPools>
+struct PoolQueue {
+  unsigned long long *head, *done;
+  int64_t W, nch, first;
+  int pool;
+  long long pend = 0;
+  bool dyn;
+  __device__ PoolQueue(unsigned long long *q, int64_t n, int64_t chunk, int kStatic) {
+    int zero = 0;
+    asm volatile("" : "+v"(zero));
+    pool = blockIdx.x % kPools;
+    head = q + 16 * pool + zero;
+    done = q + 16 * kPools;
+    W = (int64_t)gridDim.x * kWavesPerBlock;
+    nch = (n + chunk - 1) / chunk;
+    first = (int64_t)kStatic * W;
+    dyn = nch > first && gridDim.x >= kPools;
+  }
+  __device__ __forceinline__ void dequeue() {
+    if (dyn && (threadIdx.x & 63) == 0)
+      pend = (long long)__hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // chunk index taken from the queue (nch: none left)
+  __device__ __forceinline__ int64_t taken() const {
+    if (!dyn) return nch;
+    const long long d = (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)pend) |
+                        ((long long)__builtin_amdgcn_readfirstlane((int)(pend >> 32)) << 32);
+    const int64_t c = first + (int64_t)kPools * d + pool;
+    return c < nch ? c : nch;
+  }
+  __device__ __forceinline__ void finish() const {
+    if (!dyn || (threadIdx.x & 63) != 0) return;
+    const unsigned long long later = (unsigned long long)(pend >> 62);  // 0 once it returned
+    const unsigned long long d = __hip_atomic_fetch_add(done, 1ull + later, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (unsigned long long)W - 1) {
+      for (int p = 0; p <= kPools; p++)
+        __hip_atomic_store(head - 16 * pool + 16 * p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+};
+
+// The product body's per-8-site work and trip shape, with the trip bases
+// from the pooled queue after kStatic static trips.
+template <int U, int kPools, int kStatic>
+__global__ void __launch_bounds__(kBlock, 1)
+pair_queue_kernel(const double *__restrict__ x1, const double *__restrict__ x2, double *__restrict__ x3,
+                  const double *__restrict__ EV, const double *__restrict__ left,
+                  const double *__restrict__ right, const int32_t *__restrict__ wgt,
+                  uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws, int64_t *scaler_sum) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 1, c = (lane >> 1) & 3, g = lane >> 3, sh = lane & 56;
+  double PL[2][4], PR[2][4], E[4][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      PL[kk][l] = left[c * 16 + (2 * h + kk) * 4 + l];
+      PR[kk][l] = right[c * 16 + (2 * h + kk) * 4 + l];
+    }
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int t = 0; t < 2; t++) E[k][t] = EV[4 * k + 2 * h + t];
+  const double m = Num<double>::minlik();
+  long long acc = 0;
+
+  auto body = [&](const f64x2 a, const f64x2 b, int64_t site0, bool valid, int w) {
+    double u1[2], u2[2];
+    {
+      const double a0 = dpp_f64<kQuadEven>(a.x), a1 = dpp_f64<kQuadEven>(a.y);
+      const double a2 = dpp_f64<kQuadOdd>(a.x), a3 = dpp_f64<kQuadOdd>(a.y);
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) {
+        double v = a0 * PL[kk][0];
+        v += a1 * PL[kk][1]; v += a2 * PL[kk][2]; v += a3 * PL[kk][3];
+        u1[kk] = v;
+      }
+    }
+    {
+      const double b0 = dpp_f64<kQuadEven>(b.x), b1 = dpp_f64<kQuadEven>(b.y);
+      const double b2 = dpp_f64<kQuadOdd>(b.x), b3 = dpp_f64<kQuadOdd>(b.y);
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) {
+        double v = b0 * PR[kk][0];
+        v += b1 * PR[kk][1]; v += b2 * PR[kk][2]; v += b3 * PR[kk][3];
+        u2[kk] = v;
+      }
+    }
+    double pm[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) pm[kk] = u1[kk] * u2[kk];
+    const double p0 = dpp_f64<kQuadEven>(pm[0]), p1 = dpp_f64<kQuadEven>(pm[1]);
+    const double p2 = dpp_f64<kQuadOdd>(pm[0]), p3 = dpp_f64<kQuadOdd>(pm[1]);
+    double o[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      double x = 0.0;
+      x += p0 * E[0][t]; x += p1 * E[1][t]; x += p2 * E[2][t]; x += p3 * E[3][t];
+      o[t] = x;
+    }
+    const bool small = valid && (__builtin_fabs(o[0]) < m) && (__builtin_fabs(o[1]) < m);
+    const unsigned long long mask = __ballot(small);
+    const bool sc = ((mask >> sh) & 0xFFull) == 0xFFull;
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const double s = o[t] * Num<double>::two32();
+      o[t] = sc ? s : o[t];
+    }
+    if (valid) {
+      f64x2 ov = {o[0], o[1]};
+      __builtin_nontemporal_store(ov, reinterpret_cast<f64x2 *>(x3 + site0 * 16) + lane);
+      if ((lane & 7) == 0 && scaler) scaler[site0 + g] = (uint8_t)sc;
+      if ((lane & 7) == 0 && sc) acc += w;
+    }
+  };
+
+  constexpr int64_t kChunk = 16 * U;
+  PoolQueue<kPools> q(ws + kWsWords, n, kChunk, kStatic);
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  // chunk of this trip and of the next one; the queue's answer for trip t + 2
+  // is requested in trip t (after its loads) and read at its end
+  int64_t ch = wave, ch1 = q.W + wave;
+  for (int trip = 0; ch < q.nch; trip++) {
+    const int64_t base = ch * kChunk;
+    const bool ask = q.dyn && trip + 2 >= kStatic;
+    if (base + kChunk <= n) {
+      f64x2 a[U][2], b[U][2];
+      int w[U][2];
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const int64_t site0 = base + u * 16 + j * 8;
+          a[u][j] = ld16<true>(reinterpret_cast<const f64x2 *>(x1 + site0 * 16) + lane);
+          b[u][j] = ld16<true>(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
+          w[u][j] = wgt ? wgt[site0 + g] : 1;
+        }
+      if (ask) q.dequeue();
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) body(a[u][j], b[u][j], base + u * 16 + j * 8, true, w[u][j]);
+    } else {
+      if (ask) q.dequeue();
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const int64_t site0 = base + u * 16 + j * 8;
+          const bool valid = site0 + g < n;
+          f64x2 a = {0.0, 0.0}, b = {0.0, 0.0};
+          int w = 0;
+          if (valid) {
+            a = reinterpret_cast<const f64x2 *>(x1 + site0 * 16)[lane];
+            b = reinterpret_cast<const f64x2 *>(x2 + site0 * 16)[lane];
+            w = wgt ? wgt[site0 + g] : 1;
+          }
+          body(a, b, site0, valid, w);
+        }
+    }
+    ch = ch1;
+    ch1 = ask ? q.taken() : (int64_t)(trip + 2) * q.W + wave;  // static grid stride before kStatic
+  }
+  q.finish();
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
+// product kernel
+using Prod = decltype(&plf_dna_f64_pair_kernel<2, true, 1, true>);
+
+__global__ void fill(double *p, int64_t n16, uint64_t seed, bool scale4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    double v = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    if (scale4 && ((i / 16) % 4 == 0)) v *= 1e-12;
+    p[i] = v;
+  }
+}
+
+struct Set {
+  double *x1, *x2, *x3;
+  uint8_t *sc;
+  int64_t *sum;
+};
+
+int main(int argc, char **argv) {
+  std::vector<int> logs;
+  for (int i = 1; i < argc; i++) logs.push_back(atoi(argv[i]));
+  if (logs.empty()) logs = {20, 18, 22};
+  const int kSets = 4, kRounds = 15, kReps = 40;
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  int occ = 0;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)&plf_dna_f64_pair_kernel<2, true, 1, true>,
+                                                  kBlock, 0));
+  const int grid = occ * cus;
+  printf("CUs %d, product occupancy %d blocks/CU, grid %d\n", cus, occ, grid);
+  double *EV, *L, *R;
+  int32_t *wgt;
+  unsigned long long *ws;
+  CK(hipMalloc(&EV, 16 * 8));
+  CK(hipMalloc(&L, 64 * 8));
+  CK(hipMalloc(&R, 64 * 8));
+  CK(hipMalloc(&ws, 2 * kWsWords * 8 * 4));
+  CK(hipMemset(ws, 0, 2 * kWsWords * 8 * 4));
+  fill<<<1, 64>>>(EV, 16, 11, false);
+  fill<<<1, 64>>>(L, 64, 12, false);
+  fill<<<1, 64>>>(R, 64, 13, false);
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+
+  struct Var {
+    const char *name;
+    void (*launch)(const Set &, int64_t, const double *, const double *, const double *, const int32_t *,
+                   unsigned long long *, int, hipStream_t);
+  };
+  auto prod = [](const Set &t, int64_t n, const double *EV, const double *L, const double *R, const int32_t *w,
+                 unsigned long long *ws, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((plf_dna_f64_pair_kernel<2, true, 1, true>), dim3(grid), dim3(kBlock), 0, s, t.x1, t.x2,
+                       t.x3, EV, L, R, w, t.sc, n, ws, t.sum);
+  };
+#define QV(P, S)                                                                                         \
+  [](const Set &t, int64_t n, const double *EV, const double *L, const double *R, const int32_t *w,     \
+     unsigned long long *ws, int grid, hipStream_t s) {                                                 \
+    hipLaunchKernelGGL((pair_queue_kernel<2, P, S>), dim3(grid), dim3(kBlock), 0, s, t.x1, t.x2, t.x3, EV, L, \
+                       R, w, t.sc, n, ws, t.sum);                                                        \
+  }
+  std::vector<Var> vars = {{"product", prod},       {"queue p8 s2", QV(8, 2)}, {"queue p8 s4", QV(8, 4)},
+                           {"queue p8 s6", QV(8, 6)}, {"queue p32 s4", QV(32, 4)}, {"queue p1 s6", QV(1, 6)}};
+  for (int lg : logs) {
+    const int64_t n = (int64_t)1 << lg;
+    std::vector<Set> sets(kSets);
+    int32_t *w;
+    CK(hipMalloc(&w, n * 4));
+    std::vector<int32_t> ones(n, 1);
+    CK(hipMemcpy(w, ones.data(), n * 4, hipMemcpyHostToDevice));
+    for (int k = 0; k < kSets; k++) {
+      CK(hipMalloc(&sets[k].x1, n * 128));
+      CK(hipMalloc(&sets[k].x2, n * 128));
+      CK(hipMalloc(&sets[k].x3, n * 128));
+      CK(hipMalloc(&sets[k].sc, n));
+      CK(hipMalloc(&sets[k].sum, 8));
+      fill<<<1024, 256>>>(sets[k].x1, n * 16, 100 + k, true);
+      fill<<<1024, 256>>>(sets[k].x2, n * 16, 200 + k, false);
+    }
+    CK(hipDeviceSynchronize());
+    // correctness: every variant bit-identical to the product on set 0, twice
+    // (the second launch checks the queue words were left at zero)
+    std::vector<double> ref3(n * 16), got3(n * 16);
+    std::vector<uint8_t> refs(n), gots(n);
+    int64_t refsum = 0, gotsum = 0;
+    bool all_ok = true;
+    for (size_t v = 0; v < vars.size(); v++) {
+      for (int rep = 0; rep < 2; rep++) {
+        CK(hipMemset(sets[0].x3, 0xff, n * 128));
+        CK(hipMemset(sets[0].sc, 0x7f, n));
+        vars[v].launch(sets[0], n, EV, L, R, w, ws, grid, s);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(v == 0 ? ref3.data() : got3.data(), sets[0].x3, n * 128, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(v == 0 ? refs.data() : gots.data(), sets[0].sc, n, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(v == 0 ? &refsum : &gotsum, sets[0].sum, 8, hipMemcpyDeviceToHost));
+        if (v > 0) {
+          const bool ok = !memcmp(ref3.data(), got3.data(), n * 128) && !memcmp(refs.data(), gots.data(), n) &&
+                          refsum == gotsum;
+          if (!ok) printf("  MISMATCH %s rep %d (sum %lld vs %lld)\n", vars[v].name, rep, (long long)gotsum,
+                          (long long)refsum);
+          all_ok = all_ok && ok;
+        }
+      }
+    }
+    std::vector<unsigned long long> wsh(2 * kWsWords);
+    CK(hipMemcpy(wsh.data(), ws, 2 * kWsWords * 8, hipMemcpyDeviceToHost));
+    bool zero = std::all_of(wsh.begin(), wsh.end(), [](unsigned long long x) { return x == 0; });
+    printf("2^%d sites: bit-identical %s, workspace zero after runs: %s, product sum %lld\n", lg,
+           all_ok ? "yes" : "NO", zero ? "yes" : "NO", (long long)refsum);
+    if (!all_ok || !zero) return 2;
+    // timing: interleaved rounds, kReps launches over the rotating sets
+    std::vector<std::vector<float>> us(vars.size());
+    for (int r = 0; r < kRounds; r++)
+      for (size_t v = 0; v < vars.size(); v++) {
+        for (int i = 0; i < 8; i++) vars[v].launch(sets[i % kSets], n, EV, L, R, w, ws, grid, s);
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < kReps; i++) vars[v].launch(sets[i % kSets], n, EV, L, R, w, ws, grid, s);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        us[v].push_back(ms * 1000.f / kReps);
+      }
+    const double bytes = 385.0 * n;
+    for (size_t v = 0; v < vars.size(); v++) {
+      std::vector<float> x = us[v];
+      std::sort(x.begin(), x.end());
+      const double med = x[x.size() / 2];
+      printf("  %-14s median %8.2f us  (min %8.2f max %8.2f)  %.3f of 8 TB/s\n", vars[v].name, med, x.front(),
+             x.back(), bytes / (med * 1e-6) / 8e12);
+    }
+    for (auto &t : sets) {
+      CK(hipFree(t.x1));
+      CK(hipFree(t.x2));
+      CK(hipFree(t.x3));
+      CK(hipFree(t.sc));
+      CK(hipFree(t.sum));
+    }
+    CK(hipFree(w));
+  }
+  return 0;
+}
