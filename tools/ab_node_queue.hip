@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "plf_dna.hpp"
@@ -84,7 +85,7 @@ struct PoolQueue {
 
 // The product body's per-8-site work and trip shape, with the trip bases
 // from the pooled queue after kStatic static trips.
-template <int U, int kPools, int kStatic>
+template <int U, int kPools, int kStatic, int Ud>
 __global__ void __launch_bounds__(kBlock, 1)
 pair_queue_kernel(const double *__restrict__ x1, const double *__restrict__ x2, double *__restrict__ x3,
                   const double *__restrict__ EV, const double *__restrict__ left,
@@ -157,20 +158,22 @@ pair_queue_kernel(const double *__restrict__ x1, const double *__restrict__ x2, 
     }
   };
 
-  constexpr int64_t kChunk = 16 * U;
-  PoolQueue<kPools> q(ws + kWsWords, n, kChunk, kStatic);
+  // static trips: chunks of U steps (16 U sites) by the grid stride; after
+  // kStatic of them, chunks of Ud steps from the pools, first = the sites the
+  // static trips cover
+  const int64_t W = (int64_t)gridDim.x * kWavesPerBlock;
+  const int64_t first = (int64_t)kStatic * W * 16 * U;
+  PoolQueue<kPools> q(ws + kWsWords, n > first ? n - first : 0, 16 * Ud, 0);
+  q.dyn = q.dyn && n > first;
   const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  // chunk of this trip and of the next one; the queue's answer for trip t + 2
-  // is requested in trip t (after its loads) and read at its end
-  int64_t ch = wave, ch1 = q.W + wave;
-  for (int trip = 0; ch < q.nch; trip++) {
-    const int64_t base = ch * kChunk;
-    const bool ask = q.dyn && trip + 2 >= kStatic;
-    if (base + kChunk <= n) {
-      f64x2 a[U][2], b[U][2];
-      int w[U][2];
+  // one chunk of S steps at base; ask: request the chunk of trip t + 2
+  auto run = [&](auto steps, int64_t base, bool ask) {
+    constexpr int S = decltype(steps)::value;
+    if (base + 16 * S <= n) {
+      f64x2 a[S][2], b[S][2];
+      int w[S][2];
 #pragma unroll
-      for (int u = 0; u < U; u++)
+      for (int u = 0; u < S; u++)
 #pragma unroll
         for (int j = 0; j < 2; j++) {
           const int64_t site0 = base + u * 16 + j * 8;
@@ -180,13 +183,13 @@ pair_queue_kernel(const double *__restrict__ x1, const double *__restrict__ x2, 
         }
       if (ask) q.dequeue();
 #pragma unroll
-      for (int u = 0; u < U; u++)
+      for (int u = 0; u < S; u++)
 #pragma unroll
         for (int j = 0; j < 2; j++) body(a[u][j], b[u][j], base + u * 16 + j * 8, true, w[u][j]);
     } else {
       if (ask) q.dequeue();
 #pragma unroll
-      for (int u = 0; u < U; u++)
+      for (int u = 0; u < S; u++)
 #pragma unroll
         for (int j = 0; j < 2; j++) {
           const int64_t site0 = base + u * 16 + j * 8;
@@ -201,8 +204,23 @@ pair_queue_kernel(const double *__restrict__ x1, const double *__restrict__ x2, 
           body(a, b, site0, valid, w);
         }
     }
-    ch = ch1;
-    ch1 = ask ? q.taken() : (int64_t)(trip + 2) * q.W + wave;  // static grid stride before kStatic
+  };
+  // base of this trip and of the next; the queue's answer for trip t + 2 is
+  // requested in trip t (after its loads) and read at its end.  Without the
+  // queue (small n or grid) every trip is a static grid-stride one.
+  int64_t base = wave * 16 * U, base1 = (W + wave) * 16 * U;
+  for (int trip = 0; base < n; trip++) {
+    const bool ask = q.dyn && trip + 2 >= kStatic;
+    if (q.dyn && trip >= kStatic) run(std::integral_constant<int, Ud>{}, base, ask);
+    else run(std::integral_constant<int, U>{}, base, ask);
+    base = base1;
+    if (ask) {
+      const int64_t c = q.taken();  // chunk index within the dynamic region (q.nch: none)
+      base1 = c < q.nch ? first + c * 16 * Ud : n;
+    } else {
+      base1 = (int64_t)(trip + 2) * W * 16 * U + wave * 16 * U;
+      if (q.dyn && trip + 2 >= kStatic) base1 = n;  // unreachable: ask covers these trips
+    }
   }
   q.finish();
   block_ticket_sum(acc, ws, scaler_sum);
@@ -268,14 +286,16 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((plf_dna_f64_pair_kernel<2, true, 1, true>), dim3(grid), dim3(kBlock), 0, s, t.x1, t.x2,
                        t.x3, EV, L, R, w, t.sc, n, ws, t.sum);
   };
-#define QV(P, S)                                                                                         \
+#define QV(P, S, UD)                                                                                     \
   [](const Set &t, int64_t n, const double *EV, const double *L, const double *R, const int32_t *w,     \
      unsigned long long *ws, int grid, hipStream_t s) {                                                 \
-    hipLaunchKernelGGL((pair_queue_kernel<2, P, S>), dim3(grid), dim3(kBlock), 0, s, t.x1, t.x2, t.x3, EV, L, \
-                       R, w, t.sc, n, ws, t.sum);                                                        \
+    hipLaunchKernelGGL((pair_queue_kernel<2, P, S, UD>), dim3(grid), dim3(kBlock), 0, s, t.x1, t.x2, t.x3, EV, \
+                       L, R, w, t.sc, n, ws, t.sum);                                                     \
   }
-  std::vector<Var> vars = {{"product", prod},       {"queue p8 s2", QV(8, 2)}, {"queue p8 s4", QV(8, 4)},
-                           {"queue p8 s6", QV(8, 6)}, {"queue p32 s4", QV(32, 4)}, {"queue p1 s6", QV(1, 6)}};
+  std::vector<Var> vars = {{"product", prod},
+                           {"q p8 s2 u2", QV(8, 2, 2)},  {"q p8 s4 u2", QV(8, 4, 2)}, {"q p8 s6 u2", QV(8, 6, 2)},
+                           {"q p32 s4 u2", QV(32, 4, 2)}, {"q p8 s6 u1", QV(8, 6, 1)}, {"q p32 s6 u1", QV(32, 6, 1)},
+                           {"q p32 s7 u1", QV(32, 7, 1)}};
   for (int lg : logs) {
     const int64_t n = (int64_t)1 << lg;
     std::vector<Set> sets(kSets);
