@@ -321,8 +321,8 @@ int main(int argc, char **argv) {
     bool all_ok = true;
     for (size_t v = 0; v < vars.size(); v++) {
       for (int rep = 0; rep < 2; rep++) {
-        CK(hipMemset(sets[0].x3, 0xff, n * 128));
-        CK(hipMemset(sets[0].sc, 0x7f, n));
+        CK(hipMemsetAsync(sets[0].x3, 0xff, n * 128, s));
+        CK(hipMemsetAsync(sets[0].sc, 0x7f, n, s));
         vars[v].launch(sets[0], n, EV, L, R, w, ws, grid, s);
         CK(hipStreamSynchronize(s));
         CK(hipMemcpy(v == 0 ? ref3.data() : got3.data(), sets[0].x3, n * 128, hipMemcpyDeviceToHost));
@@ -331,8 +331,24 @@ int main(int argc, char **argv) {
         if (v > 0) {
           const bool ok = !memcmp(ref3.data(), got3.data(), n * 128) && !memcmp(refs.data(), gots.data(), n) &&
                           refsum == gotsum;
-          if (!ok) printf("  MISMATCH %s rep %d (sum %lld vs %lld)\n", vars[v].name, rep, (long long)gotsum,
-                          (long long)refsum);
+          if (!ok) {
+            int64_t bad3 = 0, bads = 0, unw = 0, first3 = -1;
+            const uint64_t *r64 = reinterpret_cast<const uint64_t *>(ref3.data());
+            const uint64_t *g64 = reinterpret_cast<const uint64_t *>(got3.data());
+            for (int64_t i = 0; i < n * 16; i++) {
+              if (r64[i] != g64[i]) {
+                bad3++;
+                if (first3 < 0) first3 = i;
+              }
+              unw += g64[i] == ~0ull;
+            }
+            for (int64_t i = 0; i < n; i++) bads += refs[i] != gots[i];
+            printf("  MISMATCH %s rep %d (sum %lld vs %lld): x3 values differing %lld (first at site %lld "
+                   "value %d: %a vs %a), unwritten %lld, scaler bytes differing %lld\n",
+                   vars[v].name, rep, (long long)gotsum, (long long)refsum, (long long)bad3,
+                   (long long)(first3 / 16), (int)(first3 % 16), first3 >= 0 ? ref3[first3] : 0.0,
+                   first3 >= 0 ? got3[first3] : 0.0, (long long)unw, (long long)bads);
+          }
           all_ok = all_ok && ok;
         }
       }
