@@ -41,41 +41,44 @@
 using namespace plfx::dev;
 
 // pooled queue words: head of pool p at q[16 p], exit count at q[16 kPools]
+// (kPools = 0: no queue, the static grid stride throughout).  The answer of a
+// request is consumed in the same trip (request before the trip's loads, read
+// after them), so no atomic result is carried across the loop -- a carried
+// one made the compiler wait for every store of the trip (vmcnt(0)) at its end.
 template <int kPools>
 struct PoolQueue {
   unsigned long long *head, *done;
-  int64_t W, nch, first;
+  int64_t W, nch;
   int pool;
-  long long pend = 0;
   bool dyn;
-  __device__ PoolQueue(unsigned long long *q, int64_t n, int64_t chunk, int kStatic) {
+  __device__ PoolQueue(unsigned long long *q, int64_t n, int64_t chunk) {
     int zero = 0;
     asm volatile("" : "+v"(zero));
-    pool = blockIdx.x % kPools;
+    pool = kPools ? blockIdx.x % kPools : 0;
     head = q + 16 * pool + zero;
-    done = q + 16 * kPools;
+    done = q + 16 * (kPools ? kPools : 1);
     W = (int64_t)gridDim.x * kWavesPerBlock;
     nch = (n + chunk - 1) / chunk;
-    first = (int64_t)kStatic * W;
-    dyn = nch > first && gridDim.x >= kPools;
+    dyn = kPools > 0 && nch > 0 && gridDim.x >= kPools;
   }
-  __device__ __forceinline__ void dequeue() {
-    if (dyn && (threadIdx.x & 63) == 0)
-      pend = (long long)__hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // lane 0: the returning add (other lanes: 0)
+  __device__ __forceinline__ long long request() const {
+    long long t = 0;
+    if ((threadIdx.x & 63) == 0)
+      t = (long long)__hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return t;
   }
-  // chunk index taken from the queue (nch: none left)
-  __device__ __forceinline__ int64_t taken() const {
-    if (!dyn) return nch;
-    const long long d = (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)pend) |
-                        ((long long)__builtin_amdgcn_readfirstlane((int)(pend >> 32)) << 32);
-    const int64_t c = first + (int64_t)kPools * d + pool;
+  // chunk index of a request's answer (nch: none left)
+  __device__ __forceinline__ int64_t chunk_of(long long t) const {
+    const long long d = (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)t) |
+                        ((long long)__builtin_amdgcn_readfirstlane((int)(t >> 32)) << 32);
+    const int64_t c = (int64_t)(kPools ? kPools : 1) * d + pool;
     return c < nch ? c : nch;
   }
+  // every request of the wave has been read (chunk_of) before this
   __device__ __forceinline__ void finish() const {
     if (!dyn || (threadIdx.x & 63) != 0) return;
-    const unsigned long long later = (unsigned long long)(pend >> 62);  // 0 once it returned
-    const unsigned long long d = __hip_atomic_fetch_add(done, 1ull + later, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long d = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (d == (unsigned long long)W - 1) {
       for (int p = 0; p <= kPools; p++)
         __hip_atomic_store(head - 16 * pool + 16 * p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -85,7 +88,7 @@ struct PoolQueue {
 
 // The product body's per-8-site work and trip shape, with the trip bases
 // from the pooled queue after kStatic static trips.
-template <int U, int kPools, int kStatic, int Ud>
+template <int U, int kPools>
 __global__ void __launch_bounds__(kBlock, 1)
 pair_queue_kernel(const double *__restrict__ x1, const double *__restrict__ x2, double *__restrict__ x3,
                   const double *__restrict__ EV, const double *__restrict__ left,
@@ -158,69 +161,62 @@ pair_queue_kernel(const double *__restrict__ x1, const double *__restrict__ x2, 
     }
   };
 
-  // static trips: chunks of U steps (16 U sites) by the grid stride; after
-  // kStatic of them, chunks of Ud steps from the pools, first = the sites the
-  // static trips cover
+  // Trips 0 and 1: chunks wave and W + wave (the grid stride); trip t >= 2:
+  // the chunk requested in trip t - 2 from the wave's pool.  Chunks are 16 U
+  // sites; the loop takes full chunks only (one straight-line body, so the
+  // compiler's wait counts stay exact), the one partial chunk of the launch
+  // runs after it.  kPools = 0: the same loop on the static grid stride.
   const int64_t W = (int64_t)gridDim.x * kWavesPerBlock;
-  const int64_t first = (int64_t)kStatic * W * 16 * U;
-  PoolQueue<kPools> q(ws + kWsWords, n > first ? n - first : 0, 16 * Ud, 0);
-  q.dyn = q.dyn && n > first;
+  constexpr int64_t kC = 16 * U;
+  const int64_t nfullch = n / kC, nch = (n + kC - 1) / kC;
+  PoolQueue<kPools> q(ws + kWsWords, n > 2 * W * kC ? n - 2 * W * kC : 0, kC);
   const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  // one chunk of S steps at base; ask: request the chunk of trip t + 2
-  auto run = [&](auto steps, int64_t base, bool ask) {
-    constexpr int S = decltype(steps)::value;
-    if (base + 16 * S <= n) {
-      f64x2 a[S][2], b[S][2];
-      int w[S][2];
+  int64_t ch = wave, ch1 = W + wave;
+  while (ch < nfullch) {
+    const int64_t base = ch * kC;
+    const long long tk = q.dyn ? q.request() : 0ll;
+    f64x2 a[U][2], b[U][2];
+    int w[U][2];
 #pragma unroll
-      for (int u = 0; u < S; u++)
+    for (int u = 0; u < U; u++)
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
-          const int64_t site0 = base + u * 16 + j * 8;
-          a[u][j] = ld16<true>(reinterpret_cast<const f64x2 *>(x1 + site0 * 16) + lane);
-          b[u][j] = ld16<true>(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
-          w[u][j] = wgt ? wgt[site0 + g] : 1;
-        }
-      if (ask) q.dequeue();
-#pragma unroll
-      for (int u = 0; u < S; u++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) body(a[u][j], b[u][j], base + u * 16 + j * 8, true, w[u][j]);
+      for (int j = 0; j < 2; j++) {
+        const int64_t site0 = base + u * 16 + j * 8;
+        a[u][j] = ld16<true>(reinterpret_cast<const f64x2 *>(x1 + site0 * 16) + lane);
+        b[u][j] = ld16<true>(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
+        w[u][j] = wgt[site0 + g];  // the harness always passes weights
+      }
+    int64_t nxt;
+    if (q.dyn) {
+      const int64_t c = q.chunk_of(tk);  // within the dynamic region; q.nch: none
+      nxt = c < q.nch ? 2 * W + c : nch;
     } else {
-      if (ask) q.dequeue();
+      nxt = ch1 + W;
+    }
 #pragma unroll
-      for (int u = 0; u < S; u++)
+    for (int u = 0; u < U; u++)
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
-          const int64_t site0 = base + u * 16 + j * 8;
-          const bool valid = site0 + g < n;
-          f64x2 a = {0.0, 0.0}, b = {0.0, 0.0};
-          int w = 0;
-          if (valid) {
-            a = reinterpret_cast<const f64x2 *>(x1 + site0 * 16)[lane];
-            b = reinterpret_cast<const f64x2 *>(x2 + site0 * 16)[lane];
-            w = wgt ? wgt[site0 + g] : 1;
-          }
-          body(a, b, site0, valid, w);
+      for (int j = 0; j < 2; j++) body(a[u][j], b[u][j], base + u * 16 + j * 8, true, w[u][j]);
+    ch = ch1;
+    ch1 = nxt;
+  }
+  if (ch < nch) {  // the partial chunk (n % kC sites), if this wave drew it
+    const int64_t base = ch * kC;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int64_t site0 = base + u * 16 + j * 8;
+        const bool valid = site0 + g < n;
+        f64x2 a = {0.0, 0.0}, b = {0.0, 0.0};
+        int w = 0;
+        if (valid) {
+          a = reinterpret_cast<const f64x2 *>(x1 + site0 * 16)[lane];
+          b = reinterpret_cast<const f64x2 *>(x2 + site0 * 16)[lane];
+          w = wgt[site0 + g];
         }
-    }
-  };
-  // base of this trip and of the next; the queue's answer for trip t + 2 is
-  // requested in trip t (after its loads) and read at its end.  Without the
-  // queue (small n or grid) every trip is a static grid-stride one.
-  int64_t base = wave * 16 * U, base1 = (W + wave) * 16 * U;
-  for (int trip = 0; base < n; trip++) {
-    const bool ask = q.dyn && trip + 2 >= kStatic;
-    if (q.dyn && trip >= kStatic) run(std::integral_constant<int, Ud>{}, base, ask);
-    else run(std::integral_constant<int, U>{}, base, ask);
-    base = base1;
-    if (ask) {
-      const int64_t c = q.taken();  // chunk index within the dynamic region (q.nch: none)
-      base1 = c < q.nch ? first + c * 16 * Ud : n;
-    } else {
-      base1 = (int64_t)(trip + 2) * W * 16 * U + wave * 16 * U;
-      if (q.dyn && trip + 2 >= kStatic) base1 = n;  // unreachable: ask covers these trips
-    }
+        body(a, b, site0, valid, w);
+      }
   }
   q.finish();
   block_ticket_sum(acc, ws, scaler_sum);
@@ -286,16 +282,14 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((plf_dna_f64_pair_kernel<2, true, 1, true>), dim3(grid), dim3(kBlock), 0, s, t.x1, t.x2,
                        t.x3, EV, L, R, w, t.sc, n, ws, t.sum);
   };
-#define QV(P, S, UD)                                                                                     \
+#define QV(P)                                                                                            \
   [](const Set &t, int64_t n, const double *EV, const double *L, const double *R, const int32_t *w,     \
      unsigned long long *ws, int grid, hipStream_t s) {                                                 \
-    hipLaunchKernelGGL((pair_queue_kernel<2, P, S, UD>), dim3(grid), dim3(kBlock), 0, s, t.x1, t.x2, t.x3, EV, \
-                       L, R, w, t.sc, n, ws, t.sum);                                                     \
+    hipLaunchKernelGGL((pair_queue_kernel<2, P>), dim3(grid), dim3(kBlock), 0, s, t.x1, t.x2, t.x3, EV, L, R, \
+                       w, t.sc, n, ws, t.sum);                                                           \
   }
-  std::vector<Var> vars = {{"product", prod},
-                           {"q p8 s2 u2", QV(8, 2, 2)},  {"q p8 s4 u2", QV(8, 4, 2)}, {"q p8 s6 u2", QV(8, 6, 2)},
-                           {"q p32 s4 u2", QV(32, 4, 2)}, {"q p8 s6 u1", QV(8, 6, 1)}, {"q p32 s6 u1", QV(32, 6, 1)},
-                           {"q p32 s7 u1", QV(32, 7, 1)}};
+  std::vector<Var> vars = {{"product", prod}, {"same, no queue", QV(0)}, {"queue p1", QV(1)},
+                           {"queue p8", QV(8)}, {"queue p32", QV(32)}};
   for (int lg : logs) {
     const int64_t n = (int64_t)1 << lg;
     std::vector<Set> sets(kSets);
