@@ -261,8 +261,8 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&EV, 16 * 8));
   CK(hipMalloc(&L, 64 * 8));
   CK(hipMalloc(&R, 64 * 8));
-  CK(hipMalloc(&ws, 2 * kWsWords * 8 * 4));
-  CK(hipMemset(ws, 0, 2 * kWsWords * 8 * 4));
+  CK(hipMalloc(&ws, 16 * kWsWords * 8));
+  CK(hipMemset(ws, 0, 16 * kWsWords * 8));
   fill<<<1, 64>>>(EV, 16, 11, false);
   fill<<<1, 64>>>(L, 64, 12, false);
   fill<<<1, 64>>>(R, 64, 13, false);
@@ -289,7 +289,7 @@ int main(int argc, char **argv) {
                        w, t.sc, n, ws, t.sum);                                                           \
   }
   std::vector<Var> vars = {{"product", prod}, {"same, no queue", QV(0)}, {"queue p1", QV(1)},
-                           {"queue p8", QV(8)}, {"queue p32", QV(32)}};
+                           {"queue p8", QV(8)}, {"queue p32", QV(32)}, {"queue p256", QV(256)}};
   for (int lg : logs) {
     const int64_t n = (int64_t)1 << lg;
     std::vector<Set> sets(kSets);
@@ -347,8 +347,8 @@ int main(int argc, char **argv) {
         }
       }
     }
-    std::vector<unsigned long long> wsh(2 * kWsWords);
-    CK(hipMemcpy(wsh.data(), ws, 2 * kWsWords * 8, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> wsh(16 * kWsWords);
+    CK(hipMemcpy(wsh.data(), ws, 16 * kWsWords * 8, hipMemcpyDeviceToHost));
     bool zero = std::all_of(wsh.begin(), wsh.end(), [](unsigned long long x) { return x == 0; });
     printf("2^%d sites: bit-identical %s, workspace zero after runs: %s, product sum %lld\n", lg,
            all_ok ? "yes" : "NO", zero ? "yes" : "NO", (long long)refsum);
