@@ -541,7 +541,10 @@ hipError_t launch_plf_prot_batch(int dtype, bool fma, const NodeDescH *nodes, in
     case 2: return launch_prot_batch_t<1, false>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
     case 3: return launch_prot_batch_t<1, true>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
     case 4: return launch_prot_batch_t<2, false>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
-    default: return launch_prot_batch_t<2, true>(dtype, fma, b, count, EV, wgt, n, ws, max_blocks, s, tipvec);
+    // tips == 2 runs only as the combination tables of tip/tip nodes (plfx_api
+    // batch_impl), which carry no sum: a tip/tip node's sum comes from the
+    // gather, so the summing tip/tip forms are not built
+    default: return hipErrorInvalidValue;
   }
 }
 
