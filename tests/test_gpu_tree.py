@@ -642,7 +642,8 @@ def _random_tree_ops(rng, ntips, recycle):
 def test_random_trees_match_oracle(ctx, oracle, seed, dtype):
     """Random topologies (with and without slot recycling) and a random mix of
     coded / dense tips: the scheduled (levels + fused pairs) traversal equals
-    the oracle's sequential one bit for bit, scaler sums included."""
+    the oracle's sequential one bit for bit, scaler sums included; the oracle's
+    equals the reference's plf() composed per op (oracle/_ref, shipped)."""
     import torch
 
     rng = np.random.default_rng(seed)
@@ -657,7 +658,13 @@ def test_random_trees_match_oracle(ctx, oracle, seed, dtype):
     wgt = rng.integers(1, 4, n).astype(np.int32)
     host = [oracle.expand_tips(codes[t], dtype) if coded[t] else dense[t].copy() for t in range(ntips)]
     host += [np.zeros(16 * n, dtype) for _ in range(nslots - ntips)]
+    ref = [h.copy() for h in host]
     esums, escal = oracle.traverse(4, 4, ops, host, pm, EV, n, wgt, want_scalers=True)
+    if oracle.ref_available(dtype):  # and the reference's own plf(), one call per op
+        rsums, _ = oracle.ref_traverse(ops, ref, pm, EV, n, wgt)
+        assert np.array_equal(rsums, esums)
+        for s in range(ntips, nslots):
+            assert np.array_equal(bits(ref[s]), bits(host[s])), s
     tt = torch.float64 if dtype == np.float64 else torch.float32
     clv = [None if coded[t] else dev(dense[t]) for t in range(ntips)]
     clv += [torch.zeros(16 * n, dtype=tt, device="cuda") for _ in range(nslots - ntips)]

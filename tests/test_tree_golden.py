@@ -86,3 +86,53 @@ def test_ref_scaled_sites_bisection(oracle, dt):
         x2 = rng.random(16 * n).astype(dt)
         _, sc, _ = oracle.plf(x1, x2, EV, L, R, np.ones(n, np.int32))
         assert np.array_equal(oracle.ref_scaled_sites(f, x1, x2, EV, L, R, n), sc)
+
+
+def _random_ops(rng, ntips, recycle):
+    """Random topology by merging random pool members; recycle reuses consumed
+    inner slots (write-after-read / write-after-write order matters)."""
+    pool, free, nxt, ops = list(range(ntips)), [], ntips, []
+    while len(pool) > 1:
+        i, j = sorted(rng.choice(len(pool), 2, replace=False))
+        a, b = pool[j], pool[i]
+        pool.pop(j)
+        pool.pop(i)
+        if recycle and free:
+            p = free.pop(0)
+        else:
+            p, nxt = nxt, nxt + 1
+        ops.append((p, a, b, len(ops)))
+        if recycle:
+            free += [c for c in (a, b) if c >= ntips]
+        pool.append(p)
+    return np.array(ops, np.int32), nxt
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_trees_oracle_equals_reference_composition(oracle, seed):
+    """Random topologies (2..40 taxa, slot recycling on odd seeds), ragged site
+    counts, dense / coded / mixed tips, f32 and f64: the oracle's traversal
+    (the checker of every GPU traversal test) equals the reference's plf()
+    called per op, byte for byte, scaler bytes and sums included."""
+    rng = np.random.default_rng(1000 + seed)
+    dt = np.float32 if seed % 3 == 0 else np.float64
+    if not oracle.ref_available(dt):
+        pytest.skip("oracle/_ref not built")
+    ntips = int(rng.integers(2, 41))
+    n = int(rng.integers(1, 300))
+    ops, nslots = _random_ops(rng, ntips, recycle=bool(seed % 2))
+    coded = rng.random(ntips) < (0.0, 0.5, 1.0)[seed % 3]
+    tips = [oracle.expand_tips(oracle.random_tip_codes(rng, n, 0.2), dt) if coded[t]
+            else rng.random(16 * n).astype(dt) for t in range(ntips)]
+    pm = (rng.random(ops.shape[0] * 128) * 0.3).astype(dt)
+    EV = (rng.random(16) * 0.3).astype(dt)
+    wgt = rng.integers(-2, 5, n).astype(np.int32)
+    a = [t.copy() for t in tips] + [np.zeros(16 * n, dt) for _ in range(nslots - ntips)]
+    b = [x.copy() for x in a]
+    s1, sc1 = oracle.traverse(4, 4, ops, a, pm, EV, n, wgt, want_scalers=True)
+    s2, sc2 = oracle.ref_traverse(ops, b, pm, EV, n, wgt, want_scalers=True)
+    for s in range(nslots):
+        assert np.array_equal(a[s].view(np.uint8), b[s].view(np.uint8)), s
+    assert np.array_equal(s1, s2)
+    for j in range(ops.shape[0]):
+        assert np.array_equal(sc1[j], sc2[j]), j
