@@ -364,6 +364,51 @@ def tree_case_digest(case):
     return h.hexdigest()
 
 
+def embed_dna_clv(x, S=20):
+    """A 4-state CLV [site][cat][4] placed in states 0..3 of an S-state CLV
+    [site][cat][S], every other value +0.0.  With P and EV embedded the same way
+    (embed_dna_mats), plf()'s S-state loop adds only exact +0.0 terms to the
+    4-state chains (x*0 = +0, v + +0 = v for every chain value plf() can hold)
+    and tests 4*(S-4) extra +0 values (< 2^-32) in the scale test, so its
+    states 0..3 reproduce the 4-state plf() bit for bit and states 4.. stay +0:
+    the reference's own plf() pins the S-state kernels on this sub-space."""
+    x = np.asarray(x)
+    n = x.size // 16
+    out = np.zeros((n, 4, S), x.dtype)
+    out[:, :, :4] = x.reshape(n, 4, 4)
+    return out.reshape(-1)
+
+
+def embed_dna_mats(m, S=20):
+    """4x4 matrices (DNA P pairs [cat][k][l] of 64 values, or EV of 16) -> S x S
+    with the 4x4 block top-left, zeros elsewhere (same count of matrices)."""
+    m = np.asarray(m)
+    k = m.size // 16
+    out = np.zeros((k, S, S), m.dtype)
+    out[:, :4, :4] = m.reshape(k, 4, 4)
+    return out.reshape(-1)
+
+
+def extract_dna_clv(xp, S=20):
+    """Inverse of embed_dna_clv: (states 0..3 as a 4-state CLV, whether every
+    other value is exactly +0.0)."""
+    xp = np.asarray(xp)
+    n = xp.size // (4 * S)
+    v = xp.reshape(n, 4, S)
+    rest = v[:, :, 4:]
+    return np.ascontiguousarray(v[:, :, :4]).reshape(-1), bool(not rest.view(np.uint8).any())
+
+
+def embedded_dna_tipvec(dtype, S=20):
+    """Protein tip-vector table (PROT_CODES x S) whose rows 0..15 are the DNA
+    state-code indicators (bit l of the code in state l, states 4.. zero): a
+    DNA code c & 15 used as a protein code reads exactly the embedded DNA tip."""
+    tv = np.zeros((PROT_CODES, S), dtype)
+    for c in range(16):
+        tv[c, :4] = [(c >> l) & 1 for l in range(4)]
+    return tv.reshape(-1)
+
+
 def clv_digest(a):
     import hashlib
 

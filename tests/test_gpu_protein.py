@@ -1,8 +1,11 @@
 """GPU tests of the S=20 (protein) kernel, BASELINE configs[4].  The reference
 is DNA-only: parity is against the oracle's generic restatement of
 the same loop (plfo_plf_gen_*), which reproduces the pinned DNA plf()
-bit-for-bit at S=4.  EXACT mode: bit-identical; FMA mode: within 1e-12
-relative (one rounding per fused term), identical scaler decisions."""
+bit-for-bit at S=4, and -- on the embedded 4-state sub-space (a DNA problem in
+states 0..3 of 20, tests/test_protein_embedded.py) -- against the reference's
+own plf(): test_protein_embedded_dna_*.  EXACT mode: bit-identical; FMA mode:
+within 1e-12 relative (one rounding per fused term), identical scaler
+decisions."""
 import numpy as np
 import pytest
 
@@ -773,3 +776,67 @@ def test_protein_coded_tree_table_children(ctx, oracle, dtype, fma, with_sum, nt
         assert np.array_equal(scal[j].cpu().numpy(), escal[j]), j
     if with_sum:
         assert sums.cpu().tolist() == einc
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("n", [1, 4099, 65537])
+def test_protein_embedded_dna_node_equals_reference(ctx, oracle, dtype, n):
+    """The protein exact kernels pinned by the reference itself on the embedded
+    4-state sub-space (oracle.embed_dna_*, tests/test_protein_embedded.py): a
+    DNA node in states 0..3 of 20 gives states 0..3 equal to the reference's
+    plf() (oracle/_ref: the f32 build / the double instantiation) bit for bit,
+    states 4..19 exactly +0.0, and the reference's scaler bytes and sum."""
+    if not oracle.ref_available(dtype):
+        pytest.skip("oracle/_ref not shipped")
+    d = oracle.gen_hostmem(n, dtype, 500 + n)
+    w = (np.arange(n, dtype=np.int32) % 5) - 1
+    f = oracle._ref_call(dtype)
+    r3 = np.empty(16 * n, dtype)
+    rinc = f(d["x1"], d["x2"], r3, d["EV"], n, d["left"], d["right"], w)
+    rsc = oracle.ref_scaled_sites(f, d["x1"], d["x2"], d["EV"], d["left"], d["right"], n)
+    x3, sc, s = run(ctx, oracle.embed_dna_clv(d["x1"]), oracle.embed_dna_clv(d["x2"]),
+                    oracle.embed_dna_mats(d["EV"]), oracle.embed_dna_mats(d["left"]),
+                    oracle.embed_dna_mats(d["right"]), w, n, fma=False)
+    got, rest_zero = oracle.extract_dna_clv(x3)
+    assert rest_zero
+    assert np.array_equal(bits(got), bits(r3))
+    assert np.array_equal(sc, rsc) and s == rinc
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("mode", ["dense", "coded", "mixed"])
+def test_protein_embedded_dna_tree64_equals_reference_golden(ctx, oracle, dtype, mode):
+    """configs[2]'s 64-taxon tree as a protein traversal (exact mode) on the
+    embedded sub-space reproduces tests/golden/tree64.npz -- the reference's
+    plf() composed per inner node -- byte for byte: batched level launches,
+    and with coded leaves (DNA codes as protein codes into the embedded tip
+    table) the tip/tip combination tables, their gather, tip/inner nodes and
+    the parents that stage children from the tables."""
+    import torch
+
+    g = np.load(__import__("conftest").GOLDEN / "tree64.npz", allow_pickle=False)
+    k = f"{'f32' if dtype == np.float32 else 'f64'}_{mode}"
+    c = oracle.tree_golden_case(dtype, mode, int(g["n"]), int(g["seed"]))
+    assert oracle.tree_case_digest(c) == str(g[f"{k}_inputs_sha256"])
+    n, ops = c["n"], c["ops"]
+    nops, nslots = ops.shape[0], 64 + ops.shape[0]
+    codes = [None if cd is None else (cd & 15).astype(np.uint8) for cd in c["codes"]]
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    clv = [None if cd is not None else dev(oracle.embed_dna_clv(t)) for t, cd in zip(c["tips"], codes)]
+    clv += [torch.zeros(V * n, dtype=tt, device="cuda") for _ in range(nops)]
+    tips = [None if cd is None else dev(cd) for cd in codes] + [None] * nops
+    sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
+    scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+    ctx.traverse(ops, clv, dev(oracle.embed_dna_mats(c["pm"])), dev(oracle.embed_dna_mats(c["EV"])), n,
+                 dev(c["wgt"]), scal, sums, tips=tips, tipvec=dev(oracle.embedded_dna_tipvec(dtype)),
+                 states=S, fma=False)
+    torch.cuda.synchronize()
+    digests = []
+    for p in ops[:, 0]:
+        x, rest_zero = oracle.extract_dna_clv(clv[int(p)].cpu().numpy())
+        assert rest_zero, int(p)
+        digests.append(oracle.clv_digest(x))
+    bad = [j for j, (a, b) in enumerate(zip(digests, g[f"{k}_x3_sha256"])) if a != str(b)]
+    assert not bad, f"parent CLVs of ops {bad[:8]} differ from the reference composition"
+    assert np.array_equal(sums.cpu().numpy(), g[f"{k}_sums"])
+    assert np.array_equal(np.stack([s_.cpu().numpy() for s_ in scal]), g[f"{k}_scaler"])
