@@ -32,9 +32,12 @@ Contents
 Parity status: the float path is pinned (reference binary + AIE goldens +
 committed fixtures); double by the reference source's double instantiation;
 4-state tree sweeps (dense and state-coded tips) by the composition of the
-reference's plf() calls (tests/golden/tree64.npz, ref_traverse).  Protein
-(S=20) and the root lnL are extensions the reference does not have: parity
-unpinned beyond being the same loop as the pinned path.
+reference's plf() calls (tests/golden/tree64.npz, ref_traverse); the S-state
+(protein) loop on the embedded 4-state sub-space (embed_dna_*: a DNA problem
+in states 0..3 of 20 must reproduce the reference's plf() bit for bit).  The
+protein loop beyond that sub-space (chains longer than 4 terms, FMA mode) and
+the root lnL are extensions the reference does not have: parity unpinned
+beyond being the same loop as the pinned path.
 """
 from __future__ import annotations
 
