@@ -328,7 +328,7 @@ TREE_GOLDEN_N = 257       # ragged: not a multiple of any kernel's trip
 TREE_GOLDEN_SEED = 6464
 
 
-TREE_GOLDEN_TIPS = ("dense", "coded", "mixed")
+TREE_GOLDEN_TIPS = ("dense", "coded", "mixed", "tipvec")
 
 
 def tree_golden_case(dtype, coded, n=TREE_GOLDEN_N, seed=TREE_GOLDEN_SEED):
@@ -337,21 +337,24 @@ def tree_golden_case(dtype, coded, n=TREE_GOLDEN_N, seed=TREE_GOLDEN_SEED):
     P and EV scaled by 0.25 so the deep levels underflow and the
     scaler path runs.  coded: False / "dense" (every tip a dense CLV), True /
     "coded" (every tip DNA state codes, 20 % ambiguous, expanded to the dense
-    CLV plf() reads) or "mixed" (tips 4j+1 and 4j+2 coded, the rest dense:
-    tip/tip, tip/inner and inner/inner nodes).  Returns dict(ops, tips (dense
-    CLVs), codes (per tip: codes or None), pm, EV, wgt, n)."""
+    CLV plf() reads), "mixed" (tips 4j+1 and 4j+2 coded, the rest dense:
+    tip/tip, tip/inner and inner/inner nodes) or "tipvec" (every tip coded,
+    expanded through a caller tip-vector table of signed values, as eigen-
+    coordinate tips are).  Returns dict(ops, tips (dense CLVs), codes (per tip:
+    codes or None), tipvec (16 x 4 or None), pm, EV, wgt, n)."""
     mode = {False: "dense", True: "coded"}.get(coded, coded)
     dt = np.dtype(dtype)
     rng = np.random.default_rng(seed + TREE_GOLDEN_TIPS.index(mode))
     ops = balanced_tree_ops(64)
-    is_coded = [mode == "coded" or (mode == "mixed" and t % 4 in (1, 2)) for t in range(64)]
+    is_coded = [mode in ("coded", "tipvec") or (mode == "mixed" and t % 4 in (1, 2)) for t in range(64)]
     codes = [random_tip_codes(rng, n, 0.2) if c else None for c in is_coded]
     dense = [None if c else rng.random(16 * n).astype(dt) for c in is_coded]
-    tips = [expand_tips(c, dt) if c is not None else d for c, d in zip(codes, dense)]
+    tv = (rng.random(64) - 0.25).astype(dt) if mode == "tipvec" else None
+    tips = [expand_tips(c, dt, tipvec=tv) if c is not None else d for c, d in zip(codes, dense)]
     pm = (rng.random(ops.shape[0] * 128) * 0.25).astype(dt)
     EV = (rng.random(16) * 0.25).astype(dt)
     wgt = rng.integers(1, 5, n).astype(np.int32)
-    return dict(ops=ops, tips=tips, codes=codes, pm=pm, EV=EV, wgt=wgt, n=n)
+    return dict(ops=ops, tips=tips, codes=codes, tipvec=tv, pm=pm, EV=EV, wgt=wgt, n=n)
 
 
 def tree_case_digest(case):

@@ -196,7 +196,7 @@ def test_tree64_full_size_window(ctx, oracle):
 
 @pytest.mark.parametrize("fuse", ["3", "2", "1", "0"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-@pytest.mark.parametrize("mode", ["dense", "coded", "mixed"])
+@pytest.mark.parametrize("mode", ["dense", "coded", "mixed", "tipvec"])
 def test_tree64_reference_golden(oracle, dtype, mode, fuse, monkeypatch):
     """configs[2] pinned by the reference itself: the 64-taxon sweep under
     every schedule (PLFX_FUSE 3: one six-level pass; 2: three-level passes +
@@ -204,7 +204,8 @@ def test_tree64_reference_golden(oracle, dtype, mode, fuse, monkeypatch):
     tests/golden/tree64.npz -- the unmodified reference plf() called per inner
     node (oracle.ref_traverse) -- byte for byte: every parent CLV (sha256), the
     per-site scaler bytes and the weighted sums; dense, state-coded and mixed
-    tips (tip/tip, tip/inner and inner/inner nodes)."""
+    tips (tip/tip, tip/inner and inner/inner nodes), and coded tips through a
+    caller tip-vector table."""
     import plfx
     import torch
 
@@ -223,12 +224,13 @@ def test_tree64_reference_golden(oracle, dtype, mode, fuse, monkeypatch):
         tips = [None if cd is None else dev(cd) for cd in c["codes"]] + [None] * nops
         sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
         scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
-        ctx.traverse(ops, clv, dev(c["pm"]), dev(c["EV"]), n, dev(c["wgt"]), scal, sums, tips=tips)
+        ctx.traverse(ops, clv, dev(c["pm"]), dev(c["EV"]), n, dev(c["wgt"]), scal, sums, tips=tips,
+                     tipvec=None if c["tipvec"] is None else dev(c["tipvec"]))
         torch.cuda.synchronize()
         sched = ctx.last_schedule()
     finally:
         ctx.close()
-    if fuse == "3" and mode != "mixed":
+    if fuse == "3" and mode in ("dense", "coded"):
         assert sched["deep6"] == 1, sched
     got = [oracle.clv_digest(clv[int(p)].cpu().numpy()) for p in ops[:, 0]]
     bad = [j for j, (a, b) in enumerate(zip(got, g[f"{k}_x3_sha256"])) if a != str(b)]

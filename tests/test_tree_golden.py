@@ -7,7 +7,7 @@ holds that composition as produced by the unmodified reference build
 (oracle.ref_traverse over oracle/_ref; generator tests/golden/make_golden.py
 make_tree64): per op the sha256 of the parent CLV, the per-site scaler bytes,
 the weighted scaler sum, and the root CLV -- f32 and f64 (the reference source
-with float spelled double), dense, state-coded and mixed tips.
+with float spelled double), dense, state-coded, mixed and tip-vector tips.
 
 Here the oracle's own sequential traversal (plf_oracle.c plfo_traverse, the
 checker of every GPU traversal test) must reproduce those bytes, and the live
@@ -19,7 +19,7 @@ import pytest
 
 from conftest import golden
 
-CASES = [(dt, mode) for dt in (np.float32, np.float64) for mode in ("dense", "coded", "mixed")]
+CASES = [(dt, mode) for dt in (np.float32, np.float64) for mode in ("dense", "coded", "mixed", "tipvec")]
 
 
 def key(dt, mode):
