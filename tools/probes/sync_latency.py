@@ -29,12 +29,13 @@ def main():
     L = torch.rand(64, dtype=torch.float64, device=dev, generator=g)
     R = torch.rand(64, dtype=torch.float64, device=dev, generator=g)
     w = torch.ones(n, dtype=torch.int32, device=dev)
-    sets = []
+    sets, keep = [], []  # the launchers hold raw pointers: keep every tensor alive
     for _ in range(4):
         x1 = torch.rand(16 * n, dtype=torch.float64, device=dev, generator=g)
         x2 = torch.rand(16 * n, dtype=torch.float64, device=dev, generator=g)
         x3 = torch.empty_like(x1)
         s = torch.zeros(1, dtype=torch.int64, device=dev)
+        keep += [x1, x2, x3, s]
         sets.append(ctx.bind_plf_dev(x1, x2, x3, EV, L, R, w, None, s))
     stream = torch.cuda.Stream(dev)
     for k in ks:
@@ -67,7 +68,9 @@ def main():
             v = sorted(v[2:])
             print(f"K={k:4d} {mode:8s}: wall - events = median {v[len(v) // 2]:7.1f} us "
                   f"(min {v[0]:7.1f}, max {v[-1]:7.1f})", flush=True)
+    torch.cuda.synchronize(dev)
     ctx.close()
+    del keep
 
 
 if __name__ == "__main__":
