@@ -265,8 +265,10 @@ class Context:
                      n=None):
         """Validate once and return a launcher ``run(stream=None)`` that issues
         the same fused PLF call with no per-call Python checks (for launch-rate
-        bound loops: a 1M-site f64 call is ~67 us of GPU time).  The tensors
-        must stay alive and unchanged in shape while the launcher is used."""
+        bound loops: a 1M-site f64 call is ~67 us of GPU time).  The launcher
+        holds references to the tensors, so their memory stays allocated while
+        it lives (a graph captured through it, too, needs it alive); the
+        tensors must keep their shape and device."""
         import torch
 
         self.plf_dev(x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, n=n,
@@ -277,11 +279,12 @@ class Context:
         args = (self.h, p(x1), p(x2), p(x3), p(EV), C.c_int64(n), p(left), p(right), p(wgt),
                 p(scaler), p(scaler_sum))
         check = self._check
-        dev = self.device
+        held = (x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum)  # raw pointers in args
 
         def run(stream=None):
             check(fn(*args, _stream_handle(stream, self.device)))
 
+        run.tensors = held
         return run
 
     # -- (3) instance-buffer contract --------------------------------------
@@ -391,8 +394,9 @@ class Context:
     def bind_plf_batch_dev(self, nodes, EV, n, wgt=None, states=4):
         """Validate once (as plf_batch_dev) and return a launcher
         ``run(stream=None)`` issuing the same batched call with a prebuilt
-        node array (graph capture / launch-rate bound loops).  The tensors must
-        stay alive and unchanged while the launcher is used."""
+        node array (graph capture / launch-rate bound loops).  The launcher
+        holds references to every node's tensors, EV and wgt, so their memory
+        stays allocated while it lives."""
         import torch
 
         if not nodes:
@@ -410,6 +414,7 @@ class Context:
         def run(stream=None):
             check(fn(h, *args, _stream_handle(stream, dev)))
 
+        run.tensors = ([dict(nd) for nd in nodes], EV, wgt)  # raw pointers in arr / args
         return run
 
     def traverse(self, ops, clv, pmats, EV, n, wgt=None, scalers=None, scaler_sums=None,

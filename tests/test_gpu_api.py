@@ -689,3 +689,40 @@ def ctypes_stream_per_thread():
     import plfx
 
     return ctypes.c_void_p(plfx.STREAM_PER_THREAD)
+
+
+def test_bound_launcher_keeps_its_tensors_alive(ctx, oracle):
+    """bind_plf_dev / bind_plf_batch_dev launchers hold their tensors: with the
+    caller's names gone and torch's cache emptied (what torch.cuda.graph does at
+    capture start), the memory stays allocated -- checked BEFORE any launch --
+    and the launcher still computes the right result."""
+    import gc
+
+    import torch
+
+    n = 4099
+    d = oracle.gen_hostmem(n, np.float64, 91)
+    e3, _, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+    torch.cuda.synchronize()
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    x3 = torch.empty_like(t["x1"])
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    run = ctx.bind_plf_dev(t["x1"], t["x2"], x3, t["EV"], t["left"], t["right"], t["wgt"], None, s)
+    nodes = [dict(x1=t["x1"], x2=t["x2"], x3=torch.empty_like(t["x1"]), left=t["left"], right=t["right"],
+                  scaler=None, scaler_sum=torch.zeros(1, dtype=torch.int64, device="cuda"))]
+    runb = ctx.bind_plf_batch_dev(nodes, t["EV"], n, t["wgt"])
+    torch.cuda.synchronize()
+    gc.collect()  # earlier tests' garbage first, so the comparison below sees only ours
+    held = torch.cuda.memory_allocated()
+    del t, x3, s, nodes
+    gc.collect()
+    torch.cuda.empty_cache()
+    assert torch.cuda.memory_allocated() == held  # nothing of the launchers' was freed
+    s = run.tensors[8]
+    s.zero_()
+    run()
+    runb()
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(run.tensors[2].cpu().numpy()), bits(e3)) and int(s.item()) == einc
+    nb = runb.tensors[0][0]
+    assert np.array_equal(bits(nb["x3"].cpu().numpy()), bits(e3)) and int(nb["scaler_sum"].item()) == einc
