@@ -282,6 +282,8 @@ class Context:
         held = (x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum)  # raw pointers in args
 
         def run(stream=None):
+            if self.h is None:  # args carry the handle: a closed context's would dangle
+                raise PlfxError(ERR_INVALID, "launcher used after its context was closed")
             check(fn(*args, _stream_handle(stream, self.device)))
 
         run.tensors = held
@@ -411,7 +413,11 @@ class Context:
         args = (F32 if EV.dtype == torch.float32 else F64, states, arr, len(nodes),
                 C.c_void_p(EV.data_ptr()), int(n), C.c_void_p(ptr(wgt)))
 
+        ctx = self
+
         def run(stream=None):
+            if ctx.h is None:  # h would dangle
+                raise PlfxError(ERR_INVALID, "launcher used after its context was closed")
             check(fn(h, *args, _stream_handle(stream, dev)))
 
         run.tensors = ([dict(nd) for nd in nodes], EV, wgt)  # raw pointers in arr / args

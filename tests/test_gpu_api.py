@@ -726,3 +726,26 @@ def test_bound_launcher_keeps_its_tensors_alive(ctx, oracle):
     assert np.array_equal(bits(run.tensors[2].cpu().numpy()), bits(e3)) and int(s.item()) == einc
     nb = runb.tensors[0][0]
     assert np.array_equal(bits(nb["x3"].cpu().numpy()), bits(e3)) and int(nb["scaler_sum"].item()) == einc
+
+
+def test_bound_launcher_after_close_raises(oracle):
+    """A launcher carries its context's handle: once the context is closed,
+    using it raises PlfxError instead of passing a freed handle to the C ABI."""
+    import plfx
+    import torch
+
+    n = 257
+    d = oracle.gen_hostmem(n, np.float64, 92)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    c = plfx.Context(0)
+    run = c.bind_plf_dev(t["x1"], t["x2"], torch.empty_like(t["x1"]), t["EV"], t["left"], t["right"],
+                         t["wgt"])
+    nodes = [dict(x1=t["x1"], x2=t["x2"], x3=torch.empty_like(t["x1"]), left=t["left"], right=t["right"])]
+    runb = c.bind_plf_batch_dev(nodes, t["EV"], n, t["wgt"])
+    run()
+    runb()
+    torch.cuda.synchronize()
+    c.close()
+    for r in (run, runb):
+        with pytest.raises(plfx.PlfxError):
+            r()
