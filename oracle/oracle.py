@@ -165,7 +165,8 @@ _native = None
 
 def ref_lib(opt: str = "O0"):
     """The reference plf() itself (oracle/_ref), or None if it was not built.
-    opt: "O0" (its own host flags), "O3", "O3v4" (-O3 -march=x86-64-v4)."""
+    opt: "O0" (its own host flags), "O3", "O3v4" (-O3 -march=x86-64-v4), "fma"
+    (-O3 -march=x86-64-v3 -ffp-contract=fast: every multiply-add fused)."""
     if opt not in _refs:
         p = {"O0": REF_O0, "O3": REF_O3}.get(opt, ORACLE_DIR / "_ref" / f"libplfref_{opt}.so")
         if not p.exists():
@@ -491,7 +492,8 @@ def ref_plf(x1, x2, EV, left, right, wgt, opt="O0"):
 
 def _ref_call(dtype, opt="O0"):
     """The reference plf() entry of one dtype over raw contiguous arrays:
-    f(x1, x2, x3, EV, n, left, right, wgt) -> scalerIncrement, or None."""
+    f(x1, x2, x3, EV, n, left, right, wgt) -> scalerIncrement, or None.
+    opt "fma": the build with every multiply-add contracted (oracle/Makefile)."""
     if np.dtype(dtype) == np.float32:
         L = ref_lib(opt)
         return None if L is None else L.plfref_plf

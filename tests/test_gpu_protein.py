@@ -840,3 +840,64 @@ def test_protein_embedded_dna_tree64_equals_reference_golden(ctx, oracle, dtype,
     assert not bad, f"parent CLVs of ops {bad[:8]} differ from the reference composition"
     assert np.array_equal(sums.cpu().numpy(), g[f"{k}_sums"])
     assert np.array_equal(np.stack([s_.cpu().numpy() for s_ in scal]), g[f"{k}_scaler"])
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("n", [1, 4099, 65537])
+def test_protein_fma_embedded_dna_node_equals_contracted_reference(ctx, oracle, dtype, n):
+    """FMA mode (the configs[4] default: f64 16x16x4 + 4x4x4 matrix cores, f32
+    16x16x4 + 4x4x1) on the embedded 4-state sub-space equals the reference
+    source compiled with FMA contraction (oracle/_ref/libplfref{,_f64}_fma.so,
+    every multiply-add of plf() fused in plf()'s order) bit for bit."""
+    if not oracle.ref_available(dtype, "fma"):
+        pytest.skip("oracle/_ref not shipped")
+    d = oracle.gen_hostmem(n, dtype, 700 + n)
+    w = (np.arange(n, dtype=np.int32) % 5) - 1
+    f = oracle._ref_call(dtype, "fma")
+    r3 = np.empty(16 * n, dtype)
+    rinc = f(d["x1"], d["x2"], r3, d["EV"], n, d["left"], d["right"], w)
+    rsc = oracle.ref_scaled_sites(f, d["x1"], d["x2"], d["EV"], d["left"], d["right"], n)
+    x3, sc, s = run(ctx, oracle.embed_dna_clv(d["x1"]), oracle.embed_dna_clv(d["x2"]),
+                    oracle.embed_dna_mats(d["EV"]), oracle.embed_dna_mats(d["left"]),
+                    oracle.embed_dna_mats(d["right"]), w, n, fma=True)
+    got, rest_zero = oracle.extract_dna_clv(x3)
+    assert rest_zero
+    assert np.array_equal(bits(got), bits(r3))
+    assert np.array_equal(sc, rsc) and s == rinc
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("mode", ["dense", "coded", "mixed"])
+def test_protein_fma_embedded_tree64_equals_contracted_reference(ctx, oracle, dtype, mode):
+    """The 64-taxon tree as an FMA-mode protein traversal on the embedded
+    sub-space equals the FMA-contracted reference's plf() composed per inner
+    node (oracle.ref_traverse over the fma build, live): every parent CLV,
+    scaler byte and sum -- batched FMA levels, tip/tip tables and their
+    gather, tip/inner nodes, table children."""
+    import torch
+
+    if not oracle.ref_available(dtype, "fma"):
+        pytest.skip("oracle/_ref not shipped")
+    g = np.load(__import__("conftest").GOLDEN / "tree64.npz", allow_pickle=False)
+    c = oracle.tree_golden_case(dtype, mode, int(g["n"]), int(g["seed"]))
+    n, ops = c["n"], c["ops"]
+    nops = ops.shape[0]
+    ref = [t.copy() for t in c["tips"]] + [np.zeros(16 * n, dtype) for _ in range(nops)]
+    rsums, rscal = oracle.ref_traverse(ops, ref, c["pm"], c["EV"], n, c["wgt"], want_scalers=True, opt="fma")
+    codes = [None if cd is None else (cd & 15).astype(np.uint8) for cd in c["codes"]]
+    tt = torch.float64 if dtype == np.float64 else torch.float32
+    clv = [None if cd is not None else dev(oracle.embed_dna_clv(t)) for t, cd in zip(c["tips"], codes)]
+    clv += [torch.zeros(V * n, dtype=tt, device="cuda") for _ in range(nops)]
+    tips = [None if cd is None else dev(cd) for cd in codes] + [None] * nops
+    sums = torch.full((nops,), -7, dtype=torch.int64, device="cuda")
+    scal = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(nops)]
+    ctx.traverse(ops, clv, dev(oracle.embed_dna_mats(c["pm"])), dev(oracle.embed_dna_mats(c["EV"])), n,
+                 dev(c["wgt"]), scal, sums, tips=tips, tipvec=dev(oracle.embedded_dna_tipvec(dtype)),
+                 states=S, fma=True)
+    torch.cuda.synchronize()
+    for j, p in enumerate(ops[:, 0]):
+        x, rest_zero = oracle.extract_dna_clv(clv[int(p)].cpu().numpy())
+        assert rest_zero, j
+        assert np.array_equal(bits(x), bits(ref[int(p)])), j
+        assert np.array_equal(scal[j].cpu().numpy(), rscal[j]), j
+    assert np.array_equal(sums.cpu().numpy(), rsums)

@@ -76,3 +76,48 @@ def test_generic_traversal_on_embedded_tree_equals_golden(oracle, dt, mode):
     assert not bad, bad[:8]
     assert np.array_equal(sums, g[f"{k}_sums"])
     assert np.array_equal(np.stack(scal), g[f"{k}_scaler"])
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("seed", range(6))
+def test_fma_restatement_equals_contracted_reference(oracle, dt, seed):
+    """PLFX_FMA's semantics -- plf()'s loop with every multiply-add fused, in
+    plf()'s order -- pinned by the reference source itself compiled with FMA
+    contraction (oracle/_ref/libplfref{,_f64}_fma.so): the oracle's fma
+    restatement at S = 4 equals it bit for bit (and differs from the unfused
+    build, so the test sees the fusion)."""
+    if not oracle.ref_available(dt, "fma"):
+        pytest.skip("oracle/_ref not built")
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 4000))
+    d = oracle.gen_hostmem(n, dt, 300 + seed)
+    x1 = d["x1"] if seed % 2 else ((rng.random(16 * n) - 0.5) * 1e-9).astype(dt)  # signed, scaling
+    w = rng.integers(-3, 5, n).astype(np.int32)
+    f = oracle._ref_call(dt, "fma")
+    r3 = np.empty(16 * n, dt)
+    rinc = f(x1, d["x2"], r3, d["EV"], n, d["left"], d["right"], w)
+    e3, esc, einc = oracle.plf_generic(4, 4, x1, d["x2"], d["EV"], d["left"], d["right"], w, fma=True)
+    assert np.array_equal(e3.view(np.uint8), r3.view(np.uint8)) and einc == rinc
+    assert np.array_equal(esc, oracle.ref_scaled_sites(f, x1, d["x2"], d["EV"], d["left"], d["right"], n))
+    u3, _, _ = oracle.plf(x1, d["x2"], d["EV"], d["left"], d["right"], w)
+    assert not np.array_equal(u3.view(np.uint8), r3.view(np.uint8))
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_generic_fma_loop_on_embedded_dna_equals_contracted_reference(oracle, dt):
+    """The S = 20 fma restatement (the checker of the protein FMA kernels) on
+    the embedded sub-space equals the FMA-contracted reference on the 4-state
+    problem: the extra terms are fma(0, 0, v) = v exactly."""
+    if not oracle.ref_available(dt, "fma"):
+        pytest.skip("oracle/_ref not built")
+    n = 2049
+    d = oracle.gen_hostmem(n, dt, 808)
+    w = (np.arange(n, dtype=np.int32) % 4)
+    f = oracle._ref_call(dt, "fma")
+    r3 = np.empty(16 * n, dt)
+    rinc = f(d["x1"], d["x2"], r3, d["EV"], n, d["left"], d["right"], w)
+    x3, sc, inc = oracle.plf_generic(S, 4, oracle.embed_dna_clv(d["x1"]), oracle.embed_dna_clv(d["x2"]),
+                                     oracle.embed_dna_mats(d["EV"]), oracle.embed_dna_mats(d["left"]),
+                                     oracle.embed_dna_mats(d["right"]), w, fma=True)
+    got, rest_zero = oracle.extract_dna_clv(x3)
+    assert rest_zero and np.array_equal(got.view(np.uint8), r3.view(np.uint8)) and inc == rinc
