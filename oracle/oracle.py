@@ -34,10 +34,12 @@ committed fixtures); double by the reference source's double instantiation;
 4-state tree sweeps (dense and state-coded tips) by the composition of the
 reference's plf() calls (tests/golden/tree64.npz, ref_traverse); the S-state
 (protein) loop on the embedded 4-state sub-space (embed_dna_*: a DNA problem
-in states 0..3 of 20 must reproduce the reference's plf() bit for bit).  The
-protein loop beyond that sub-space (chains longer than 4 terms, FMA mode) and
-the root lnL are extensions the reference does not have: parity unpinned
-beyond being the same loop as the pinned path.
+in states 0..3 of 20 must reproduce the reference's plf() bit for bit), and
+the fused-multiply-add form (PLFX_FMA) by the reference source compiled with
+FMA contraction (oracle/_ref/libplfref{,_f64}_fma.so).  The protein loop
+beyond that sub-space (chains longer than 4 terms) and the root lnL are
+extensions the reference does not have: parity unpinned beyond being the same
+loop as the pinned path.
 """
 from __future__ import annotations
 
