@@ -398,6 +398,34 @@ def embed_dna_mats(m, S=20):
     return out.reshape(-1)
 
 
+def embed_clv_blocks(xs, S=20):
+    """CLVs of len(xs) <= S/4 4-state problems in states 4b..4b+3, rest +0.0."""
+    n = xs[0].size // 16
+    out = np.zeros((n, 4, S), xs[0].dtype)
+    for b, x in enumerate(xs):
+        out[:, :, 4 * b:4 * b + 4] = np.asarray(x).reshape(n, 4, 4)
+    return out.reshape(-1)
+
+
+def embed_mat_blocks(ms, S=20):
+    """Matrices (P pairs of 64 or EV of 16 values each) of len(ms) problems as
+    the diagonal 4x4 blocks of S x S matrices, zeros elsewhere."""
+    k = np.asarray(ms[0]).size // 16
+    out = np.zeros((k, S, S), np.asarray(ms[0]).dtype)
+    for b, m in enumerate(ms):
+        out[:, 4 * b:4 * b + 4, 4 * b:4 * b + 4] = np.asarray(m).reshape(k, 4, 4)
+    return out.reshape(-1)
+
+
+def extract_clv_blocks(xp, nblocks, S=20):
+    """(the nblocks 4-state CLVs, whether every state past them is +0.0)."""
+    xp = np.asarray(xp)
+    n = xp.size // (4 * S)
+    v = xp.reshape(n, 4, S)
+    outs = [np.ascontiguousarray(v[:, :, 4 * b:4 * b + 4]).reshape(-1) for b in range(nblocks)]
+    return outs, bool(not v[:, :, 4 * nblocks:].view(np.uint8).any())
+
+
 def extract_dna_clv(xp, S=20):
     """Inverse of embed_dna_clv: (states 0..3 as a 4-state CLV, whether every
     other value is exactly +0.0)."""

@@ -901,3 +901,39 @@ def test_protein_fma_embedded_tree64_equals_contracted_reference(ctx, oracle, dt
         assert np.array_equal(bits(x), bits(ref[int(p)])), j
         assert np.array_equal(scal[j].cpu().numpy(), rscal[j]), j
     assert np.array_equal(sums.cpu().numpy(), rsums)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("n", [4099, 65537])
+def test_protein_five_dna_blocks_equal_reference(ctx, oracle, dtype, fma, n):
+    """Five 4-state problems side by side in one protein node (states
+    4b..4b+3, block-diagonal P and EV; oracle.embed_*_blocks) reach every state
+    position of the protein kernels -- rows 16..19 go through the 4x4x4 (f64)
+    / 4x4x1 (f32) matrix-core forms in FMA mode -- and each block equals its
+    own reference plf(): the reference build in exact mode, the build with
+    FMA contraction in FMA mode; scaler bytes and sum as the reference's (the
+    blocks share the host_mem scaling pattern)."""
+    opt = "fma" if fma else "O0"
+    if not oracle.ref_available(dtype, opt):
+        pytest.skip("oracle/_ref not shipped")
+    ps = [oracle.gen_hostmem(n, dtype, 1200 + 7 * b + n % 97) for b in range(5)]
+    w = (np.arange(n, dtype=np.int32) % 4) - 1
+    f = oracle._ref_call(dtype, opt)
+    refs, incs = [], []
+    for d in ps:
+        r3 = np.empty(16 * n, dtype)
+        incs.append(f(d["x1"], d["x2"], r3, d["EV"], n, d["left"], d["right"], w))
+        refs.append(r3)
+    rsc = oracle.ref_scaled_sites(f, ps[0]["x1"], ps[0]["x2"], ps[0]["EV"], ps[0]["left"], ps[0]["right"], n)
+    x3, sc, s = run(ctx, oracle.embed_clv_blocks([d["x1"] for d in ps]),
+                    oracle.embed_clv_blocks([d["x2"] for d in ps]),
+                    oracle.embed_mat_blocks([d["EV"] for d in ps]),
+                    oracle.embed_mat_blocks([d["left"] for d in ps]),
+                    oracle.embed_mat_blocks([d["right"] for d in ps]), w, n, fma=fma)
+    outs, rest_zero = oracle.extract_clv_blocks(x3, 5)
+    assert rest_zero
+    for b in range(5):
+        assert np.array_equal(bits(outs[b]), bits(refs[b])), b
+    assert len(set(incs)) == 1 and s == incs[0]
+    assert np.array_equal(sc, rsc)

@@ -121,3 +121,35 @@ def test_generic_fma_loop_on_embedded_dna_equals_contracted_reference(oracle, dt
                                      oracle.embed_dna_mats(d["right"]), w, fma=True)
     got, rest_zero = oracle.extract_dna_clv(x3)
     assert rest_zero and np.array_equal(got.view(np.uint8), r3.view(np.uint8)) and inc == rinc
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("fma", [False, True])
+def test_generic_loop_on_five_dna_blocks_equals_reference(oracle, dt, fma):
+    """Five 4-state problems side by side (states 4b..4b+3, block-diagonal P
+    and EV) cover every state position of the 20-state loop: each block
+    equals its own reference plf() (exact: the reference build; FMA: the
+    contracted build), given the blocks share the scaling pattern (the
+    host_mem protocol scales every 4th site in each)."""
+    opt = "fma" if fma else "O0"
+    if not oracle.ref_available(dt, opt):
+        pytest.skip("oracle/_ref not built")
+    n = 1001
+    ps = [oracle.gen_hostmem(n, dt, 900 + b) for b in range(5)]
+    w = np.arange(n, dtype=np.int32) % 3
+    f = oracle._ref_call(dt, opt)
+    refs, incs = [], []
+    for d in ps:
+        r3 = np.empty(16 * n, dt)
+        incs.append(f(d["x1"], d["x2"], r3, d["EV"], n, d["left"], d["right"], w))
+        refs.append(r3)
+    x3, sc, inc = oracle.plf_generic(S, 4, oracle.embed_clv_blocks([d["x1"] for d in ps]),
+                                     oracle.embed_clv_blocks([d["x2"] for d in ps]),
+                                     oracle.embed_mat_blocks([d["EV"] for d in ps]),
+                                     oracle.embed_mat_blocks([d["left"] for d in ps]),
+                                     oracle.embed_mat_blocks([d["right"] for d in ps]), w, fma=fma)
+    outs, rest_zero = oracle.extract_clv_blocks(x3, 5)
+    assert rest_zero
+    for b in range(5):
+        assert np.array_equal(outs[b].view(np.uint8), refs[b].view(np.uint8)), b
+    assert len(set(incs)) == 1 and inc == incs[0]
