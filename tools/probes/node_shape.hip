@@ -142,6 +142,17 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((block_stream<V>), dim3(G * cus), dim3(256), 0, s, (const f64x2 *)t.x1,             \
                        (const f64x2 *)t.x2, (f64x2 *)t.x3, n * 8); }, false, {}});
   PROD(2, 4) PROD(2, 2) PROD(1, 4) PROD(1, 2) PROD(1, 6) PROD(4, 2)
+  // the product's own work split: no weighted sum (no weight loads, no
+  // ticket), and neither the sum nor the scaler bytes
+  vars.push_back({"product U=2 4/CU no sum", [&](const Set &t) {
+    hipLaunchKernelGGL((plf_dna_f64_pair_kernel<2, false, 1, true>), dim3(4 * cus), dim3(kBlock), 0, s, t.x1,
+                       t.x2, t.x3, EV, L, R, w, t.sc, n, ws, (int64_t *)nullptr); }, false, {}});
+  vars.push_back({"product U=2 4/CU no sum/sc", [&](const Set &t) {
+    hipLaunchKernelGGL((plf_dna_f64_pair_kernel<2, false, 1, true>), dim3(4 * cus), dim3(kBlock), 0, s, t.x1,
+                       t.x2, t.x3, EV, L, R, w, (uint8_t *)nullptr, n, ws, (int64_t *)nullptr); }, false, {}});
+  vars.push_back({"product U=2 4/CU wgt=null", [&](const Set &t) {
+    hipLaunchKernelGGL((plf_dna_f64_pair_kernel<2, true, 1, true>), dim3(4 * cus), dim3(kBlock), 0, s, t.x1,
+                       t.x2, t.x3, EV, L, R, (const int32_t *)nullptr, t.sc, n, ws, t.sum); }, false, {}});
   PSTR(2, 4) PSTR(2, 2) PSTR(1, 4) PSTR(1, 2) PSTR(1, 6)
   BSTR(1, 2) BSTR(2, 2) BSTR(2, 4) BSTR(4, 4)
   // bit-check every product shape against U=2 4/CU (the product)
