@@ -81,6 +81,112 @@ __global__ void __launch_bounds__(256) block_stream(const f64x2 *__restrict__ a,
   }
 }
 
+// The product body with a packed epilogue per trip (U = 2: 32 sites per wave
+// trip): ONE weight load (lane l < 32: site l of the trip) instead of four
+// 8-lane loads, and ONE scaler store (lanes 0..7: a dword = 4 sites' bytes)
+// instead of four 8-lane byte stores; the trip's 32 scale bits come from the
+// four ballots (wave-uniform).  x3, scaler bytes and the sum must equal the
+// product's (checked).
+__global__ void __launch_bounds__(kBlock, 1)
+pair_packed(const double *__restrict__ x1, const double *__restrict__ x2, double *__restrict__ x3,
+            const double *__restrict__ EV, const double *__restrict__ left, const double *__restrict__ right,
+            const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+            int64_t *scaler_sum) {
+  constexpr int U = 2;
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 1, c = (lane >> 1) & 3, sh = lane & 56;
+  double PL[2][4], PR[2][4], E[4][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      PL[kk][l] = left[c * 16 + (2 * h + kk) * 4 + l];
+      PR[kk][l] = right[c * 16 + (2 * h + kk) * 4 + l];
+    }
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int t = 0; t < 2; t++) E[k][t] = EV[4 * k + 2 * h + t];
+  const double m = Num<double>::minlik();
+  long long acc = 0;
+  // one 8-site block; returns its 8 scale bits (wave-uniform)
+  auto body = [&](const f64x2 a, const f64x2 b, int64_t site0) -> unsigned {
+    double u1[2], u2[2];
+    {
+      const double a0 = dpp_f64<kQuadEven>(a.x), a1 = dpp_f64<kQuadEven>(a.y);
+      const double a2 = dpp_f64<kQuadOdd>(a.x), a3 = dpp_f64<kQuadOdd>(a.y);
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) {
+        double v = a0 * PL[kk][0];
+        v += a1 * PL[kk][1]; v += a2 * PL[kk][2]; v += a3 * PL[kk][3];
+        u1[kk] = v;
+      }
+    }
+    {
+      const double b0 = dpp_f64<kQuadEven>(b.x), b1 = dpp_f64<kQuadEven>(b.y);
+      const double b2 = dpp_f64<kQuadOdd>(b.x), b3 = dpp_f64<kQuadOdd>(b.y);
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) {
+        double v = b0 * PR[kk][0];
+        v += b1 * PR[kk][1]; v += b2 * PR[kk][2]; v += b3 * PR[kk][3];
+        u2[kk] = v;
+      }
+    }
+    double pm[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) pm[kk] = u1[kk] * u2[kk];
+    const double p0 = dpp_f64<kQuadEven>(pm[0]), p1 = dpp_f64<kQuadEven>(pm[1]);
+    const double p2 = dpp_f64<kQuadOdd>(pm[0]), p3 = dpp_f64<kQuadOdd>(pm[1]);
+    double o[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      double x = 0.0;
+      x += p0 * E[0][t]; x += p1 * E[1][t]; x += p2 * E[2][t]; x += p3 * E[3][t];
+      o[t] = x;
+    }
+    const bool small = (__builtin_fabs(o[0]) < m) && (__builtin_fabs(o[1]) < m);
+    const unsigned long long mask = __ballot(small);
+    const bool sc = ((mask >> sh) & 0xFFull) == 0xFFull;
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const double s = o[t] * Num<double>::two32();
+      o[t] = sc ? s : o[t];
+    }
+    f64x2 ov = {o[0], o[1]};
+    __builtin_nontemporal_store(ov, reinterpret_cast<f64x2 *>(x3 + site0 * 16) + lane);
+    unsigned bits = 0;  // bit g: site g of the block scaled (from the uniform mask)
+#pragma unroll
+    for (int g = 0; g < 8; g++) bits |= (((mask >> (8 * g)) & 0xFFull) == 0xFFull ? 1u : 0u) << g;
+    return bits;
+  };
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
+  for (int64_t base = wave * 16 * U; base + 16 * U <= n; base += stride) {  // full trips (the probe's n)
+    f64x2 a[U][2], b[U][2];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int64_t site0 = base + u * 16 + j * 8;
+        a[u][j] = ld16<true>(reinterpret_cast<const f64x2 *>(x1 + site0 * 16) + lane);
+        b[u][j] = ld16<true>(reinterpret_cast<const f64x2 *>(x2 + site0 * 16) + lane);
+      }
+    const int wl = wgt[base + (lane & 31)];  // one load: the trip's 32 weights
+    unsigned T = 0;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) T |= body(a[u][j], b[u][j], base + u * 16 + j * 8) << (8 * (2 * u + j));
+    if (lane < 32 && ((T >> lane) & 1)) acc += wl;
+    if (lane < 8) {
+      const unsigned q = T >> (4 * lane);
+      const unsigned d = (q & 1u) | ((q >> 1) & 1u) << 8 | ((q >> 2) & 1u) << 16 | ((q >> 3) & 1u) << 24;
+      reinterpret_cast<unsigned *>(scaler + base)[lane] = d;
+    }
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
 __global__ void fill(double *p, int64_t n16, uint64_t seed, bool scale4) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
@@ -150,6 +256,9 @@ int main(int argc, char **argv) {
   vars.push_back({"product U=2 4/CU no sum/sc", [&](const Set &t) {
     hipLaunchKernelGGL((plf_dna_f64_pair_kernel<2, false, 1, true>), dim3(4 * cus), dim3(kBlock), 0, s, t.x1,
                        t.x2, t.x3, EV, L, R, w, (uint8_t *)nullptr, n, ws, (int64_t *)nullptr); }, false, {}});
+  vars.push_back({"packed epilogue 4/CU", [&](const Set &t) {
+    hipLaunchKernelGGL(pair_packed, dim3(4 * cus), dim3(kBlock), 0, s, t.x1, t.x2, t.x3, EV, L, R, w, t.sc, n,
+                       ws, t.sum); }, true, {}});
   vars.push_back({"product U=2 4/CU wgt=null", [&](const Set &t) {
     hipLaunchKernelGGL((plf_dna_f64_pair_kernel<2, true, 1, true>), dim3(4 * cus), dim3(kBlock), 0, s, t.x1,
                        t.x2, t.x3, EV, L, R, (const int32_t *)nullptr, t.sc, n, ws, t.sum); }, false, {}});
