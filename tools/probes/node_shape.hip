@@ -187,6 +187,140 @@ pair_packed(const double *__restrict__ x1, const double *__restrict__ x2, double
   block_ticket_sum(acc, ws, scaler_sum);
 }
 
+// The product's arithmetic fed by LDS-DMA: every 8-site step's x1 / x2 rows
+// go global -> LDS (global_load_lds_dwordx4: lane l's 16 B land at
+// stage + 16 l, exactly the lane's register-load layout) into a wave-private
+// ring D steps deep, so a wave keeps D steps of loads in flight through its
+// arithmetic without holding them in VGPRs.  Steps: wave w takes 8-site
+// blocks w, w + W, ...; per step after the wait: 2 ds_read_b128, the body,
+// 1 x3 store, 1 scaler store, then the DMA of step + D (2) and of its
+// weights (1, into LDS too) -- 5 vector-memory ops, so the step issued D steps ago is complete at
+// vmcnt((D - 1) * 5) (gfx9 counts stores in vmcnt, in order).
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
+template <int D, int ST>
+__device__ __forceinline__ void wait_first(int st) {
+  if constexpr (ST < D) {
+    if (st == ST) wait_vm<(D - 1 - ST) * 3 + ST * 5>();
+    else wait_first<D, ST + 1>(st);
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(kBlock, 1)
+pair_dma(const double *__restrict__ x1, const double *__restrict__ x2, double *__restrict__ x3,
+         const double *__restrict__ EV, const double *__restrict__ left, const double *__restrict__ right,
+         const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
+         int64_t *scaler_sum) {
+  __shared__ __attribute__((aligned(16))) double ring[kWavesPerBlock][D][2][128];  // [wave][stage][x1|x2][64 lanes x 2]
+  __shared__ int wring[kWavesPerBlock][D][64];  // the step's weights, lane l: site g(l) (DMA, 4 B per lane)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int h = lane & 1, c = (lane >> 1) & 3, g = lane >> 3, sh = lane & 56;
+  double PL[2][4], PR[2][4], E[4][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      PL[kk][l] = left[c * 16 + (2 * h + kk) * 4 + l];
+      PR[kk][l] = right[c * 16 + (2 * h + kk) * 4 + l];
+    }
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int t = 0; t < 2; t++) E[k][t] = EV[4 * k + 2 * h + t];
+  const double m = Num<double>::minlik();
+  long long acc = 0;
+  const int64_t W = (int64_t)gridDim.x * kWavesPerBlock;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wv;
+  const int64_t nsteps = n / 8;  // the probe's n: whole 8-site blocks
+  const int64_t mine = nsteps > wave ? (nsteps - wave + W - 1) / W : 0;  // this wave's steps
+  auto issue = [&](int64_t k, int st) {  // DMA of the wave's step k into stage st (k < mine)
+    const int64_t site0 = (wave + k * W) * 8;
+    __builtin_amdgcn_global_load_lds((const void *)(x1 + site0 * 16 + 2 * lane),
+                                     (__attribute__((address_space(3))) void *)&ring[wv][st][0][0], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void *)(x2 + site0 * 16 + 2 * lane),
+                                     (__attribute__((address_space(3))) void *)&ring[wv][st][1][0], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void *)(wgt + site0 + g),
+                                     (__attribute__((address_space(3))) void *)&wring[wv][st][0], 4, 0, 0);
+  };
+  // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left at their maxima (gfx9
+  // encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])
+  constexpr int kAfter = (D - 1) * 5;
+  constexpr int kWaitStep = 0x0F70 | (kAfter & 15) | ((kAfter >> 4) << 14);
+  constexpr int kWaitAll = 0x0F70;
+#pragma unroll
+  for (int st = 0; st < D; st++)
+    if (st < mine) issue(st, st);
+  for (int64_t k0 = 0; k0 < mine; k0 += D) {
+#pragma unroll
+    for (int st = 0; st < D; st++) {
+      const int64_t k = k0 + st;
+      if (k >= mine) break;
+      // the step issued D steps ago: everything after it may stay in flight
+      // first round: after step st's prologue DMA came the prologue DMAs of
+      // stages st+1.. (3 each) and steps 0..st-1 (5 each) -- fewer than later
+      if (k + D > mine) __builtin_amdgcn_s_waitcnt(kWaitAll);  // the tail: vmcnt(0)
+      else if (k0 == 0) wait_first<D, 0>(st);
+      else __builtin_amdgcn_s_waitcnt(kWaitStep);
+      const f64x2 a = *reinterpret_cast<const f64x2 *>(&ring[wv][st][0][2 * lane]);
+      const f64x2 b = *reinterpret_cast<const f64x2 *>(&ring[wv][st][1][2 * lane]);
+      const int w = wring[wv][st][lane];
+      const int64_t site0 = (wave + k * W) * 8;
+      double u1[2], u2[2];
+      {
+        const double a0 = dpp_f64<kQuadEven>(a.x), a1 = dpp_f64<kQuadEven>(a.y);
+        const double a2 = dpp_f64<kQuadOdd>(a.x), a3 = dpp_f64<kQuadOdd>(a.y);
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+          double v = a0 * PL[kk][0];
+          v += a1 * PL[kk][1]; v += a2 * PL[kk][2]; v += a3 * PL[kk][3];
+          u1[kk] = v;
+        }
+      }
+      {
+        const double b0 = dpp_f64<kQuadEven>(b.x), b1 = dpp_f64<kQuadEven>(b.y);
+        const double b2 = dpp_f64<kQuadOdd>(b.x), b3 = dpp_f64<kQuadOdd>(b.y);
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+          double v = b0 * PR[kk][0];
+          v += b1 * PR[kk][1]; v += b2 * PR[kk][2]; v += b3 * PR[kk][3];
+          u2[kk] = v;
+        }
+      }
+      double pm[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) pm[kk] = u1[kk] * u2[kk];
+      const double p0 = dpp_f64<kQuadEven>(pm[0]), p1 = dpp_f64<kQuadEven>(pm[1]);
+      const double p2 = dpp_f64<kQuadOdd>(pm[0]), p3 = dpp_f64<kQuadOdd>(pm[1]);
+      double o[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        double x = 0.0;
+        x += p0 * E[0][t]; x += p1 * E[1][t]; x += p2 * E[2][t]; x += p3 * E[3][t];
+        o[t] = x;
+      }
+      const bool small = (__builtin_fabs(o[0]) < m) && (__builtin_fabs(o[1]) < m);
+      const unsigned long long mask = __ballot(small);
+      const bool sc = ((mask >> sh) & 0xFFull) == 0xFFull;
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const double s2 = o[t] * Num<double>::two32();
+        o[t] = sc ? s2 : o[t];
+      }
+      f64x2 ov = {o[0], o[1]};
+      __builtin_nontemporal_store(ov, reinterpret_cast<f64x2 *>(x3 + site0 * 16) + lane);
+      if ((lane & 7) == 0) {
+        scaler[site0 + g] = (uint8_t)sc;
+        if (sc) acc += w;
+      }
+      if (k + D < mine) issue(k + D, st);
+    }
+  }
+  block_ticket_sum(acc, ws, scaler_sum);
+}
+
 __global__ void fill(double *p, int64_t n16, uint64_t seed, bool scale4) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
@@ -256,6 +390,11 @@ int main(int argc, char **argv) {
   vars.push_back({"product U=2 4/CU no sum/sc", [&](const Set &t) {
     hipLaunchKernelGGL((plf_dna_f64_pair_kernel<2, false, 1, true>), dim3(4 * cus), dim3(kBlock), 0, s, t.x1,
                        t.x2, t.x3, EV, L, R, w, (uint8_t *)nullptr, n, ws, (int64_t *)nullptr); }, false, {}});
+#define DMA(D, G)                                                                                          \
+  vars.push_back({"dma ring D=" #D " " #G "/CU", [&](const Set &t) {                                      \
+    hipLaunchKernelGGL((pair_dma<D>), dim3(G * cus), dim3(kBlock), 0, s, t.x1, t.x2, t.x3, EV, L, R, w, t.sc, n, \
+                       ws, t.sum); }, true, {}});
+  DMA(2, 4) DMA(4, 4) DMA(4, 2) DMA(6, 2) DMA(8, 2) DMA(3, 4)
   vars.push_back({"packed epilogue 4/CU", [&](const Set &t) {
     hipLaunchKernelGGL(pair_packed, dim3(4 * cus), dim3(kBlock), 0, s, t.x1, t.x2, t.x3, EV, L, R, w, t.sc, n,
                        ws, t.sum); }, true, {}});
