@@ -60,6 +60,46 @@ def test_launched_rank_does_not_relaunch(monkeypatch):
     assert called == []
 
 
+def test_sites_defaults_per_workload_and_explicit_values_kept():
+    """--sites unset: each workload's BASELINE size (node / nodes512 2^20,
+    protein / prottree64 2^18, swemu1024 1024); an explicit --sites, 2^20
+    included, is used as given (the round-4 sentinel turned an explicit 2^20
+    protein request into 2^18), and the PMC key names the sites that run."""
+    for wl, n in (("node", 1 << 20), ("nodes512", 1 << 20), ("tree64", 1 << 20),
+                  ("protein", 1 << 18), ("prottree64", 1 << 18), ("swemu1024", 1024)):
+        a = bench.parse(["--workload", wl])
+        assert a.sites == n, wl
+    for wl in ("protein", "prottree64", "swemu1024", "node"):
+        a = bench.parse(["--workload", wl, "--sites", str(1 << 20)])
+        assert a.sites == 1 << 20, wl
+    assert bench.traffic_key(bench.parse(["--workload", "protein", "--exact"])).endswith("sites262144")
+    assert bench.traffic_key(bench.parse(["--workload", "protein", "--sites", "1048576"])).endswith(
+        "sites1048576")
+    a = bench.parse([])
+    assert a.workload == "node" and not a.no_nodes512 and a.nodes == 512
+    assert bench.parse(["--no-nodes512"]).no_nodes512
+
+
+def test_speedup_fields_labelled():
+    """The node line's speed-ups: like for like against the stated baseline
+    (dtype, cores) and the sw_emu path; the reference's f32 -O0 one-thread
+    row kept with its basis spelled out."""
+    cb = {"value": 4.0e8, "cores": 16, "swemu_path": {"value": 1.0e8, "cores": 16},
+          "reference_plf_O0_f32_1thread": 4.0e6}
+    out = bench.speedup_fields(1.6e10, 1.2e8, cb, "f64")
+    s = out["speedup_vs_cpu_baseline"]
+    assert s["excluding_pcie"] == 40.0 and s["including_pcie"] == 0.3
+    assert s["vs_swemu_path_excluding_pcie"] == 160.0
+    assert "f64" in s["basis"] and "16 cores" in s["basis"]
+    r = out["speedup_vs_reference_plf"]
+    assert r["excluding_pcie"] == 4000.0
+    assert "f32" in r["basis"] and "-O0" in r["basis"] and "1 thread" in r["basis"]
+    assert "not like for like" in r["basis"]
+    out = bench.speedup_fields(1.0, 1.0, {"value": 1.0, "cores": 1}, "f32")
+    assert "speedup_vs_reference_plf" not in out
+    assert "vs_swemu_path_excluding_pcie" not in out["speedup_vs_cpu_baseline"]
+
+
 class _WL:
     bytes_per_step = 12345
 

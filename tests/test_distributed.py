@@ -47,22 +47,27 @@ def _worker(rank, world, port, q):
                                              torch.device("cpu"), world)
         bad = bench.combine_ranks(1.0, 1.0, torch.tensor(3), 4 if rank == 1 else 3,
                                   torch.device("cpu"), world)[2]
-        q.put((rank, wall, devt, ok, bad))
+        skew = bench.rank_clock_spread(100.0 + 25e-6 * rank, 200.0 - 40e-6 * rank, torch.device("cpu"),
+                                       world)
+        q.put((rank, wall, devt, ok, bad, skew))
     finally:
         dist.destroy_process_group()
 
 
 def test_combine_ranks_gloo_world2():
-    for rank, wall, devt, ok, bad in _spawn(_worker, 2):
+    for rank, wall, devt, ok, bad, skew in _spawn(_worker, 2):
         assert wall == 11.0 and devt == 10.0   # max over ranks
         assert ok is True                      # sum of got == sum of expected
         assert bad is False                    # one rank's mismatch is seen by every rank
+        # the ranks' region-start / -end clocks: max - min, in us, on every rank
+        assert abs(skew[0] - 25.0) < 1e-3 and abs(skew[1] - 40.0) < 1e-3
 
 
 def test_combine_ranks_single():
     import bench
 
     assert bench.combine_ranks(3.0, 2.0, torch.tensor(5), 5, torch.device("cpu"), 1) == (3.0, 2.0, True)
+    assert bench.rank_clock_spread(5.0, 6.0, torch.device("cpu"), 1) == (0.0, 0.0)
 
 
 # --- BASELINE configs[3] on the CPU: real nodes, the product's partition, the

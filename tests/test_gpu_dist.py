@@ -95,7 +95,8 @@ def test_nodes_three_ranks_ragged_split():
     port = _port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "2",
-           "--sites", "65536", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--buffer-sets", "2"]
+           "--sites", "65536", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--buffer-sets", "2",
+           "--no-nodes512"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT),
                        env={**os.environ, "PLFX_DIST_BACKEND": "gloo", "OMP_NUM_THREADS": "4"})
     assert r.returncode == 0, r.stderr[-3000:]
@@ -103,6 +104,7 @@ def test_nodes_three_ranks_ragged_split():
     assert d["n_gpus"] == 2 and len(d["config"]["lnl_per_rank"]) == 2
     assert d["config"]["lnl_all_ranks"] == sum(d["config"]["lnl_per_rank"])
     assert d["config"]["scaler_events_all_ranks"] == 2 * (65536 // 4)
+    assert "nodes512" not in d["config"]  # --no-nodes512
 
 
 def test_bench_gpus_two_without_outer_launcher():
@@ -113,7 +115,7 @@ def test_bench_gpus_two_without_outer_launcher():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env.update(PLFX_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
     cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--sites", "65536", "--steps", "3",
-           "--warmup", "1", "--no-cpu-baseline", "--buffer-sets", "2"]
+           "--warmup", "1", "--no-cpu-baseline", "--buffer-sets", "2", "--nodes", "12"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT), env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = r.stdout.splitlines()
@@ -123,6 +125,12 @@ def test_bench_gpus_two_without_outer_launcher():
     assert d["config"]["launcher"] == "torch.distributed.run started by bench.py"
     assert d["config"]["distributed"] == "gloo"
     assert d["config"]["scaler_events_all_ranks"] == 2 * (65536 // 4)
+    assert d["value_device"] >= d["value"] > 0 and d["barrier_skew_us"] >= 0
+    # the default invocation also times BASELINE configs[3]: 12 nodes, 6 per rank
+    sub = d["config"]["nodes512"]
+    assert sub["check"] == "ok" and sub["scaling"] == "strong" and sub["nodes_per_rank"] == 6
+    assert sub["nodes_in_job"] == 12 and sub["scaler_events_all_ranks"] == 12 * (65536 // 4)
+    assert sub["value_device"] >= sub["value"] > 0 and sub["barrier_skew_us"] >= 0
 
 
 def test_nodes512_full_size_windows(oracle):
@@ -170,9 +178,10 @@ def test_nodes512_full_size_windows(oracle):
 def test_eight_ranks_gloo_rehearsal():
     """The driver's N = 8 layout rehearsed on the box's one GPU: 8 ranks under
     torch.distributed.run (gloo, every rank's device folded onto GPU 0) for the
-    default node workload and for nodes512 with 16 nodes (2 per rank): one JSON
-    line, every rank's lnL in the one all-reduce, the scaler totals exact, and
-    the nodes512 job lnL equal to one rank's bit for bit."""
+    default node workload -- with its config.nodes512 sub-record (16 nodes, 2
+    per rank) -- and for --workload nodes512: one JSON line, every rank's lnL
+    in the one all-reduce, the scaler totals exact, value_device >= value,
+    and the nodes512 job lnL equal to one rank's bit for bit."""
     def run(nproc, *args):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
@@ -184,9 +193,22 @@ def test_eight_ranks_gloo_rehearsal():
         assert len(lines) == 1, r.stdout
         return json.loads(lines[0])
 
-    d = run(8, "--sites", "65536", "--buffer-sets", "2")
+    d = run(8, "--sites", "65536", "--buffer-sets", "2", "--nodes", "16")
     assert d["n_gpus"] == 8 and d["check"] == "ok" and len(d["config"]["lnl_per_rank"]) == 8
     assert d["config"]["scaler_events_all_ranks"] == 8 * (65536 // 4)
+    # N > 1 honesty fields: device-time rate and the ranks' barrier-exit spread
+    assert d["value_device"] >= d["value"] > 0 and d["barrier_skew_us"] >= 0
+    # BASELINE configs[3] rides along in the default invocation: 16 nodes over
+    # 8 ranks, its one lnL all-reduce equal to one rank's bit for bit
+    s8 = d["config"]["nodes512"]
+    d1 = run(1, "--sites", "65536", "--buffer-sets", "2", "--nodes", "16")
+    s1 = d1["config"]["nodes512"]
+    assert s8["check"] == s1["check"] == "ok" and s8["scaling"] == "strong"
+    assert s8["nodes_per_rank"] == 2 and s1["nodes_per_rank"] == 16 and s8["nodes_in_job"] == 16
+    assert s8["lnl_all_nodes_all_ranks"] == s1["lnl_all_nodes_all_ranks"]
+    assert s8["scaler_events_all_ranks"] == s1["scaler_events_all_ranks"] == 16 * (65536 // 4)
+    assert s8["value_device"] >= s8["value"] > 0 and s8["extra_wall_s"] > 0
+    assert d1["barrier_skew_us"] == 0.0 and d1["value_device"] >= d1["value"]
     e8 = run(8, "--workload", "nodes512", "--nodes", "16", "--sites", "4099")
     e1 = run(1, "--workload", "nodes512", "--nodes", "16", "--sites", "4099")
     assert e8["check"] == e1["check"] == "ok" and e8["scaling"] == "strong"
