@@ -37,16 +37,24 @@ constexpr int kHostChunksMax = 16;
 // returns an entry to the pool -- unless a graph was captured through it: the
 // graph's replays keep using the entry's words, so it is retired (never handed
 // to another stream) and the context waits for the device when destroyed.
+// Every call that used an entry outside a capture records the entry's `done`
+// event on its stream after its launches (WsDone), so plfx_ctx_destroy waits
+// for an entry's last work through that event and never touches a caller's
+// stream handle (which may no longer exist).
 struct StreamWs {
   hipStream_t stream = nullptr;
   std::thread::id tid;               // owning thread for hipStreamPerThread, else none
   bool in_use = false;
   bool captured = false;             // used while its stream was capturing
   bool retired = false;              // released after a capture, or its thread exited
+  bool cap_now = false;              // the current call's stream is capturing
+  hipEvent_t done = nullptr;         // recorded after each uncaptured call's launches
   unsigned long long *ws = nullptr;  // kWsRegions x kWsWords u64
   double *lnl_partials = nullptr;    // kLnlMaxGrid doubles
   unsigned long long *lnl_ticket = nullptr;
-  char *tt = nullptr;  // tip/tip protein combination tables (kTtEntryBytes, allocated with the entry)
+  // tip/tip protein combination tables (kTtEntryBytes): allocated with the
+  // entry, or on first use with PLFX_CTX_LAZY_TABLES (nullptr until then)
+  char *tt = nullptr;
 };
 constexpr int kWsPool = PLFX_WS_POOL;
 
@@ -56,6 +64,7 @@ struct plfx_ctx {
   int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
   int fuse = 3;  // traverse: 3 six-level subtrees before 2's, 2 three-level subtrees +
                  // level pairs, 1 level pairs, 0 none (PLFX_FUSE)
+  bool lazy_tables = false;         // PLFX_CTX_LAZY_TABLES
   std::deque<StreamWs> wss;         // per-stream workspaces (stable addresses)
   std::vector<void *> ws_blocks;    // their allocations (the pool's, then one per extra entry)
   uint8_t *tt_codes = nullptr;      // the tip/tip tables' two constant 576-code arrays (kTtCodeBytes)
@@ -212,7 +221,7 @@ StreamWs *ws_take(plfx_ctx *ctx, StreamWs &w, hipStream_t s) {
 }
 
 // The workspace of stream s: its own, else a free pool entry (zero at rest),
-// else a retired per-thread entry reclaimed after a device synchronisation,
+// else a retired per-thread entry reclaimed after its `done` event,
 // else a new allocation (zeroed in order on s) -- neither of the last two
 // inside a stream capture.  An entry used while s is capturing is marked: the
 // graph keeps using it after the capture.
@@ -228,26 +237,22 @@ StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
       }
   if (!got && !cap) {
     // entries of exited threads' per-thread streams (not captured: those
-    // stay retired): their last launches must be done before reuse
-    bool any = false;
-    for (StreamWs &w : ctx->wss) any |= w.in_use && w.retired && !w.captured;
-    if (any) {
-      hipError_t e = hipDeviceSynchronize();
-      if (e != hipSuccess) {
-        *rc = hip_fail(ctx, e, "reclaiming workspaces of exited threads");
-        return nullptr;
-      }
-      for (StreamWs &w : ctx->wss)
-        if (w.in_use && w.retired && !w.captured) w.in_use = false;
-      for (StreamWs &w : ctx->wss)
-        if (!w.in_use) {
-          got = ws_take(ctx, w, s);
-          break;
+    // stay retired): their last launches must be done before reuse -- waited
+    // for through the entry's event (the thread's stream is gone)
+    for (StreamWs &w : ctx->wss)
+      if (w.in_use && w.retired && !w.captured) {
+        hipError_t e = hipEventSynchronize(w.done);
+        if (e != hipSuccess) {
+          *rc = hip_fail(ctx, e, "reclaiming the workspace of an exited thread");
+          return nullptr;
         }
-    }
+        w.in_use = false;
+        if (!got) got = ws_take(ctx, w, s);
+      }
   }
   if (got) {
     got->captured = got->captured || cap;
+    got->cap_now = cap;
     return got;
   }
   if ((int)ctx->wss.size() >= PLFX_MAX_STREAMS) {
@@ -266,24 +271,44 @@ StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
   // freed stream-ordered at destroy, which a plain hipFree would turn into a
   // wait for the whole device)
   void *block = nullptr;
-  hipError_t e = hipMallocAsync(&block, kWsEntryBytes + kTtEntryBytes, s);
+  const size_t bytes = kWsEntryBytes + (ctx->lazy_tables ? 0 : kTtEntryBytes);
+  hipEvent_t done = nullptr;
+  hipError_t e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
   if (e != hipSuccess) {
-    *rc = fail(ctx, PLFX_ERR_NOMEM, "workspace hipMallocAsync(%zu): %s", kWsEntryBytes + kTtEntryBytes,
-               hipGetErrorString(e));
+    *rc = hip_fail(ctx, e, "workspace event");
+    return nullptr;
+  }
+  e = hipMallocAsync(&block, bytes, s);
+  if (e != hipSuccess) {
+    (void)hipEventDestroy(done);
+    *rc = fail(ctx, PLFX_ERR_NOMEM, "workspace hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
     return nullptr;
   }
   e = hipMemsetAsync(block, 0, kWsEntryBytes, s);
   if (e != hipSuccess) {
     (void)hipFreeAsync(block, s);
+    (void)hipEventDestroy(done);
     *rc = hip_fail(ctx, e, "workspace memset");
     return nullptr;
   }
   ctx->ws_blocks.push_back(block);
   StreamWs w;
-  ws_carve(w, block, static_cast<char *>(block) + kWsEntryBytes);
+  ws_carve(w, block, ctx->lazy_tables ? nullptr : static_cast<char *>(block) + kWsEntryBytes);
+  w.done = done;
   ctx->wss.push_back(w);
   return ws_take(ctx, ctx->wss.back(), s);
 }
+
+// Records the entry's `done` event on the call's stream when the call's
+// launches are issued (at scope exit), unless the stream is capturing: a
+// captured entry's work belongs to the graph and is waited for device-wide.
+struct WsDone {
+  StreamWs *w;
+  hipStream_t s;
+  ~WsDone() {
+    if (w && w->done && !w->cap_now) (void)hipEventRecord(w->done, s);
+  }
+};
 
 // the workspace of stream s as `out`; returns from the caller on failure
 #define PLFX_WS(ctx, s, out)                      \
@@ -292,7 +317,8 @@ StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
     int wrc_ = PLFX_OK;                           \
     out = ws_for((ctx), (s), &wrc_);              \
     if (!out) return wrc_;                        \
-  } while (0)
+  } while (0);                                    \
+  WsDone out##_done_{out, (s)}
 
 // [a, a + na) and [b, b + nb) share a byte
 bool overlap(const void *a, size_t na, const void *b, size_t nb) {
@@ -340,6 +366,8 @@ int plf_dev(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int64_t
 int ensure_dbuf(plfx_ctx *ctx, size_t bytes) {
   if (bytes <= ctx->d_cap) return PLFX_OK;
   if (ctx->d_buf) {
+    // the last call's downloads (d2h_stream) and launches (stream) read it
+    if (ctx->d2h_stream) PLFX_HIP(ctx, hipStreamSynchronize(ctx->d2h_stream));
     PLFX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     PLFX_HIP(ctx, hipFreeAsync(ctx->d_buf, ctx->stream));
     ctx->d_buf = nullptr;
@@ -481,6 +509,19 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
     // kernel, then x3 / scaler / sum gathered by code pair (a write stream;
     // the direct kernel is compute-bound: 77 us f64, 95 us f32 per 2^18 sites)
     {
+      if (!w->tt) {  // PLFX_CTX_LAZY_TABLES: this entry's tables on its first tip/tip use
+        if (w->cap_now)
+          return fail(ctx, PLFX_ERR_INVALID,
+                      "protein tip/tip tables: the context was created with PLFX_CTX_LAZY_TABLES and "
+                      "this stream has not made a tip/tip call outside a capture yet");
+        void *t = nullptr;
+        hipError_t e = hipMallocAsync(&t, kTtEntryBytes, s);
+        if (e != hipSuccess)
+          return fail(ctx, PLFX_ERR_NOMEM, "tip/tip tables hipMallocAsync(%zu): %s", kTtEntryBytes,
+                      hipGetErrorString(e));
+        ctx->ws_blocks.push_back(t);
+        w->tt = static_cast<char *>(t);
+      }
       char *tt = w->tt;
       const uint8_t *cc1 = ctx->tt_codes, *cc2 = cc1 + 1024;
       for (int j = 0; j < count; j += plfx::kMaxBatch) {
@@ -566,8 +607,11 @@ extern "C" {
 
 int plfx_get_version(void) { return PLFX_VERSION; }
 
-int plfx_ctx_create(int device, plfx_ctx **out) {
+int plfx_ctx_create(int device, plfx_ctx **out) { return plfx_ctx_create_ex(device, 0u, out); }
+
+int plfx_ctx_create_ex(int device, unsigned flags, plfx_ctx **out) {
   if (!out) return PLFX_ERR_INVALID;
+  if (flags & ~(unsigned)PLFX_CTX_LAZY_TABLES) return PLFX_ERR_INVALID;
   *out = nullptr;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
@@ -578,6 +622,7 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
   plfx_ctx *ctx = new (std::nothrow) plfx_ctx();
   if (!ctx) return PLFX_ERR_NOMEM;
   ctx->device = device;
+  ctx->lazy_tables = (flags & PLFX_CTX_LAZY_TABLES) != 0;
   DeviceGuard guard(device);  // the caller's current device is restored on return
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
@@ -593,6 +638,8 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
   // the workspace pool: kWsPool entries (reduction words zeroed before return,
   // tip/tip tables), and the tables' constant code arrays
   auto undo = [&](int code) {
+    for (StreamWs &w : ctx->wss)
+      if (w.done) (void)hipEventDestroy(w.done);
     for (void *b : ctx->ws_blocks) (void)hipFreeAsync(b, ctx->stream);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -602,8 +649,10 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
   void *pool = nullptr, *tabs = nullptr, *codes = nullptr;
   if (hipMallocAsync(&pool, kWsPool * kWsEntryBytes, ctx->stream) != hipSuccess) return undo(PLFX_ERR_NOMEM);
   ctx->ws_blocks.push_back(pool);
-  if (hipMallocAsync(&tabs, kWsPool * kTtEntryBytes, ctx->stream) != hipSuccess) return undo(PLFX_ERR_NOMEM);
-  ctx->ws_blocks.push_back(tabs);
+  if (!ctx->lazy_tables) {
+    if (hipMallocAsync(&tabs, kWsPool * kTtEntryBytes, ctx->stream) != hipSuccess) return undo(PLFX_ERR_NOMEM);
+    ctx->ws_blocks.push_back(tabs);
+  }
   if (hipMallocAsync(&codes, kTtCodeBytes, ctx->stream) != hipSuccess) return undo(PLFX_ERR_NOMEM);
   ctx->ws_blocks.push_back(codes);
   uint8_t cc[kTtCodeBytes] = {};
@@ -618,8 +667,11 @@ int plfx_ctx_create(int device, plfx_ctx **out) {
   ctx->tt_codes = static_cast<uint8_t *>(codes);
   for (int i = 0; i < kWsPool; i++) {
     StreamWs w;
-    ws_carve(w, static_cast<char *>(pool) + i * kWsEntryBytes, static_cast<char *>(tabs) + i * kTtEntryBytes);
+    ws_carve(w, static_cast<char *>(pool) + i * kWsEntryBytes,
+             tabs ? static_cast<char *>(tabs) + i * kTtEntryBytes : nullptr);
     ctx->wss.push_back(w);
+    if (hipEventCreateWithFlags(&ctx->wss.back().done, hipEventDisableTiming) != hipSuccess)
+      return undo(PLFX_ERR_HIP);
   }
   {
     std::lock_guard<std::mutex> l(g_live_mu);
@@ -639,31 +691,31 @@ int plfx_ctx_destroy(plfx_ctx *ctx) {
   {
     DeviceGuard guard(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    // all device memory of the context is stream-ordered (hipMallocAsync):
-    // freed on its stream below, since hipFree would wait for the whole device
-    if (ctx->d_buf) (void)hipFreeAsync(ctx->d_buf, ctx->stream);
+    // the staging buffer's last downloads run on d2h_stream: done before the
+    // free.  All device memory of the context is stream-ordered
+    // (hipMallocAsync): freed on its stream below, since hipFree would wait for
+    // the whole device
     if (ctx->d2h_stream) {
       (void)hipStreamSynchronize(ctx->d2h_stream);
       (void)hipStreamDestroy(ctx->d2h_stream);
     }
+    if (ctx->d_buf) (void)hipFreeAsync(ctx->d_buf, ctx->stream);
     for (hipEvent_t e : ctx->chunk_done)
       if (e) (void)hipEventDestroy(e);
     // Workspace entries still held: their last launches must be done before
-    // the free.  A stream holding one is waited for (it must still exist,
-    // plfx.h); the device is waited for only when no stream can stand for the
-    // entry's work -- an entry used under a capture (the graph may be
-    // replaying on any stream), a retired one, or another thread's
-    // hipStreamPerThread (this thread cannot name that stream).
+    // the free.  Each is waited for through its own `done` event, recorded
+    // after every uncaptured call that used it -- never through the caller's
+    // stream handle, which may already be destroyed.  Only an entry used under
+    // a capture (the graph may still replay on any stream) needs the device.
     bool device_wide = false;
-    const std::thread::id me = std::this_thread::get_id();
     for (StreamWs &w : ctx->wss) {
       if (!w.in_use) continue;
-      if (w.captured || w.retired || (w.stream == hipStreamPerThread && w.tid != me))
-        device_wide = true;
-      else if (w.stream != ctx->stream)
-        (void)hipStreamSynchronize(w.stream);
+      if (w.captured) device_wide = true;
+      else if (w.done) (void)hipEventSynchronize(w.done);
     }
     if (device_wide) (void)hipDeviceSynchronize();
+    for (StreamWs &w : ctx->wss)
+      if (w.done) (void)hipEventDestroy(w.done);
     for (void *b : ctx->ws_blocks) (void)hipFreeAsync(b, ctx->stream);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -925,10 +977,14 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   }
   hipStream_t s = pick(ctx, stream);
   unsigned long long *ws = nullptr;
+  StreamWs *tw = nullptr;
   if (nops > 0 && n > 0) {
-    PLFX_WS(ctx, s, w);
-    ws = w->ws;
+    int wrc = PLFX_OK;
+    tw = ws_for(ctx, s, &wrc);
+    if (!tw) return wrc;
+    ws = tw->ws;
   }
+  WsDone tw_done_{tw, s};  // after every launch of the traversal
   const char *pm = static_cast<const char *>(pmats);
   // the node descriptor of op j, tip child first (dense/tip runs as tip/dense:
   // the product u1*u2 commutes exactly); *kind = number of tip children

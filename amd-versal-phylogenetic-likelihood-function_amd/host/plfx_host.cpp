@@ -6,6 +6,7 @@
 //                    [--aie window|stream] [--window BYTES] [--seed S]
 //                    [--dump PREFIX] [--no-check] [--quiet]
 //                    [--no-intermediate] [--csv FILE] [--devices D0,D1,...]
+//                    [--reduce host|rccl]
 //
 // Mirrors host_mem.cpp:
 //   * argv shape <sites> <calls> <instances> (host_mem.cpp:13-38); the xclbin
@@ -38,6 +39,13 @@
 //     GPUs of a node the way its instances share one card; a device may be
 //     listed twice (two contexts on one GPU).  Default: GPU 0;
 //   * host scaler reduction sum scaler[j]*wgt[j] (host_mem.cpp:384-388);
+//     --reduce rccl instead: every instance's weighted sum on its GPU
+//     (plfx_scaler_sum, in the kernel region) into its slot of a per-GPU
+//     int64[instances] vector, then ONE RCCL all-reduce over the --devices
+//     list (ncclCommInitAll, plfx_rccl.hpp; distinct GPUs only) and the
+//     instance totals added on the host -- the north star's all-reduce over
+//     xGMI in place of the host loop.  The reduction that ran is printed
+//     ("reduce = ..."); the default stays the reference's host loop;
 //   * the correctness check of host_mem.cpp:403-442: this program's own CPU
 //     plf() (below, plf.cpp:19-65 restated) run plf_calls times and timed,
 //     every CLV value and every scalerIncrement compared exactly, "Test result:
@@ -54,6 +62,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -63,6 +72,7 @@
 
 #include "../../include/plfx.h"
 #include "../csrc/testbench.hpp"
+#include "plfx_rccl.hpp"
 
 namespace {
 
@@ -92,13 +102,15 @@ struct Opts {
   bool quiet = false;
   bool no_intermediate = false;
   std::vector<int> devices{0};
+  bool rccl = false;  // --reduce host (default, host_mem.cpp:384-388) | rccl
 };
 
 Opts parse(int argc, char **argv) {
   if (argc < 4)
     die("usage: plfx_host <alignment sites> <plf calls> <parallel instances> [--target hw|sw_emu] "
         "[--dtype f32|f64] [--layout comb|sep] [--aie window|stream] [--window BYTES] [--seed S] "
-        "[--dump PREFIX] [--no-check] [--quiet] [--no-intermediate] [--csv FILE] [--devices D0,D1,...]");
+        "[--dump PREFIX] [--no-check] [--quiet] [--no-intermediate] [--csv FILE] [--devices D0,D1,...] "
+        "[--reduce host|rccl]");
   Opts o;
   try {
     o.sites = std::stoull(argv[1]);
@@ -147,6 +159,11 @@ Opts parse(int argc, char **argv) {
       o.no_intermediate = true;
     } else if (a == "--csv") {
       o.csv = next();
+    } else if (a == "--reduce") {
+      std::string v = next();
+      if (v == "rccl") o.rccl = true;
+      else if (v == "host") o.rccl = false;
+      else die("bad reduction " + v + " (host|rccl)");
     } else if (a == "--devices") {
       o.devices.clear();
       const std::string v = next();
@@ -171,6 +188,7 @@ Opts parse(int argc, char **argv) {
     die("stream movers exist in the COMBINED layout only");
   if (o.sw_emu && o.no_intermediate) die("--no-intermediate is a GPU (hw) run mode");
   if (o.sw_emu && (o.devices.size() != 1 || o.devices[0] != 0)) die("--devices is a GPU (hw) option");
+  if (o.sw_emu && o.rccl) die("--reduce rccl is a GPU (hw) option");
   return o;
 }
 
@@ -337,7 +355,7 @@ int run(const Opts &o) {
     std::vector<plfx_ctx *> ctxs(nd, nullptr);
     int rc = PLFX_OK;
     for (size_t q = 0; q < nd; q++) {
-      rc = plfx_ctx_create(o.devices[q], &ctxs[q]);
+      rc = plfx_ctx_create_ex(o.devices[q], PLFX_CTX_LAZY_TABLES, &ctxs[q]);  // DNA only: no table pool
       if (rc != PLFX_OK) die("plfx_ctx_create(" + std::to_string(o.devices[q]) + ") failed: " + std::to_string(rc));
     }
     auto slot = [&](uint32_t k) { return (size_t)k % nd; };
@@ -366,6 +384,58 @@ int run(const Opts &o) {
         for (auto *v : {&eb, &e1, &e2, &ee}) HIPCHK(hipEventCreate(&(*v)[(size_t)i * P + k]));
       if (!o.no_intermediate) tb.pack<T>(k, ev, bl, br, xl.data(), xr.data(), hL[k], hR[k]);
     }
+    // --reduce rccl: the communicator over the list, per list entry a stream
+    // and the int64[P] slot vector (dSlot: instance k's sum in slot k on its own
+    // GPU, zeros elsewhere) with its reduced copy (dSum); per instance its
+    // weights on the device
+    std::unique_ptr<plfx_host::NodeComm> comm;
+    std::vector<int64_t *> dSlot(nd, nullptr), dSum(nd, nullptr);
+    std::vector<hipStream_t> sq(nd, nullptr);
+    std::vector<int32_t *> dW(P, nullptr);
+    if (o.rccl) {
+      std::string err;
+      comm.reset(new plfx_host::NodeComm(o.devices, err));
+      if (!err.empty()) die(err);
+      for (size_t q = 0; q < nd; q++) {
+        HIPCHK(hipSetDevice(o.devices[q]));
+        HIPCHK(hipMalloc((void **)&dSlot[q], P * sizeof(int64_t)));
+        HIPCHK(hipMalloc((void **)&dSum[q], P * sizeof(int64_t)));
+        HIPCHK(hipMemset(dSlot[q], 0, P * sizeof(int64_t)));
+        HIPCHK(hipStreamCreateWithFlags(&sq[q], hipStreamNonBlocking));
+      }
+      for (uint32_t k = 0; k < P; k++) {
+        on(k);
+        const uint64_t nk = tb.alignments_per_instance(k);
+        HIPCHK(hipMalloc((void **)&dW[k], std::max<uint64_t>(nk, 1) * sizeof(int32_t)));
+        HIPCHK(hipMemcpy(dW[k], wgt.data() + tb.instance_site_offset(k), nk * sizeof(int32_t),
+                         hipMemcpyHostToDevice));
+      }
+    }
+    // instance k's weighted scaler sum on its GPU, into its slot (rccl only)
+    auto device_sum = [&](uint32_t k) {
+      if (!o.rccl) return;
+      plfx_ctx *ctx = ctxs[slot(k)];
+      rc = plfx_scaler_sum(ctx, dS[k], dW[k], (int64_t)tb.alignments_per_instance(k), dSlot[slot(k)] + k, st[k]);
+      if (rc != PLFX_OK) die(std::string("plfx_scaler_sum: ") + plfx_last_error(ctx));
+    };
+    // the call's scalerIncrement: the reference's host loop (host_mem.cpp:
+    // 385-388) over the downloaded bytes, or ONE RCCL all-reduce of the slot
+    // vectors (after every instance of the call finished) and the P totals
+    auto reduce_call = [&](uint32_t i) -> long long {
+      long long s = 0;
+      if (!o.rccl) {
+        for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
+        return s;
+      }
+      const std::string err = comm->allreduce_sum(std::vector<double *>(nd, nullptr), 0, dSlot, P, sq, &dSum);
+      if (!err.empty()) die(err);
+      for (size_t q = 0; q < nd; q++) HIPCHK(hipStreamSynchronize(sq[q]));
+      std::vector<int64_t> v(P);
+      HIPCHK(hipSetDevice(o.devices[0]));
+      HIPCHK(hipMemcpy(v.data(), dSum[0], P * sizeof(int64_t), hipMemcpyDeviceToHost));
+      for (int64_t x : v) s += x;
+      return s;
+    };
     for (size_t q = 0; q < nd; q++) {
       HIPCHK(hipSetDevice(o.devices[q]));
       HIPCHK(hipDeviceSynchronize());
@@ -404,6 +474,7 @@ int run(const Opts &o) {
           HIPCHK(hipStreamWaitEvent(st[k], j_up[k], 0));
           HIPCHK(hipEventRecord(e1[ev_i], st[k]));  // time: t1
           run_instance(k);
+          device_sum(k);
           HIPCHK(hipEventRecord(e2[ev_i], st[k]));  // time: t2
           HIPCHK(hipStreamWaitEvent(sr[k], e2[ev_i], 0));
           HIPCHK(hipMemcpyAsync(result[i].data() + off * 16, dO[k], nk * 16 * es, hipMemcpyDeviceToHost, st[k]));
@@ -413,9 +484,7 @@ int run(const Opts &o) {
           HIPCHK(hipEventRecord(ee[ev_i], st[k]));  // time: end
         }
         for (uint32_t k = 0; k < P; k++) HIPCHK(hipStreamSynchronize(st[k]));
-        long long s = 0;  // host_mem.cpp:385-388
-        for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
-        inc[i] = s;
+        inc[i] = reduce_call(i);
       } else {
         // NO_INTERMEDIATE_RESULTS (host_mem.cpp:327-392): prepare, run, reduce
         Regions &r = callreg[i];
@@ -430,6 +499,7 @@ int run(const Opts &o) {
           HIPCHK(hipEventRecord(j_up[k], sr[k]));
           HIPCHK(hipStreamWaitEvent(st[k], j_up[k], 0));
           run_instance(k);
+          device_sum(k);
           HIPCHK(hipEventRecord(j_run[k], st[k]));
           HIPCHK(hipStreamWaitEvent(so[k], j_run[k], 0));
           HIPCHK(hipMemcpyAsync(scaler[i].data() + off, dS[k], nk, hipMemcpyDeviceToHost, st[k]));
@@ -439,9 +509,7 @@ int run(const Opts &o) {
         }
         for (uint32_t k = 0; k < P; k++) HIPCHK(hipStreamSynchronize(st[k]));
         r.t2 = ms_since(std::chrono::steady_clock::now());
-        long long s = 0;  // host_mem.cpp:385-388
-        for (uint64_t j = 0; j < o.sites; j++) s += (long long)scaler[i][j] * wgt[j];
-        inc[i] = s;
+        inc[i] = reduce_call(i);  // the "scaling wgt mult" region
         r.end = ms_since(std::chrono::steady_clock::now());
       }
       roctxRangePop();
@@ -469,6 +537,17 @@ int run(const Opts &o) {
       (void)hipEventDestroy(e0[k]);
       for (uint32_t i = 0; i < o.calls; i++)
         for (auto *v : {&eb, &e1, &e2, &ee}) (void)hipEventDestroy((*v)[(size_t)i * P + k]);
+    }
+    comm.reset();  // before the streams it reduced on go away
+    for (size_t q = 0; q < nd && o.rccl; q++) {
+      HIPCHK(hipSetDevice(o.devices[q]));
+      (void)hipStreamDestroy(sq[q]);
+      (void)hipFree(dSlot[q]);
+      (void)hipFree(dSum[q]);
+    }
+    for (uint32_t k = 0; k < P && o.rccl; k++) {
+      on(k);
+      (void)hipFree(dW[k]);
     }
     for (plfx_ctx *c : ctxs) plfx_ctx_destroy(c);
   }
@@ -582,6 +661,11 @@ int run(const Opts &o) {
     }
     for (uint32_t i = 0; i < o.calls; i++) std::printf("scalerIncrement[call %u] = %lld\n", i, inc[i]);
   }
+  if (!o.sw_emu)
+    std::printf("reduce = %s\n", o.rccl ? ("rccl (" + std::to_string(o.devices.size()) + " rank" +
+                                           (o.devices.size() > 1 ? "s" : "") + ", RCCL " +
+                                           plfx_host::NodeComm::version() + ")").c_str()
+                                        : "host (host_mem.cpp:384-388 loop)");
   std::printf("Test result: %s\n", verdict.c_str());
   if (!o.csv.empty()) {  // write_to_csv (timing.h:153-194), ms per call
     FILE *f = std::fopen(o.csv.c_str(), "w");

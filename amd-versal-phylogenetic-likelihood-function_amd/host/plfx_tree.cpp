@@ -10,6 +10,7 @@
 //   usage: plfx_tree <taxa (power of 2)> <sites> <sweeps>
 //                    [--dtype f32|f64] [--tips] [--alpha A] [--seed S] [--quiet]
 //                    [--states 4|20] [--fma] [--devices D0,D1,...]
+//                    [--reduce rccl|host]
 //
 // --states 20: a 20-state reversible model (fixed exchangeabilities and
 // frequencies), amino-acid tips (codes 0..19, 5 % X), the protein kernels
@@ -18,9 +19,15 @@
 // --devices D0,D1,...: the alignment's sites split over the listed GPUs by
 // the reference's ceil rule (plfx_shard, include.h:181-189), one context per
 // entry; every GPU sweeps the whole tree over its own site block (its P
-// matrices, traversal and root lnL), the host adds the per-GPU lnL in list
-// order -- the same value as one GPU up to the summation order (a device may
-// be listed twice: two contexts on one GPU).
+// matrices, traversal and root lnL).  The per-GPU lnL and the per-node scaler
+// totals are then summed by ONE RCCL all-reduce over the listed GPUs
+// (--reduce rccl, the default: ncclCommInitAll over the list, a grouped
+// ncclAllReduce of f64 lnL + int64[inner nodes] on the GPUs' streams,
+// plfx_rccl.hpp) -- the north star's single all-reduce over xGMI -- or, with
+// --reduce host, copied back and added on the host in list order (a device
+// may then be listed twice: two contexts on one GPU; RCCL refuses that).  The
+// reduction that ran is printed ("reduce = ...").  Same value as one GPU up
+// to the summation order.
 //
 // Prints the per-sweep device time, the node-site rate and the lnL (%.17g);
 // with the same seed, dense tips and coded tips give the identical lnL (the tip
@@ -28,14 +35,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <random>
 #include <string>
 #include <vector>
 
 #include "../../include/plfx.h"
+#include "plfx_rccl.hpp"
 
 namespace {
 
@@ -79,6 +89,7 @@ struct Opts {
   double alpha = 0.5;
   uint32_t seed = 20250117u;
   std::vector<int> devices{0};
+  bool rccl = true;  // --reduce rccl (default) | host
 };
 
 // One GPU's share: its context, its site block [off, off + n) and the device
@@ -164,7 +175,9 @@ int run(const Opts &o) {
     if (plfx_shard((uint64_t)n, nd, q, &off, &cnt) != PLFX_OK) die("too many devices for this many sites");
     p.off = (int64_t)off;
     p.n = (int64_t)cnt;
-    if (plfx_ctx_create(p.device, &p.ctx) != PLFX_OK) die("no gfx950 device " + std::to_string(p.device));
+    // DNA sweeps never use the protein tip/tip tables: no ~95 MB table pool
+    if (plfx_ctx_create_ex(p.device, S == 4 ? PLFX_CTX_LAZY_TABLES : 0u, &p.ctx) != PLFX_OK)
+      die("no gfx950 device " + std::to_string(p.device));
     HIPCHK(hipSetDevice(p.device));
     p.clv.assign(nslots, nullptr);
     p.tip.assign(nslots, nullptr);
@@ -198,6 +211,18 @@ int run(const Opts &o) {
     for (auto &e : p.ev) HIPCHK(hipEventCreate(&e));
   }
 
+  // the communicator of the one all-reduce (made before the sweeps: RCCL's
+  // setup is not part of the timed work)
+  std::unique_ptr<plfx_host::NodeComm> comm;
+  if (o.rccl) {
+    std::string err;
+    comm.reset(new plfx_host::NodeComm(o.devices, err));
+    if (!err.empty()) die(err);
+  }
+  const std::string reduce_desc =
+      o.rccl ? "rccl (" + std::to_string(nd) + " rank" + (nd > 1 ? "s" : "") + ", RCCL " +
+                   plfx_host::NodeComm::version() + ")"
+             : "host (" + std::to_string(nd) + " part" + (nd > 1 ? "s" : "") + ", list order)";
   auto sweep = [&](Part<T> &p) {  // enqueued on the part's stream, returns at once
     plfx_ctx *ctx = p.ctx;
     PLFXCHK(ctx, plfx_pmatrix(ctx, dt, S, PLFX_PMAT_STATE, p.d_eig, p.d_rates, 4, p.d_blen, 2 * nops, p.d_pm,
@@ -217,15 +242,41 @@ int run(const Opts &o) {
       HIPCHK(hipEventRecord(p.ev[i + 1], p.st));
     }
   for (auto &p : parts) HIPCHK(hipStreamSynchronize(p.st));
-  double lnl = 0.0;
+  // the one reduction of the per-GPU partials: lnL (f64) and the scaler totals
+  // of every inner node (int64)
+  double lnl = 0.0, reduce_us = 0.0;
   long long scale_events = 0;
   std::vector<int64_t> sums(nops);
-  for (auto &p : parts) {  // list order: a fixed summation order
-    double v = 0.0;
-    HIPCHK(hipMemcpy(&v, p.d_lnl, sizeof v, hipMemcpyDeviceToHost));
-    lnl += v;
-    HIPCHK(hipMemcpy(sums.data(), p.d_sums, nops * sizeof(int64_t), hipMemcpyDeviceToHost));
+  if (o.rccl) {
+    std::vector<double *> f;
+    std::vector<int64_t *> iv;
+    std::vector<hipStream_t> st;
+    for (auto &p : parts) {
+      f.push_back(p.d_lnl);
+      iv.push_back(p.d_sums);
+      st.push_back(p.st);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    const std::string err = comm->allreduce_sum(f, 1, iv, (size_t)nops, st);
+    if (!err.empty()) die(err);
+    for (auto &p : parts) HIPCHK(hipStreamSynchronize(p.st));
+    reduce_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    // every rank holds the job's totals now: rank 0's
+    HIPCHK(hipSetDevice(parts[0].device));
+    HIPCHK(hipMemcpy(&lnl, parts[0].d_lnl, sizeof lnl, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(sums.data(), parts[0].d_sums, nops * sizeof(int64_t), hipMemcpyDeviceToHost));
     for (int64_t s : sums) scale_events += s;
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (auto &p : parts) {  // list order: a fixed summation order
+      double v = 0.0;
+      HIPCHK(hipSetDevice(p.device));
+      HIPCHK(hipMemcpy(&v, p.d_lnl, sizeof v, hipMemcpyDeviceToHost));
+      lnl += v;
+      HIPCHK(hipMemcpy(sums.data(), p.d_sums, nops * sizeof(int64_t), hipMemcpyDeviceToHost));
+      for (int64_t s : sums) scale_events += s;
+    }
+    reduce_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
   }
   // a sweep's time: the slowest GPU's
   float tot_ms = 0.f, mn = 1e30f, mx = 0.f;
@@ -256,9 +307,12 @@ int run(const Opts &o) {
     std::printf("| sweep time (ms) avg / min / max | %14.4f / %10.4f / %10.4f |\n", avg, mn, mx);
     std::printf("| inner-node sites per second     | %46.4e |\n", (double)nops * n / (avg * 1e-3));
     std::printf("| scaling events (last sweep)     | %46lld |\n", scale_events);
+    std::printf("| lnL reduction / time (us)       | %32s / %11.1f |\n", reduce_desc.c_str(), reduce_us);
     std::printf("==================================================================================\n");
   }
+  std::printf("reduce = %s\n", reduce_desc.c_str());
   std::printf("lnL = %.17g\n", lnl);
+  comm.reset();  // before the streams it reduced on go away
   for (auto &p : parts) {
     HIPCHK(hipSetDevice(p.device));
     for (auto &e : p.ev) (void)hipEventDestroy(e);
@@ -275,7 +329,8 @@ int run(const Opts &o) {
 int main(int argc, char **argv) {
   if (argc < 4)
     die("usage: plfx_tree <taxa (power of 2)> <sites> <sweeps> [--dtype f32|f64] [--tips] "
-        "[--alpha A] [--seed S] [--quiet] [--states 4|20] [--fma] [--devices D0,D1,...]");
+        "[--alpha A] [--seed S] [--quiet] [--states 4|20] [--fma] [--devices D0,D1,...] "
+        "[--reduce rccl|host]");
   Opts o;
   try {
     o.taxa = std::stoi(argv[1]);
@@ -308,6 +363,11 @@ int main(int argc, char **argv) {
       if (o.states != 4 && o.states != 20) die("states must be 4 or 20");
     } else if (a == "--fma") {
       o.fma = true;
+    } else if (a == "--reduce") {
+      const std::string v = next();
+      if (v == "rccl") o.rccl = true;
+      else if (v == "host") o.rccl = false;
+      else die("bad reduction " + v + " (rccl|host)");
     } else if (a == "--devices") {
       o.devices.clear();
       const std::string v = next();

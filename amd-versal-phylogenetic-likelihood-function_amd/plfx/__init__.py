@@ -37,7 +37,7 @@ F32, F64 = 0, 1
 
 # symbols declared by include/plfx.h (checked by tests/test_abi.py)
 EXPORTS = (
-    "plfx_ctx_create", "plfx_ctx_destroy", "plfx_last_error", "plfx_get_version",
+    "plfx_ctx_create", "plfx_ctx_create_ex", "plfx_ctx_destroy", "plfx_last_error", "plfx_get_version",
     "plfx_ctx_stream", "plfx_ctx_device", "plfx_ctx_synchronize", "plfx_ctx_release_stream",
     "plfx_plf_f32", "plfx_plf_f64", "plfx_plf_dev_f32", "plfx_plf_dev_f64",
     "plfx_instance_run", "plfx_instance_run_host", "plfx_scaler_sum",
@@ -60,6 +60,7 @@ SCHED_KEYS = ("deep6", "deep5", "deep4", "septets", "triples", "unfused", "launc
 PMAT_STATE, PMAT_EIGEN = 0, 1
 EXACT, FMA = 0, 1
 PROT_CODES = 24  # protein tip codes: rows of the tip-vector table (plfx.h section 8)
+CTX_LAZY_TABLES = 1  # PLFX_CTX_LAZY_TABLES
 
 
 class PlfxError(RuntimeError):
@@ -103,6 +104,7 @@ def load():
     L = C.CDLL(str(LIB_PATH))
     vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int
     L.plfx_ctx_create.argtypes = [i32, C.POINTER(vp)]
+    L.plfx_ctx_create_ex.argtypes = [i32, C.c_uint, C.POINTER(vp)]
     L.plfx_ctx_destroy.argtypes = [vp]
     L.plfx_last_error.argtypes = [vp]
     L.plfx_last_error.restype = C.c_char_p
@@ -159,12 +161,14 @@ def load():
 
 class Context:
     """A libplfx context bound to one HIP device (replaces acap_info,
-    app/src/include.h:28-147)."""
+    app/src/include.h:28-147).  lazy_tables=True (PLFX_CTX_LAZY_TABLES, for
+    DNA-only users): the protein tip/tip tables are allocated on a stream's
+    first tip/tip call instead of with the context (~95 MB)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, lazy_tables: bool = False):
         self._L = load()
         h = C.c_void_p()
-        rc = self._L.plfx_ctx_create(int(device), C.byref(h))
+        rc = self._L.plfx_ctx_create_ex(int(device), CTX_LAZY_TABLES if lazy_tables else 0, C.byref(h))
         if rc != OK:
             raise PlfxError(rc, f"plfx_ctx_create(device={device}) failed "
                                 "(no gfx950 device visible?)")

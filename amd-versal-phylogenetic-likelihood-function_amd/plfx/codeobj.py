@@ -7,9 +7,10 @@ library it times hashes to the same value (otherwise `traffic` is null and
 `traffic_stale` true).
 
 Layout walked here (no external tools, so it runs on the GPU box as is):
-libplfx.so (ELF64) -> section `.hip_fatbin` -> clang offload bundle
-(`__CLANG_OFFLOAD_BUNDLE__`, uncompressed) -> the entry whose triple names
-gfx950 -> that code object (ELF64) -> `.symtab`.  A kernel's hash covers,
+libplfx.so (ELF64) -> section `.hip_fatbin` -> its clang offload bundles
+(`__CLANG_OFFLOAD_BUNDLE__`, uncompressed; one per HIP translation unit) ->
+the entries whose triple names gfx950 -> those code objects (ELF64) ->
+`.symtab`, merged.  A kernel's hash covers,
 for every symbol that names the kernel (its mangled identifier) (all its
 template instantiations, sorted by symbol name), the function's instruction
 bytes and its 64-byte kernel descriptor (`<sym>.kd`) with the
@@ -43,25 +44,43 @@ def _sections(elf: bytes):
     return [(name(h[0]), h[3], h[4], h[5], h[6], h[9]) for h in hdrs]
 
 
-def gfx950_code_object(lib: str | Path) -> bytes:
-    """The gfx950 code object embedded in `lib`."""
+def gfx950_code_objects(lib: str | Path) -> list[bytes]:
+    """Every gfx950 code object embedded in `lib`: the .hip_fatbin section
+    holds one clang offload bundle per HIP translation unit linked in
+    (concatenated, each aligned), walked here bundle by bundle -- a kernel
+    may live in any of them, whatever the link order.  Compressed bundles
+    (CCOB) are refused with a ValueError."""
     data = Path(lib).read_bytes()
     secs = {s[0]: s for s in _sections(data)}
     if ".hip_fatbin" not in secs:
         raise ValueError(f"{lib}: no .hip_fatbin section")
     _, _, off, size, _, _ = secs[".hip_fatbin"]
     fat = data[off:off + size]
-    if not fat.startswith(_BUNDLE_MAGIC):
-        raise ValueError(f"{lib}: .hip_fatbin is not an uncompressed offload bundle")
-    n = struct.unpack_from("<Q", fat, len(_BUNDLE_MAGIC))[0]
-    p = len(_BUNDLE_MAGIC) + 8
-    for _ in range(n):
-        eoff, esize, tlen = struct.unpack_from("<QQQ", fat, p)
-        triple = fat[p + 24:p + 24 + tlen].decode()
-        p += 24 + tlen
-        if "gfx950" in triple:
-            return fat[eoff:eoff + esize]
-    raise ValueError(f"{lib}: no gfx950 entry in the offload bundle")
+    if fat.lstrip(b"\0").startswith(b"CCOB"):
+        raise ValueError(f"{lib}: compressed offload bundle (CCOB) not supported")
+    out, pos = [], fat.find(_BUNDLE_MAGIC)
+    if pos < 0:
+        raise ValueError(f"{lib}: .hip_fatbin holds no uncompressed offload bundle")
+    while pos >= 0:
+        n = struct.unpack_from("<Q", fat, pos + len(_BUNDLE_MAGIC))[0]
+        p = pos + len(_BUNDLE_MAGIC) + 8
+        end = p
+        for _ in range(n):
+            eoff, esize, tlen = struct.unpack_from("<QQQ", fat, p)
+            triple = fat[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            end = max(end, pos + eoff + esize)
+            if "gfx950" in triple and esize:
+                out.append(fat[pos + eoff:pos + eoff + esize])
+        pos = fat.find(_BUNDLE_MAGIC, max(end, p))
+    if not out:
+        raise ValueError(f"{lib}: no gfx950 entry in the offload bundles")
+    return out
+
+
+def gfx950_code_object(lib: str | Path) -> bytes:
+    """The first gfx950 code object of `lib` (see gfx950_code_objects)."""
+    return gfx950_code_objects(lib)[0]
 
 
 def _symbols(co: bytes):
@@ -88,32 +107,41 @@ def _named(sym: str, kernel: str) -> bool:
     return f"{len(kernel)}{kernel}" in sym
 
 
+def _all_symbols(lib: str | Path):
+    """{name: (code object, type, offset, size)} over every gfx950 code object."""
+    out = {}
+    for co in gfx950_code_objects(lib):
+        for nm, typ, off, size in _symbols(co):
+            if nm not in out or (size and not out[nm][3]):
+                out[nm] = (co, typ, off, size)
+    return out
+
+
 def kernel_code_sha256(lib: str | Path, kernel: str) -> str:
     """sha256 over every instantiation of `kernel` (base name, e.g.
-    "plf_dna_f64_pair_kernel") in `lib`'s gfx950 code object: instruction
+    "plf_dna_f64_pair_kernel") in `lib`'s gfx950 code objects: instruction
     bytes + kernel descriptor (entry offset zeroed), by symbol name."""
-    co = gfx950_code_object(lib)
-    syms = {nm: (typ, off, size) for nm, typ, off, size in _symbols(co)}
-    funcs = sorted(nm for nm, (typ, _, size) in syms.items()
+    syms = _all_symbols(lib)
+    funcs = sorted(nm for nm, (_, typ, _, size) in syms.items()
                    if _named(nm, kernel) and typ == 2 and size > 0)  # STT_FUNC
     if not funcs:
         raise KeyError(f"no kernel named *{kernel}* in {lib}")
     h = hashlib.sha256()
     for nm in funcs:
-        _, off, size = syms[nm]
+        co, _, off, size = syms[nm]
         h.update(nm.encode() + b"\0")
         h.update(co[off:off + size])
         kd = syms.get(nm + ".kd")
         if kd is not None:
-            b = bytearray(co[kd[1]:kd[1] + kd[2]])
+            b = bytearray(kd[0][kd[2]:kd[2] + kd[3]])
             b[16:24] = bytes(8)  # kernel_code_entry_byte_offset: where the linker put it
             h.update(bytes(b))
     return h.hexdigest()
 
 
 def kernel_instantiations(lib: str | Path, kernel: str) -> list[str]:
-    co = gfx950_code_object(lib)
-    return sorted(nm for nm, typ, _, size in _symbols(co) if _named(nm, kernel) and typ == 2 and size > 0)
+    return sorted(nm for nm, (_, typ, _, size) in _all_symbols(lib).items()
+                  if _named(nm, kernel) and typ == 2 and size > 0)
 
 
 def default_lib() -> Path:

@@ -69,13 +69,13 @@
  * the pool.  A hipStreamPerThread workspace whose thread exits without
  * releasing it is retired too, and reclaimed (after a device-wide wait, not
  * inside a capture) when the context runs out of workspaces.
- * plfx_ctx_destroy() waits for the context's stream and for every other
- * stream still holding a workspace -- so such streams must still exist at
- * destroy; release them first otherwise -- and waits for the whole device
+ * plfx_ctx_destroy() waits for the context's stream and for the last work of
+ * every workspace still held, through an event the library records after each
+ * call that used it (never through the caller's stream handle: that stream
+ * may already be destroyed); it waits for the whole device
  * (hipDeviceSynchronize, which must not overlap a global-mode capture in
- * another thread) only when a workspace was used under a capture, is retired,
- * or belongs to another thread's hipStreamPerThread.  Graph replays still in
- * flight must finish before destroy.
+ * another thread) only when a workspace was used under a capture.  Graph
+ * replays still in flight must finish before destroy.
  * The same workspace also holds the tile/chunk queues of the protein f64 FMA
  * kernel (from 2^20 sites) and of the fused six-level tree passes: blocks or
  * waves that run ahead take more of the alignment instead of a fixed share
@@ -89,7 +89,10 @@
  * No allocation happens per call after warm-up (the host entry points keep
  * grow-only staging buffers in the context).  Each workspace also holds the
  * protein tip/tip combination tables (about 11.8 MB; the pool's
- * PLFX_WS_POOL of them are allocated with the context).
+ * PLFX_WS_POOL of them, ~95 MB, are allocated with the context).  A context
+ * created with PLFX_CTX_LAZY_TABLES (DNA-only users) allocates a workspace's
+ * tables on its first protein tip/tip call instead; that first call may then
+ * not be inside a capture (PLFX_ERR_INVALID).
  * Every entry point rejects a parent CLV x3 that shares any byte with a child
  * it reads (PLFX_ERR_INVALID).
  *
@@ -110,7 +113,7 @@
 extern "C" {
 #endif
 
-#define PLFX_VERSION 10100 /* 1.1.0 */
+#define PLFX_VERSION 10200 /* 1.2.0 */
 #define PLFX_MAX_STREAMS 64 /* streams holding a workspace at a time, per context */
 #define PLFX_WS_POOL 8      /* workspaces allocated with the context */
 
@@ -136,6 +139,10 @@ typedef struct plfx_ctx plfx_ctx;
 /* Replaces acap_info (app/src/include.h:28-147): binds a HIP device and owns
  * a non-blocking stream, the scaler-sum workspace and host staging buffers. */
 int plfx_ctx_create(int device, plfx_ctx **ctx);
+/* flags: 0 (= plfx_ctx_create) or PLFX_CTX_LAZY_TABLES (see "Streams and the
+ * scaler-sum workspace"); other bits are PLFX_ERR_INVALID. */
+#define PLFX_CTX_LAZY_TABLES 1u
+int plfx_ctx_create_ex(int device, unsigned flags, plfx_ctx **ctx);
 int plfx_ctx_destroy(plfx_ctx *ctx);
 const char *plfx_last_error(const plfx_ctx *ctx);
 int plfx_get_version(void);

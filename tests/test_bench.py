@@ -161,3 +161,55 @@ def test_code_hash_names_kernels_exactly():
         lib, "plf_dna_f64_pair_kernel")
     ok, why = codeobj.check_stamp({"no_such_kernel": "0" * 64}, lib)
     assert not ok and "no_such_kernel" in why
+
+
+def test_codeobj_walks_every_bundle(tmp_path):
+    """the .hip_fatbin section holds one offload bundle per HIP
+    translation unit; a kernel in a later bundle must resolve.  A synthetic
+    library whose .hip_fatbin puts a padded host-only bundle in front of the
+    real one still resolves every kernel to the same hash."""
+    import struct
+
+    from plfx import codeobj
+
+    lib = codeobj.default_lib()
+    data = bytearray(lib.read_bytes())
+    name, addr, off, size, _, _ = next(s for s in codeobj._sections(bytes(data)) if s[0] == ".hip_fatbin")
+    fat = bytes(data[off:off + size])
+    # a first bundle with only a host entry, padded to 4096, then the real one
+    host = b"host-x86_64-unknown-linux-gnu-"
+    hdr = codeobj._BUNDLE_MAGIC + struct.pack("<Q", 1) + struct.pack("<QQQ", 4096, 0, len(host)) + host
+    first = hdr + bytes(4096 - len(hdr))
+    # splice: the new section content replaces the old at the same offset,
+    # appended at the end of the file with the section header pointed there
+    new = first + fat
+    shoff = struct.unpack_from("<Q", data, 0x28)[0]
+    shentsize, shnum, _ = struct.unpack_from("<HHH", data, 0x3A)
+    for i in range(shnum):
+        h = shoff + i * shentsize
+        if struct.unpack_from("<Q", data, h + 24)[0] == off and struct.unpack_from("<Q", data, h + 32)[0] == size:
+            struct.pack_into("<QQ", data, h + 24, len(data), len(new))
+    data += new
+    p = tmp_path / "libtwo.so"
+    p.write_bytes(bytes(data))
+    assert len(codeobj.gfx950_code_objects(p)) == 1
+    for k in ("plf_dna_f64_pair_kernel", "plf_dna_kernel", "root_lnl_kernel"):
+        assert codeobj.kernel_code_sha256(p, k) == codeobj.kernel_code_sha256(lib, k)
+
+
+def test_every_stamped_kernel_resolves():
+    """Every kernel named in a committed PMC record's code stamp
+    (profiles/*_pmc_traffic.json) names code that exists in the library's
+    gfx950 code objects (its hash may differ when the kernel changed)."""
+    import json
+
+    from plfx import codeobj
+
+    lib = codeobj.default_lib()
+    seen = 0
+    for path in sorted((ROOT / "profiles").glob("*_pmc_traffic.json")):
+        code = json.loads(path.read_text()).get("code") or {}
+        for k in code:
+            assert codeobj.kernel_instantiations(lib, k), (path.name, k)
+            seen += 1
+    assert seen > 0

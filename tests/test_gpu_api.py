@@ -602,6 +602,103 @@ def test_destroy_waits_for_its_streams_not_the_device(oracle):
     torch.cuda.synchronize()
 
 
+def test_destroy_after_the_callers_stream_is_gone(oracle):
+    """a stream that still holds a workspace may be
+    destroyed by its owner before the context is (e.g. a Context collected at
+    interpreter exit).  plfx_ctx_destroy waits for the workspace's last work
+    through the library's own event and never touches the dead handle: the
+    close returns, the sums of the stream's launches are complete, and a new
+    context on the same device works."""
+    import plfx
+    import torch
+
+    n = 1 << 18
+    d = oracle.gen_hostmem(n, np.float64, 53)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    _, _, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+    o3 = torch.empty_like(t["x1"])
+    s = torch.zeros(6, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    c = plfx.Context(0)
+    hs = _new_streams(3)
+    for i, h in enumerate(hs):  # every stream takes a workspace, none is released
+        for j in range(2):
+            c.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None,
+                      s[2 * i + j:2 * i + j + 1], stream=h)
+    _destroy_streams(hs)  # owner destroys them while their work may still run
+    c.close()
+    assert s.tolist() == [einc] * 6
+    with plfx.Context(0) as c2:
+        s2 = torch.zeros(1, dtype=torch.int64, device="cuda")
+        c2.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s2)
+        torch.cuda.synchronize()
+        assert int(s2.item()) == einc
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_lazy_tables_context(oracle, dtype):
+    """plfx_ctx_create_ex(PLFX_CTX_LAZY_TABLES) skips the ~95 MB of
+    protein tip/tip tables at creation (DNA-only users).  DNA works as
+    before; a stream's FIRST tip/tip protein call inside a capture is refused
+    with PLFX_ERR_INVALID (its tables would be allocated then); the same call
+    outside a capture allocates them and is bit-exact, and later captures on
+    that stream work."""
+    import plfx
+    import torch
+
+    free0 = torch.cuda.mem_get_info()[0]
+    S, n = 20, 3001
+    rng = np.random.default_rng(9)
+    EV = (rng.random(S * S) - 0.25).astype(dtype)
+    left = (rng.random(4 * S * S) * 1e-11).astype(dtype)
+    right = rng.random(4 * S * S).astype(dtype)
+    w = rng.integers(1, 5, n).astype(np.int32)
+    c1, c2 = oracle.random_protein_codes(rng, n, 0.3), oracle.random_protein_codes(rng, n, 0.3)
+    e1, e2 = oracle.expand_protein_tips(c1, dtype), oracle.expand_protein_tips(c2, dtype)
+    f3, fsc, finc = oracle.plf_generic(S, 4, e1, e2, EV, left, right, w, fma=True)
+    t = [dev(a) for a in (c1, c2, EV, left, right, w)]
+    x3 = torch.empty(4 * S * n, dtype=t[2].dtype, device="cuda")
+    sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with plfx.Context(0, lazy_tables=True) as c:
+        assert free0 - torch.cuda.mem_get_info()[0] < 64 << 20  # no 95-MB table pool
+        d = oracle.gen_hostmem(4099, dtype, 54)
+        x = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+        e3, _, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+        o3, s0 = torch.empty_like(x["x1"]), torch.zeros(1, dtype=torch.int64, device="cuda")
+        c.plf_dev(x["x1"], x["x2"], o3, x["EV"], x["left"], x["right"], x["wgt"], None, s0, stream=st)
+        st.synchronize()
+        assert np.array_equal(bits(o3.cpu().numpy()), bits(e3)) and int(s0.item()) == einc
+
+        def call():
+            c.plf_tips_dev(x3, t[2], n, t[3], t[4], tip1=t[0], tip2=t[1], wgt=t[5], scaler=sc,
+                           scaler_sum=s, states=S, fma=True, stream=st)
+
+        g = torch.cuda.CUDAGraph()
+        with pytest.raises(plfx.PlfxError) as ei:
+            with torch.cuda.graph(g, stream=st):
+                call()
+        assert ei.value.code == plfx.ERR_INVALID and "LAZY_TABLES" in str(ei.value)
+        del g
+        torch.cuda.synchronize()
+        call()  # outside a capture: allocates this stream's tables
+        st.synchronize()
+        assert np.array_equal(bits(x3.cpu().numpy()), bits(f3))
+        assert np.array_equal(sc.cpu().numpy(), fsc) and int(s.item()) == finc
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            call()
+        x3.zero_()
+        s.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(x3.cpu().numpy()), bits(f3)) and int(s.item()) == finc
+        del g
+
+
 def test_release_after_capture_retires_the_workspace(oracle):
     """releasing a stream whose workspace a graph was
     captured through must not hand that workspace to another stream -- the

@@ -351,7 +351,8 @@ def test_host_driver_end_to_end(oracle, tmp_path):
     inputs (std::mt19937, same seed).  --no-intermediate is the reference's
     NO_INTERMEDIATE_RESULTS mode (host_mem.cpp:327-392,454-468) and --csv its
     write_to_csv (timing.h:153-194); --devices spreads the instances over a
-    GPU list, one context per entry."""
+    GPU list, one context per entry; --reduce rccl replaces the host scaler
+    loop by per-instance device sums and ONE RCCL all-reduce."""
     exe = PKG / "build" / "plfx_host"
     assert exe.exists()
     cases = ((np.float32, ["--dtype", "f32", "--layout", "comb", "--window", "1024"], False),
@@ -361,7 +362,12 @@ def test_host_driver_end_to_end(oracle, tmp_path):
              # instances over a GPU list (one context per entry; the box has one GPU,
              # so two contexts on it): instances 0 and 2 on context 0, 1 on context 1
              (np.float64, ["--dtype", "f64", "--layout", "sep", "--window", "8192", "--devices", "0,0"], False),
-             (np.float32, ["--dtype", "f32", "--layout", "comb", "--window", "1024", "--devices", "0,0"], True))
+             (np.float32, ["--dtype", "f32", "--layout", "comb", "--window", "1024", "--devices", "0,0"], True),
+             # the scaler totals through ONE RCCL all-reduce (world 1 on the box)
+             # instead of the host loop, in both run modes
+             (np.float64, ["--dtype", "f64", "--layout", "sep", "--window", "8192", "--devices", "0",
+                           "--reduce", "rccl"], False),
+             (np.float64, ["--dtype", "f64", "--layout", "comb", "--window", "8192", "--reduce", "rccl"], True))
     for ci, (dtype, args, noint) in enumerate(cases):
         n, calls, P = 3001, 2, 3
         pre = str(tmp_path / f"out{ci}_{np.dtype(dtype).name}")
@@ -398,6 +404,10 @@ def test_host_driver_end_to_end(oracle, tmp_path):
         # the driver's own check (host_mem.cpp:403-442): CPU plf() vs the GPU, exact
         assert "Test result: Passed" in r.stdout
         assert "Reference (CPU plf" in r.stdout and "Speed up (excluding transfers)" in r.stdout
+        assert ("reduce = rccl (1 rank, RCCL " if "rccl" in args else "reduce = host (") in r.stdout
+    bad = subprocess.run([str(exe), "3001", "1", "2", "--devices", "0,0", "--reduce", "rccl"],
+                         capture_output=True, text=True, timeout=120)
+    assert bad.returncode != 0 and "distinct GPUs" in bad.stderr  # refused, not a silent host sum
 
 
 def test_dropin_header_reference_call(tmp_path):
