@@ -37,10 +37,11 @@ constexpr int kHostChunksMax = 16;
 // returns an entry to the pool -- unless a graph was captured through it: the
 // graph's replays keep using the entry's words, so it is retired (never handed
 // to another stream) and the context waits for the device when destroyed.
-// Every call that used an entry outside a capture records the entry's `done`
-// event on its stream after its launches (WsDone), so plfx_ctx_destroy waits
-// for an entry's last work through that event and never touches a caller's
-// stream handle (which may no longer exist).
+// plfx_ctx_destroy never touches a caller's stream handle (the stream may be
+// gone by then): an entry still held by a stream other than the context's is
+// waited for device-wide.  (An event recorded after each call cannot stand
+// in: HIP rejects waiting on an event whose stream was destroyed -- an exited
+// thread's hipStreamPerThread gave hipErrorCapturedEvent (907) on the box.)
 struct StreamWs {
   hipStream_t stream = nullptr;
   std::thread::id tid;               // owning thread for hipStreamPerThread, else none
@@ -48,7 +49,6 @@ struct StreamWs {
   bool captured = false;             // used while its stream was capturing
   bool retired = false;              // released after a capture, or its thread exited
   bool cap_now = false;              // the current call's stream is capturing
-  hipEvent_t done = nullptr;         // recorded after each uncaptured call's launches
   unsigned long long *ws = nullptr;  // kWsRegions x kWsWords u64
   double *lnl_partials = nullptr;    // kLnlMaxGrid doubles
   unsigned long long *lnl_ticket = nullptr;
@@ -221,7 +221,7 @@ StreamWs *ws_take(plfx_ctx *ctx, StreamWs &w, hipStream_t s) {
 }
 
 // The workspace of stream s: its own, else a free pool entry (zero at rest),
-// else a retired per-thread entry reclaimed after its `done` event,
+// else a retired per-thread entry reclaimed after a device synchronisation,
 // else a new allocation (zeroed in order on s) -- neither of the last two
 // inside a stream capture.  An entry used while s is capturing is marked: the
 // graph keeps using it after the capture.
@@ -237,18 +237,24 @@ StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
       }
   if (!got && !cap) {
     // entries of exited threads' per-thread streams (not captured: those
-    // stay retired): their last launches must be done before reuse -- waited
-    // for through the entry's event (the thread's stream is gone)
-    for (StreamWs &w : ctx->wss)
-      if (w.in_use && w.retired && !w.captured) {
-        hipError_t e = hipEventSynchronize(w.done);
-        if (e != hipSuccess) {
-          *rc = hip_fail(ctx, e, "reclaiming the workspace of an exited thread");
-          return nullptr;
-        }
-        w.in_use = false;
-        if (!got) got = ws_take(ctx, w, s);
+    // stay retired): their last launches must be done before reuse, and the
+    // thread's stream is gone -- so the device is waited for
+    bool any = false;
+    for (StreamWs &w : ctx->wss) any |= w.in_use && w.retired && !w.captured;
+    if (any) {
+      hipError_t e = hipDeviceSynchronize();
+      if (e != hipSuccess) {
+        *rc = hip_fail(ctx, e, "reclaiming workspaces of exited threads");
+        return nullptr;
       }
+      for (StreamWs &w : ctx->wss)
+        if (w.in_use && w.retired && !w.captured) w.in_use = false;
+      for (StreamWs &w : ctx->wss)
+        if (!w.in_use) {
+          got = ws_take(ctx, w, s);
+          break;
+        }
+    }
   }
   if (got) {
     got->captured = got->captured || cap;
@@ -272,43 +278,23 @@ StreamWs *ws_for(plfx_ctx *ctx, hipStream_t s, int *rc) {
   // wait for the whole device)
   void *block = nullptr;
   const size_t bytes = kWsEntryBytes + (ctx->lazy_tables ? 0 : kTtEntryBytes);
-  hipEvent_t done = nullptr;
-  hipError_t e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+  hipError_t e = hipMallocAsync(&block, bytes, s);
   if (e != hipSuccess) {
-    *rc = hip_fail(ctx, e, "workspace event");
-    return nullptr;
-  }
-  e = hipMallocAsync(&block, bytes, s);
-  if (e != hipSuccess) {
-    (void)hipEventDestroy(done);
     *rc = fail(ctx, PLFX_ERR_NOMEM, "workspace hipMallocAsync(%zu): %s", bytes, hipGetErrorString(e));
     return nullptr;
   }
   e = hipMemsetAsync(block, 0, kWsEntryBytes, s);
   if (e != hipSuccess) {
     (void)hipFreeAsync(block, s);
-    (void)hipEventDestroy(done);
     *rc = hip_fail(ctx, e, "workspace memset");
     return nullptr;
   }
   ctx->ws_blocks.push_back(block);
   StreamWs w;
   ws_carve(w, block, ctx->lazy_tables ? nullptr : static_cast<char *>(block) + kWsEntryBytes);
-  w.done = done;
   ctx->wss.push_back(w);
   return ws_take(ctx, ctx->wss.back(), s);
 }
-
-// Records the entry's `done` event on the call's stream when the call's
-// launches are issued (at scope exit), unless the stream is capturing: a
-// captured entry's work belongs to the graph and is waited for device-wide.
-struct WsDone {
-  StreamWs *w;
-  hipStream_t s;
-  ~WsDone() {
-    if (w && w->done && !w->cap_now) (void)hipEventRecord(w->done, s);
-  }
-};
 
 // the workspace of stream s as `out`; returns from the caller on failure
 #define PLFX_WS(ctx, s, out)                      \
@@ -317,8 +303,7 @@ struct WsDone {
     int wrc_ = PLFX_OK;                           \
     out = ws_for((ctx), (s), &wrc_);              \
     if (!out) return wrc_;                        \
-  } while (0);                                    \
-  WsDone out##_done_{out, (s)}
+  } while (0)
 
 // [a, a + na) and [b, b + nb) share a byte
 bool overlap(const void *a, size_t na, const void *b, size_t nb) {
@@ -638,8 +623,6 @@ int plfx_ctx_create_ex(int device, unsigned flags, plfx_ctx **out) {
   // the workspace pool: kWsPool entries (reduction words zeroed before return,
   // tip/tip tables), and the tables' constant code arrays
   auto undo = [&](int code) {
-    for (StreamWs &w : ctx->wss)
-      if (w.done) (void)hipEventDestroy(w.done);
     for (void *b : ctx->ws_blocks) (void)hipFreeAsync(b, ctx->stream);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -670,8 +653,6 @@ int plfx_ctx_create_ex(int device, unsigned flags, plfx_ctx **out) {
     ws_carve(w, static_cast<char *>(pool) + i * kWsEntryBytes,
              tabs ? static_cast<char *>(tabs) + i * kTtEntryBytes : nullptr);
     ctx->wss.push_back(w);
-    if (hipEventCreateWithFlags(&ctx->wss.back().done, hipEventDisableTiming) != hipSuccess)
-      return undo(PLFX_ERR_HIP);
   }
   {
     std::lock_guard<std::mutex> l(g_live_mu);
@@ -702,20 +683,17 @@ int plfx_ctx_destroy(plfx_ctx *ctx) {
     if (ctx->d_buf) (void)hipFreeAsync(ctx->d_buf, ctx->stream);
     for (hipEvent_t e : ctx->chunk_done)
       if (e) (void)hipEventDestroy(e);
-    // Workspace entries still held: their last launches must be done before
-    // the free.  Each is waited for through its own `done` event, recorded
-    // after every uncaptured call that used it -- never through the caller's
-    // stream handle, which may already be destroyed.  Only an entry used under
-    // a capture (the graph may still replay on any stream) needs the device.
+    // Workspace entries still held by a stream other than the context's:
+    // their last launches must be done before the free.  The caller's stream
+    // handle is never used here -- the stream may already be destroyed (e.g.
+    // a context collected after its user's streams) -- so the device is
+    // waited for; releasing streams (plfx_ctx_release_stream) before destroy
+    // avoids that wait.  An entry used under a capture needs it anyway (its
+    // graph may still be replaying on any stream).
     bool device_wide = false;
-    for (StreamWs &w : ctx->wss) {
-      if (!w.in_use) continue;
-      if (w.captured) device_wide = true;
-      else if (w.done) (void)hipEventSynchronize(w.done);
-    }
-    if (device_wide) (void)hipDeviceSynchronize();
     for (StreamWs &w : ctx->wss)
-      if (w.done) (void)hipEventDestroy(w.done);
+      if (w.in_use && (w.captured || w.retired || w.stream != ctx->stream)) device_wide = true;
+    if (device_wide) (void)hipDeviceSynchronize();
     for (void *b : ctx->ws_blocks) (void)hipFreeAsync(b, ctx->stream);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -977,14 +955,10 @@ int plfx_traverse_tips(plfx_ctx *ctx, int dtype, int states, int flags, const pl
   }
   hipStream_t s = pick(ctx, stream);
   unsigned long long *ws = nullptr;
-  StreamWs *tw = nullptr;
   if (nops > 0 && n > 0) {
-    int wrc = PLFX_OK;
-    tw = ws_for(ctx, s, &wrc);
-    if (!tw) return wrc;
-    ws = tw->ws;
+    PLFX_WS(ctx, s, w);
+    ws = w->ws;
   }
-  WsDone tw_done_{tw, s};  // after every launch of the traversal
   const char *pm = static_cast<const char *>(pmats);
   // the node descriptor of op j, tip child first (dense/tip runs as tip/dense:
   // the product u1*u2 commutes exactly); *kind = number of tip children

@@ -69,12 +69,12 @@
  * the pool.  A hipStreamPerThread workspace whose thread exits without
  * releasing it is retired too, and reclaimed (after a device-wide wait, not
  * inside a capture) when the context runs out of workspaces.
- * plfx_ctx_destroy() waits for the context's stream and for the last work of
- * every workspace still held, through an event the library records after each
- * call that used it (never through the caller's stream handle: that stream
- * may already be destroyed); it waits for the whole device
- * (hipDeviceSynchronize, which must not overlap a global-mode capture in
- * another thread) only when a workspace was used under a capture.  Graph
+ * plfx_ctx_destroy() waits for the context's stream; if a stream other than
+ * the context's still holds a workspace, or one was used under a capture, it
+ * waits for the whole device (hipDeviceSynchronize, which must not overlap a
+ * global-mode capture in another thread) -- it never uses a caller's stream
+ * handle, which may already be destroyed.  Release streams before destroy
+ * (plfx_ctx_release_stream) to keep destroy off the device-wide wait.  Graph
  * replays still in flight must finish before destroy.
  * The same workspace also holds the tile/chunk queues of the protein f64 FMA
  * kernel (from 2^20 sites) and of the fused six-level tree passes: blocks or

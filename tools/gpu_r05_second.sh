@@ -19,7 +19,7 @@ step() {  # name, limit, command...
   return 0
 }
 cd $R
-step pytest_new 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_api.py -k "destroy_after or lazy_tables" tests/test_gpu_tree.py -k "rccl or driver_end" tests/test_gpu_parity.py::test_host_driver_end_to_end
+step pytest_new 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_api.py -k "destroy or lazy_tables or exited_threads or rccl or driver_end" tests/test_gpu_tree.py tests/test_gpu_parity.py::test_host_driver_end_to_end
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread
 step valu_probe 240 ./build/valu_f64
 step sweep 300 python -u bench.py --sweep
