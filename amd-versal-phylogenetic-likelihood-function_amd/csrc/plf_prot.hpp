@@ -22,7 +22,7 @@
 // (*_batch_kernel: node = blockIdx.y, plf_dna.hpp NodeBatch).
 // The measured-and-not-adopted forms and knobs (the round-1 readlane kernel,
 // ablations, swizzles, rings, SGPR operands, ...) live in the tuning copy
-// tools/plf_prot_tune.hpp@f9b3af3; DESIGN.md section 3.3 has the measurements.
+// tools/plf_prot_tune.hpp@f9b3af3; HISTORY.md section 3.3 has the measurements.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -319,7 +319,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
         for (int j = 0; j < RV; j++) ring[l][j] = G[o + l * RV + j];
 #pragma unroll
       for (int l = 0; l < S; l++) {
-        asm volatile("" : "+v"(o) : "v"(tok));  // column l+kDist is read after column l-1 is used
+        __builtin_amdgcn_sched_barrier(0);  // column l+kDist is read after column l-1 is used
         if (l + kDist < S) {
 #pragma unroll
           for (int j = 0; j < RV; j++) ring[(l + kDist) % (kDist + 1)][j] = G[o + (l + kDist) * RV + j];
@@ -455,10 +455,15 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
     __syncthreads();  // also: every wave is done reading x2 from the tile
     const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
     const bool sc = (all >> lane) & 1ull;
+    // x 2^32 on a scaled site as one v_ldexp by 32 or 0 per value (exact
+    // either way: the same bits as the multiply-and-select, one VALU
+    // instruction per value instead of three)
+    int e = sc ? 32 : 0;
+    asm volatile("" : "+v"(e));  // else LLVM turns it back into ldexp(O, 32) + select
 #pragma unroll
     for (int l = 0; l < S; l++) {
-      const T sv = O[l] * Num<T>::two32();
-      O[l] = sc ? sv : O[l];
+      if constexpr (sizeof(T) == 8) O[l] = ldexp(O[l], e);
+      else O[l] = ldexpf(O[l], e);
     }
     row_write<T>(tile, lane, c, O);
     const int64_t site = base + lane;

@@ -571,7 +571,7 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
   // 32 neighbouring allocations of 128 MiB ran up to 15 % slower than a mixed
   // one while each of its nodes alone ran at the same speed (nodes512 at N = 1:
   // launches of 2.09-2.48 ms consecutive, 2.10-2.12 ms interleaved;
-  // tools/probes/nodes_groups.py, nodes_sched.py).
+  // tools/probes/nodes_groups.py, nodes_sched.py, HISTORY.md section 5).
   const int L = (count + plfx::kMaxBatch - 1) / plfx::kMaxBatch;
   const plfx::NodeDescH *all = reinterpret_cast<const plfx::NodeDescH *>(nodes);
   for (int j = 0; j < L; j++) {

@@ -98,7 +98,7 @@
  *
  * Timing note: after an idle gap of ~0.3 s or more the MI355X lowers its
  * shader clock to ~1.8-2.0 GHz for the first ~10-15 ms of renewed load
- * (DVFS; measured in-kernel).  HBM-bound calls (DNA)
+ * (DVFS; measured in-kernel, HISTORY.md section 3.3).  HBM-bound calls (DNA)
  * run <= 4 % slower through it, the protein matrix-core kernels ~10 %.  It
  * is a property of the device's power management, not of a context or a
  * process, so no library-side warm-up can absorb it.

@@ -1,9 +1,9 @@
-// prot_wt.hpp -- (measured, not adopted: DESIGN.md section 3.3, round 4) exact-mode protein (S = 20, C = 4) node update with
+// prot_wt.hpp -- (measured, not adopted: HISTORY.md section 3.3, round 4) exact-mode protein (S = 20, C = 4) node update with
 // wave-private site tiles: plf()'s loop (app/src/plf.cpp:19-65, 4 -> 20
 // states) with separate multiplies and adds in its order, bit-identical to
 // plf_prot_lds_kernel and to the double / float instantiation of the loop.
 //
-// Why a second form: plf_prot_lds_kernel
+// Why a second form (HISTORY.md section 3.3, round 4): plf_prot_lds_kernel
 // runs one category per wave over a 64-site block tile, so every child tile and
 // the 80-value scale test cross the block's four waves through LDS barriers,
 // and its 42-KB tile plus a 28.8-KB matrix copy per block hold the CU to two
@@ -22,7 +22,7 @@
 //     category copies 816 dwords apart (= 48 mod 64: four disjoint bank sets
 //     in a ds_read_b128 lane group); tile rows 44 chunks of 16 B per site,
 //     categories 11 chunks apart: every row read, row write and staging access
-//     of the lane map is conflict-free (bank model: DESIGN.md section 3.3).
+//     of the lane map is conflict-free (bank model: HISTORY.md section 3.3).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
