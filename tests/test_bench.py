@@ -213,3 +213,36 @@ def test_every_stamped_kernel_resolves():
             assert codeobj.kernel_instantiations(lib, k), (path.name, k)
             seen += 1
     assert seen > 0
+
+
+def test_launch_check_against_record_shapes():
+    """a PMC record counts only for the dispatch it measured --
+    the timed graph's kernel nodes (mangled names, grid and workgroup sizes)
+    must dispatch the record's kernels with the recorded shapes."""
+    mangled = "_ZN4plfx3dev23plf_dna_f64_pair_kernelILi2ELb1ELi1ELb1EEEvPKdS3_Pd"
+    rec = {"plf_dna_f64_pair_kernel": [[262144, 256]]}
+    ok, why = bench.launch_check(rec, [(mangled, 262144, 256)] * 20)
+    assert ok and "counted grid" in why
+    ok, why = bench.launch_check(rec, [(mangled, 131072, 256)])
+    assert not ok and "dispatched as" in why
+    ok, why = bench.launch_check(rec, [("_ZN4plfx3dev14plf_dna_kernelIfEEvv", 262144, 256)])
+    assert not ok and "not dispatched" in why
+    assert bench.launch_check(None, [(mangled, 1, 1)])[0]          # old record: not checked
+    assert bench.launch_check(rec, None)[0]                        # no graph: not checked
+
+
+def test_pmc_tools_record_launch_shapes():
+    """The PMC record tools read the dispatch shapes from rocprofv3's counter
+    CSV (demangled or truncated kernel names), as bench.py compares them."""
+    import importlib.util
+
+    def load(name):
+        spec = importlib.util.spec_from_file_location(name, ROOT / "tools" / f"{name}.py")
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        return m
+
+    pt, ps = load("pmc_traffic"), load("pmc_step")
+    assert pt.shapes(ROOT / "profiles" / "r04_node_pmc_fetch.csv", "plf_dna_f64_pair_kernel") == [[262144, 256]]
+    tree = ps.launch_shapes(ROOT / "profiles" / "r04_tree64_pmc_fetch.csv")
+    assert tree["plf_dna_f64_deep_kernel"] == [[131072, 512]]

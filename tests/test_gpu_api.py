@@ -528,6 +528,41 @@ def test_tiptip_tables_on_a_first_call_inside_capture(oracle, dtype):
         del g
 
 
+def test_graph_kernel_launches_names_the_dispatch(ctx, oracle):
+    """bench.graph_kernel_launches reads a captured graph's kernel nodes: the
+    headline node call is one plf_dna_f64_pair_kernel dispatch of 256-thread
+    workgroups over the co-resident grid -- what bench.py checks a PMC
+    record's launch shapes against."""
+    import sys
+
+    import torch
+
+    from conftest import ROOT
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+    from plfx import codeobj
+
+    n = 1 << 16
+    d = oracle.gen_hostmem(n, np.float64, 55)
+    t = {k: dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    o3 = torch.empty_like(t["x1"])
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st = torch.cuda.Stream()
+    ctx.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s, stream=st)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g, stream=st):
+        for _ in range(3):
+            ctx.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s, stream=st)
+    ls = bench.graph_kernel_launches(g)
+    assert len(ls) == 3 and all(nm and codeobj._named(nm, "plf_dna_f64_pair_kernel") for nm, _, _ in ls)
+    assert {w for _, _, w in ls} == {256} and len({gsz for _, gsz, _ in ls}) == 1
+    ok, _ = bench.launch_check({"plf_dna_f64_pair_kernel": [[ls[0][1], 256]]}, ls)
+    assert ok
+    del g
+
+
 def test_x3_partial_overlap_rejected(ctx):
     """a parent CLV sharing ANY byte with a child is
     refused (PLFX_ERR_INVALID) on every device entry point -- not only

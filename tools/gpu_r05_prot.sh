@@ -18,7 +18,7 @@ step() {  # name, limit, command...
   return 0
 }
 cd $R
-step pytest_protein 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_protein.py tests/test_gpu_api.py -k "protein or Protein or prot"
+step pytest_protein 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_protein.py tests/test_gpu_api.py -k "protein or Protein or prot or graph_kernel"
 for r in 1 2 3; do
   for v in old ldexp new; do
     step time_${v}_$r 120 ./build/time_prot_exact_$v $v

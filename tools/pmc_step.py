@@ -26,6 +26,18 @@ import statistics as st
 PLF_KERNELS = ("plf_dna", "root_lnl", "plf_prot", "pmatrix", "prot_tiptip")
 
 
+def launch_shapes(path, exclude=()):
+    """{kernel: [[grid size, workgroup size], ...]} of the PLF dispatches."""
+    g = collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        nm = r["Kernel_Name"]
+        if not nm.startswith(PLF_KERNELS) or nm.startswith(tuple(exclude)):
+            continue
+        base = nm.split("(")[0].split("<")[0].split("::")[-1]
+        g[base].add((int(r["Grid_Size"]), int(r["Workgroup_Size"])))
+    return {k: sorted([a, b] for a, b in v) for k, v in g.items()}
+
+
 def groups(path, name, exclude=()):
     g = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
@@ -64,6 +76,8 @@ def main():
         rec["key"] = a.key
     # ties the record to the machine code it was counted on (bench.py checks it)
     rec["code"] = codeobj.stamp([r["kernel"] for r in rows])
+    # and the dispatch shapes it was counted with (bench.py checks the timed graph's)
+    rec["launch"] = launch_shapes(a.fetch, a.exclude)
     json.dump(rec, open(a.out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
