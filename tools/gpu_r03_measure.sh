@@ -31,9 +31,9 @@ small() {  # copy a file to OUT if it is under 8 MB
 cd $R
 step bench 400 python -u $R/bench.py "$@"
 cd /tmp && export TMPDIR=/tmp
-step trace 400 rocprofv3 --kernel-trace --stats -T -d $TMPP/trace -o run --output-format csv -- python3 $R/bench.py "$@" --no-cpu-baseline
-step fetch 400 rocprofv3 --pmc FETCH_SIZE -T -d $TMPP/fetch -o run --output-format csv -- python3 $R/bench.py "$@" --no-cpu-baseline --no-second-region --steps $P --warmup 2 --launch bound
-step write 400 rocprofv3 --pmc WRITE_SIZE -T -d $TMPP/write -o run --output-format csv -- python3 $R/bench.py "$@" --no-cpu-baseline --no-second-region --steps $P --warmup 2 --launch bound
+step trace 400 rocprofv3 --kernel-trace --stats -T -d $TMPP/trace -o run --output-format csv -- python3 $R/bench.py "$@" --no-cpu-baseline --no-nodes512
+step fetch 400 rocprofv3 --pmc FETCH_SIZE -T -d $TMPP/fetch -o run --output-format csv -- python3 $R/bench.py "$@" --no-cpu-baseline --no-nodes512 --no-second-region --steps $P --warmup 2 --launch bound
+step write 400 rocprofv3 --pmc WRITE_SIZE -T -d $TMPP/write -o run --output-format csv -- python3 $R/bench.py "$@" --no-cpu-baseline --no-nodes512 --no-second-region --steps $P --warmup 2 --launch bound
 ALG=$(python3 -c "import json; d=json.loads(open('$OUT/bench.log').read().strip().splitlines()[-1]); print(d['roofline']['bytes_per_step'])")
 KEY=$(python3 $R/bench.py "$@" --print-traffic-key)
 FCSV=$(find $TMPP/fetch -name "*counter_collection.csv" | head -1)
