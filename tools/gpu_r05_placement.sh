@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r05_placement
 mkdir -p $OUT
 cd $R
-timeout -k 10 180 ./build/tree_placement > $OUT/probe.log 2>&1 || { echo probe failed; tail -5 $OUT/probe.log; exit 1; }
+timeout -k 10 240 ./build/tree_placement > $OUT/probe.log 2>&1 || { echo probe failed; tail -5 $OUT/probe.log; exit 1; }
 cat $OUT/probe.log
 for t in sep slab; do
   X=""; [ $t = slab ] && X="--stagger 256"

@@ -14,6 +14,8 @@
 //   slab+G     one hipMalloc, buffer j at j x (128 MiB + G)
 //   sep-rev    127 hipMalloc calls, used in reverse order
 // Rates are GB/s of the 127 x 128 B per site it moves (the pass's bytes).
+// Each placement runs with the grid stride of the product pass and blocked
+// (every wave its own contiguous range of sites).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/tree_placement.hip -o build/tree_placement
 #include <hip/hip_runtime.h>
 
@@ -32,12 +34,20 @@ struct Ptrs {
   f64x2 *out[kOut];
 };
 
-template <int U>
+// kBlocked: wave w streams its own contiguous 1/waves of the sites (so the
+// addresses in flight at once sit all over every buffer) instead of the
+// grid stride (all waves inside one 512-KiB window of every buffer at once).
+template <int U, bool kBlocked>
 __global__ void __launch_bounds__(512, 1) pass(Ptrs p, int64_t n) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6);
-  const int64_t stride = (int64_t)gridDim.x * 8 * 8 * U;  // sites
-  for (int64_t base = wave * 8 * U; base < n; base += stride) {
+  const int64_t waves = (int64_t)gridDim.x * 8;
+  const int64_t step = 8 * U;
+  const int64_t per = (n / step + waves - 1) / waves * step;  // sites per wave (blocked)
+  const int64_t first = kBlocked ? wave * per : wave * step;
+  const int64_t last = kBlocked ? (first + per < n ? first + per : n) : n;
+  const int64_t stride = kBlocked ? step : waves * step;
+  for (int64_t base = first; base < last; base += stride) {
     f64x2 acc[U];
 #pragma unroll
     for (int u = 0; u < U; u++) acc[u] = f64x2{0.0, 0.0};
@@ -77,20 +87,24 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  auto time = [&](const char *name, const std::vector<void *> &bufs) {
+  auto time1 = [&](const char *name, const std::vector<void *> &bufs, auto kern, const char *mode) {
     Ptrs p;
     for (int s = 0; s < kIn; s++) p.in[s] = static_cast<const f64x2 *>(bufs[s]);
     for (int o = 0; o < kOut; o++) p.out[o] = static_cast<f64x2 *>(bufs[kIn + o]);
     const int reps = 10;
-    for (int i = 0; i < 2; i++) hipLaunchKernelGGL(pass<2>, dim3(cus), dim3(512), 0, 0, p, n);
+    for (int i = 0; i < 2; i++) hipLaunchKernelGGL(kern, dim3(cus), dim3(512), 0, 0, p, n);
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < reps; i++) hipLaunchKernelGGL(pass<2>, dim3(cus), dim3(512), 0, 0, p, n);
+    for (int i = 0; i < reps; i++) hipLaunchKernelGGL(kern, dim3(cus), dim3(512), 0, 0, p, n);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / reps, gbs = 127.0 * 128 * n / (us * 1e-6) / 1e9;
-    std::printf("%-12s %9.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", name, us, gbs, gbs / 8000);
+    std::printf("%-12s %-8s %9.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", name, mode, us, gbs, gbs / 8000);
+  };
+  auto time = [&](const char *name, const std::vector<void *> &bufs) {
+    time1(name, bufs, pass<2, false>, "stride");
+    time1(name, bufs, pass<2, true>, "blocked");
   };
   for (int round = 0; round < 3; round++) {
     time("sep", sep);
