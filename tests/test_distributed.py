@@ -49,13 +49,15 @@ def _worker(rank, world, port, q):
                                   torch.device("cpu"), world)[2]
         skew = bench.rank_clock_spread(100.0 + 25e-6 * rank, 200.0 - 40e-6 * rank, torch.device("cpu"),
                                        world)
-        q.put((rank, wall, devt, ok, bad, skew))
+        mx = bench.max_over_ranks(3.5 * (rank + 1), torch.device("cpu"), world)
+        q.put((rank, wall, devt, ok, bad, skew, mx))
     finally:
         dist.destroy_process_group()
 
 
 def test_combine_ranks_gloo_world2():
-    for rank, wall, devt, ok, bad, skew in _spawn(_worker, 2):
+    for rank, wall, devt, ok, bad, skew, mx in _spawn(_worker, 2):
+        assert mx == 7.0
         assert wall == 11.0 and devt == 10.0   # max over ranks
         assert ok is True                      # sum of got == sum of expected
         assert bad is False                    # one rank's mismatch is seen by every rank

@@ -126,6 +126,9 @@ def test_bench_gpus_two_without_outer_launcher():
     assert d["config"]["distributed"] == "gloo"
     assert d["config"]["scaler_events_all_ranks"] == 2 * (65536 // 4)
     assert d["value_device"] >= d["value"] > 0 and d["barrier_skew_us"] >= 0
+    # the ranks start at one agreed instant; the per-rank barrier-bracketed
+    # wall is reported beside the job time
+    assert d["wall_barrier_ms_per_step"] > 0 and d["ms_per_step"] > 0
     # the default invocation also times BASELINE configs[3]: 12 nodes, 6 per rank
     sub = d["config"]["nodes512"]
     assert sub["check"] == "ok" and sub["scaling"] == "strong" and sub["nodes_per_rank"] == 6
