@@ -28,7 +28,7 @@ namespace plfx_host {
 class NodeComm {
  public:
   // err: empty on success, else why the communicator could not be made
-  NodeComm(const std::vector<int> &devices, std::string &err) : devices_(devices) {
+  NodeComm(const std::vector<int> &devices, std::string &err) {
     std::vector<int> d = devices;
     std::sort(d.begin(), d.end());
     if (std::adjacent_find(d.begin(), d.end()) != d.end()) {
@@ -77,7 +77,6 @@ class NodeComm {
   }
 
  private:
-  std::vector<int> devices_;
   std::vector<ncclComm_t> comms_;
 };
 
