@@ -15,7 +15,8 @@
 //   sep-rev    127 hipMalloc calls, used in reverse order
 // Rates are GB/s of the 127 x 128 B per site it moves (the pass's bytes).
 // Each placement runs with the grid stride of the product pass and blocked
-// (every wave its own contiguous range of sites).
+// (every wave its own contiguous range of sites); with PLACEMENT_POLICIES set,
+// the strided form with write-back loads and/or stores instead.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/tree_placement.hip -o build/tree_placement
 #include <hip/hip_runtime.h>
 
@@ -37,7 +38,8 @@ struct Ptrs {
 // kBlocked: wave w streams its own contiguous 1/waves of the sites (so the
 // addresses in flight at once sit all over every buffer) instead of the
 // grid stride (all waves inside one 512-KiB window of every buffer at once).
-template <int U, bool kBlocked>
+// kLdNT / kStNT: non-temporal loads / stores (the product pass uses both).
+template <int U, bool kBlocked, bool kLdNT = true, bool kStNT = true>
 __global__ void __launch_bounds__(512, 1) pass(Ptrs p, int64_t n) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6);
@@ -56,13 +58,17 @@ __global__ void __launch_bounds__(512, 1) pass(Ptrs p, int64_t n) {
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const int64_t b = base + 8 * u < n ? base + 8 * u : n - 8;
-        acc[u] += __builtin_nontemporal_load(p.in[s] + b * 8 + lane);
+        if constexpr (kLdNT) acc[u] += __builtin_nontemporal_load(p.in[s] + b * 8 + lane);
+        else acc[u] += p.in[s][b * 8 + lane];
       }
 #pragma unroll 8
     for (int o = 0; o < kOut; o++)
 #pragma unroll
       for (int u = 0; u < U; u++)
-        if (base + 8 * u < n) __builtin_nontemporal_store(acc[u], p.out[o] + (base + 8 * u) * 8 + lane);
+        if (base + 8 * u < n) {
+          if constexpr (kStNT) __builtin_nontemporal_store(acc[u], p.out[o] + (base + 8 * u) * 8 + lane);
+          else p.out[o][(base + 8 * u) * 8 + lane] = acc[u];
+        }
   }
 }
 
@@ -102,9 +108,16 @@ int main(int argc, char **argv) {
     const double us = ms * 1e3 / reps, gbs = 127.0 * 128 * n / (us * 1e-6) / 1e9;
     std::printf("%-12s %-8s %9.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", name, mode, us, gbs, gbs / 8000);
   };
+  const bool policies = std::getenv("PLACEMENT_POLICIES") != nullptr;
   auto time = [&](const char *name, const std::vector<void *> &bufs) {
     time1(name, bufs, pass<2, false>, "stride");
-    time1(name, bufs, pass<2, true>, "blocked");
+    if (policies) {  // cache policies of the strided form
+      time1(name, bufs, pass<2, false, false, true>, "ld-wb");
+      time1(name, bufs, pass<2, false, true, false>, "st-wb");
+      time1(name, bufs, pass<2, false, false, false>, "both-wb");
+    } else {
+      time1(name, bufs, pass<2, true>, "blocked");
+    }
   };
   for (int round = 0; round < 3; round++) {
     time("sep", sep);
