@@ -255,10 +255,41 @@ __device__ __forceinline__ void site_cat_tips(const T (&a)[4], const T (&b)[4], 
   }
 }
 
+// Site -> wave mapping of the node kernels.  kSegL2 = 0: every wave strides
+// over all n sites, so the whole chip works inside one window of each CLV.
+// kSegL2 = 3: blocks b, b + 8, ... -- one XCD's blocks (blocks are dealt
+// round-robin over the 8 XCDs, MI355X_MICROARCH.md) -- stride over the
+// (b % 8)-th eighth of the sites only, eight windows far apart.  On very
+// long CLVs the one-window pattern loses HBM rate (f32 0.59-0.62 of 8 TB/s at
+// 1e8-5e8 sites against 0.70-0.75 at 2^20-2^22); eight windows recover it,
+// but cost 6-8 % at 2^24 sites -- so the launchers pick the mapping by size
+// (plf_kernels.hip segment_grid; tools/probes/size_scaling.hip,
+// tools/max_sites.py --ab).  The grid must be a multiple of 2^kSegL2.
+// Out: this wave's index within its segment, the stride, and its segment's
+// first site and end (lo = 0, hi = n without segments).
+template <int kSegL2, int kSitesPerStep>
+__device__ __forceinline__ void wave_sites(int64_t n, int64_t &wave, int64_t &stride, int64_t &lo,
+                                           int64_t &hi) {
+  if constexpr (kSegL2 == 0) {
+    wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    stride = (int64_t)gridDim.x * kWavesPerBlock * kSitesPerStep;
+    lo = 0;
+    hi = n;
+  } else {
+    constexpr int64_t S = 1 << kSegL2;
+    wave = (int64_t)(blockIdx.x >> kSegL2) * kWavesPerBlock + (threadIdx.x >> 6);
+    stride = (int64_t)(gridDim.x >> kSegL2) * kWavesPerBlock * kSitesPerStep;
+    const int64_t steps = (n + kSitesPerStep - 1) / kSitesPerStep;
+    const int64_t per = (steps + S - 1) / S * kSitesPerStep;  // sites per segment, whole steps
+    lo = (int64_t)(blockIdx.x & (S - 1)) * per;
+    hi = lo + per < n ? lo + per : n;
+  }
+}
+
 // Knobs: U = 16-site wave steps per loop trip (bytes in flight per lane =
 // 2*U*4*sizeof(T)); NT = non-temporal CLV loads; kSum = produce the weighted
 // scaler sum; kMinWaves = __launch_bounds__ occupancy hint (waves per SIMD).
-template <typename T, int U, bool kSum, bool NT, bool T1 = false, bool T2 = false>
+template <typename T, int U, bool kSum, bool NT, bool T1 = false, bool T2 = false, int kSegL2 = 0>
 __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *__restrict__ x2,
                                              T *__restrict__ x3, const T *__restrict__ EV,
                                              const T *__restrict__ left, const T *__restrict__ right,
@@ -287,11 +318,11 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
   const T m = Num<T>::minlik();
 
   long long acc = 0;
-  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
-  const int64_t nfull = n - (16 * U - 1);  // base < nfull  <=>  whole step in range
+  int64_t wave, stride, lo, hi;
+  wave_sites<kSegL2, 16 * U>(n, wave, stride, lo, hi);
+  const int64_t nfull = hi - (16 * U - 1);  // base < nfull  <=>  whole step in range
 
-  int64_t base = wave * 16 * U;
+  int64_t base = lo + wave * 16 * U;
   // full steps: no bounds checks, every load of the step issued up front
   for (; base < nfull; base += stride) {
     T a[U][4], b[U][4];
@@ -331,11 +362,11 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
     }
   }
   // tail (at most one partial step per wave)
-  if (base < n) {
+  if (base < hi) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int64_t site = base + u * 16 + q;
-      const bool valid = site < n;
+      const bool valid = site < hi;
       T a[4] = {T(0), T(0), T(0), T(0)}, b[4] = {T(0), T(0), T(0), T(0)};
       int k1 = 0, k2 = 0;
       if (valid) {
@@ -370,14 +401,15 @@ __device__ __forceinline__ void dna_cat_body(const T *__restrict__ x1, const T *
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
 
-template <typename T, int U, bool kSum, bool NT, int kMinWaves>
+template <typename T, int U, bool kSum, bool NT, int kMinWaves, int kSegL2 = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
                const T *__restrict__ EV, const T *__restrict__ left,
                const T *__restrict__ right, const int32_t *__restrict__ wgt,
                uint8_t *__restrict__ scaler, int64_t n, unsigned long long *ws,
                int64_t *scaler_sum) {
-  dna_cat_body<T, U, kSum, NT>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum);
+  dna_cat_body<T, U, kSum, NT, false, false, kSegL2>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws,
+                                                     scaler_sum);
 }
 
 // f64 DNA kernel, lane-pair mapping: every wave memory instruction touches one
@@ -397,7 +429,7 @@ __device__ __forceinline__ f64x2 ld16(const f64x2 *p) {
 
 // T1/T2: child 1/2 is a tip (one state code per site, see build_tip_table);
 // its lane pair reads ump[2h], ump[2h+1] as one 16-B LDS row slice.
-template <int U, bool kSum, bool NTL, bool T1 = false, bool T2 = false>
+template <int U, bool kSum, bool NTL, bool T1 = false, bool T2 = false, int kSegL2 = 0>
 __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
                                               const double *__restrict__ x2,
                                               double *__restrict__ x3,
@@ -436,9 +468,9 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
   const double m = Num<double>::minlik();
 
   long long acc = 0;
-  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 16 * U;
-  const int64_t nfull = n - (16 * U - 1);
+  int64_t wave, stride, lo, hi;
+  wave_sites<kSegL2, 16 * U>(n, wave, stride, lo, hi);
+  const int64_t nfull = hi - (16 * U - 1);
 
   // one 8-site block: loads are done by the caller
   auto body = [&](const f64x2 a, const f64x2 b, int k1, int k2, int64_t site0, bool valid,
@@ -501,7 +533,7 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
     }
   };
 
-  int64_t base = wave * 16 * U;
+  int64_t base = lo + wave * 16 * U;
   for (; base < nfull; base += stride) {
     f64x2 a[U][2], b[U][2];
     int w[U][2], k1[U][2], k2[U][2];
@@ -523,13 +555,13 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
         body(T1 ? f64x2{} : a[u][j], T2 ? f64x2{} : b[u][j], T1 ? k1[u][j] : 0,
              T2 ? k2[u][j] : 0, base + u * 16 + j * 8, true, kSum ? w[u][j] : 0);
   }
-  if (base < n) {  // tail: at most one partial step per wave
+  if (base < hi) {  // tail: at most one partial step per wave
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
       for (int j = 0; j < 2; j++) {
         const int64_t site0 = base + u * 16 + j * 8;
-        const bool valid = site0 + g < n;
+        const bool valid = site0 + g < hi;
         f64x2 a = {0.0, 0.0}, b = {0.0, 0.0};
         int w = 0, k1 = 0, k2 = 0;
         if (valid) {
@@ -545,14 +577,15 @@ __device__ __forceinline__ void dna_pair_body(const double *__restrict__ x1,
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
 
-template <int U, bool kSum, int kMinWaves, bool NTL = false>
+template <int U, bool kSum, int kMinWaves, bool NTL = false, int kSegL2 = 0>
 __global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_dna_f64_pair_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                         double *__restrict__ x3, const double *__restrict__ EV,
                         const double *__restrict__ left, const double *__restrict__ right,
                         const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
                         unsigned long long *ws, int64_t *scaler_sum) {
-  dna_pair_body<U, kSum, NTL>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum);
+  dna_pair_body<U, kSum, NTL, false, false, kSegL2>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws,
+                                                   scaler_sum);
 }
 
 // Batched inner-node updates: one launch evaluates gridDim.y <= kMaxBatch

@@ -99,6 +99,20 @@ int cu_count() {
   return cus;
 }
 
+// Node kernels switch to the XCD-segmented site mapping (plf_dna.hpp
+// wave_sites, kSegL2 = 3) from min_sites up, or always / never with
+// DnaArgs::segments.  The thresholds are measured, segmented vs not on the same
+// buffers, calls alternating (tools/max_sites.py --ab, three boxes,
+// profiles/r05_node_segments_ab.log): f32 +3-4 % at 2^25 sites, +9-29 % from
+// 5e7 up; f64 +1 % at 2^26, +5-12 % from 1e8 up -- and both 6-8 % SLOWER at
+// 2^24, equal below.  Returns the segmented launch's grid, a multiple of 8
+// (blocks b and b + 8 share an XCD), or 0: not segmented.
+constexpr int64_t kSegMinSites32 = int64_t(1) << 25, kSegMinSites64 = int64_t(1) << 26;
+int64_t segment_grid(const DnaArgs &a, int64_t gx, int64_t min_sites) {
+  if (a.segments == 0 || (a.segments < 0 && a.n < min_sites)) return 0;
+  return gx >= 8 ? gx - gx % 8 : 8;
+}
+
 template <typename T, bool kSum>
 hipError_t launch_cat(const DnaArgs &a, int max_blocks, hipStream_t s) {
   static int cache = 0;
@@ -109,7 +123,9 @@ hipError_t launch_cat(const DnaArgs &a, int max_blocks, hipStream_t s) {
   // (tools/ab_defer.hip@f9b3af3, tools/tune_f32.hip@f9b3af3; profiles/r02_tune_f32.log)
   const int64_t gx = grid_x((const void *)kernel, cache, kGridMul32, a.n, kWavesPerBlock * 16 * kU32,
                             1, max_blocks > 0 ? max_blocks : kBlocksPerCu32 * cu_count());
-  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
+  const int64_t gs = segment_grid(a, gx, kSegMinSites32);
+  if (gs) kernel = &dev::plf_dna_kernel<T, kU32, kSum, kNt, kMinWaves, 3>;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)(gs ? gs : gx)), dim3(kBlock), 0, s, (const T *)a.x1,
                      (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,
                      (const T *)a.right, a.wgt, a.scaler, a.n, a.ws, a.scaler_sum);
   return hipGetLastError();
@@ -121,7 +137,9 @@ hipError_t launch_pair(const DnaArgs &a, int max_blocks, hipStream_t s) {
   auto kernel = &dev::plf_dna_f64_pair_kernel<kU64, kSum, kMinWaves, kNtl64>;
   const int64_t gx = grid_x((const void *)kernel, cache, kGridMul64, a.n, kWavesPerBlock * 16 * kU64,
                             1, max_blocks);
-  hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
+  const int64_t gs = segment_grid(a, gx, kSegMinSites64);
+  if (gs) kernel = &dev::plf_dna_f64_pair_kernel<kU64, kSum, kMinWaves, kNtl64, 3>;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)(gs ? gs : gx)), dim3(kBlock), 0, s, (const double *)a.x1,
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV,
                      (const double *)a.left, (const double *)a.right, a.wgt, a.scaler, a.n, a.ws,
                      a.scaler_sum);

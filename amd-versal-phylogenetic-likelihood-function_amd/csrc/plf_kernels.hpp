@@ -20,6 +20,8 @@ struct DnaArgs {
                             // launch also takes its tile queue from ws + kWsWords when
                             // non-null (2 x kWsWords words, zero at rest)
   int64_t n;
+  int segments = -1;        // node kernels' XCD-segmented site mapping: -1 by size, 0 off,
+                            // 1 on (plf_kernels.hip use_segments; PLFX_NODE_SEGMENTS)
 };
 
 // Fused DNA (4 states x 4 Gamma categories) inner-node update.

@@ -62,6 +62,8 @@ struct plfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
+  int node_segments = -1;           // node kernels' XCD-segmented mapping: -1 by size, 0 off, 1 on
+                                    // (PLFX_NODE_SEGMENTS; plf_kernels.hip use_segments)
   int fuse = 3;  // traverse: 3 six-level subtrees before 2's, 2 three-level subtrees +
                  // level pairs, 1 level pairs, 0 none (PLFX_FUSE)
   bool lazy_tables = false;         // PLFX_CTX_LAZY_TABLES
@@ -341,7 +343,7 @@ int plf_dev(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int64_t
     return PLFX_OK;
   }
   PLFX_WS(ctx, s, w);
-  plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, w->ws, n};
+  plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, w->ws, n, ctx->node_segments};
   hipError_t e = sizeof(T) == 4 ? plfx::launch_plf_dna_f32(a, ctx->max_blocks, s)
                                 : plfx::launch_plf_dna_f64(a, ctx->max_blocks, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "plf_dna launch");
@@ -620,6 +622,7 @@ int plfx_ctx_create_ex(int device, unsigned flags, plfx_ctx **out) {
     if (v > 0) ctx->max_blocks = v;
   }
   if (const char *env = std::getenv("PLFX_FUSE")) ctx->fuse = std::atoi(env);
+  if (const char *env = std::getenv("PLFX_NODE_SEGMENTS")) ctx->node_segments = std::atoi(env) > 0 ? 1 : 0;
   // the workspace pool: kWsPool entries (reduction words zeroed before return,
   // tip/tip tables), and the tables' constant code arrays
   auto undo = [&](int code) {

@@ -175,6 +175,143 @@ def test_plf_dev_beyond_2g_elements(ctx, oracle, dtype):
     torch.cuda.empty_cache()
 
 
+def fill_uniform(t, g, chunk=1 << 30):
+    """U[0,1) in place, chunk by chunk (one 64-GB tensor in bounded pieces)."""
+    flat = t.view(-1)
+    for i in range(0, flat.numel(), chunk):
+        flat[i:i + chunk].uniform_(generator=g)
+
+
+@pytest.mark.parametrize("dtype,n", [(np.float32, 1_000_000_000), (np.float64, 500_000_000)])
+def test_plf_dev_reference_sweep_maximum(ctx, oracle, dtype, n):
+    """The largest ALIGNMENT_SITES of the reference's sweep (Makefile:16: up to
+    1e9 sites, in f32) in ONE device call: 1e9 sites f32 and 5e8 sites f64
+    (the largest sweep point whose three f64 CLVs fit: 192 GB), each ~197 GB of
+    one GPU's 288 GB.  Element indices pass 2^32 (the reference's 32-bit byte
+    counts overflow here).  Windows at the start, at the 2^31- and
+    2^32-element crossings, in the middle and at the ragged end are bit-exact
+    against the oracle; Σ scaler·wgt equals the sum over the per-site scaler
+    bytes (chunked, size-independent)."""
+    import torch
+
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    g = torch.Generator(device="cuda")
+    g.manual_seed(97)
+    x1 = torch.empty(16 * n, dtype=tdt, device="cuda")
+    x2 = torch.empty_like(x1)
+    x3 = torch.empty_like(x1)
+    try:
+        fill_uniform(x1, g)
+        fill_uniform(x2, g)
+        x1.view(n, 16)[0::4] *= 1e-12
+        EV = torch.rand(16, dtype=tdt, device="cuda", generator=g)
+        L = torch.rand(64, dtype=tdt, device="cuda", generator=g)
+        R = torch.rand(64, dtype=tdt, device="cuda", generator=g)
+        wgt = torch.randint(0, 3, (n,), dtype=torch.int32, device="cuda", generator=g)
+        sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+        s = torch.zeros(1, dtype=torch.int64, device="cuda")
+        ctx.plf_dev(x1, x2, x3, EV, L, R, wgt, sc, s)
+        torch.cuda.synchronize()
+        c = 1 << 26
+        tot = sum(int((sc[i:i + c].to(torch.int64) * wgt[i:i + c]).sum().item()) for i in range(0, n, c))
+        assert int(s.item()) == tot
+        assert sum(int(sc[i:i + c].sum(dtype=torch.int64).item()) for i in range(0, n, c)) >= n // 4
+        h = lambda t: t.cpu().numpy()  # noqa: E731
+        for lo in (0, (1 << 27) - 1000, (1 << 28) - 1000, n // 2 + 3, n - 2000):
+            m = min(2000, n - lo)
+            sl = slice(16 * lo, 16 * (lo + m))
+            e3, esc, _ = oracle.plf(h(x1[sl]), h(x2[sl]), h(EV), h(L), h(R), h(wgt[lo:lo + m]))
+            assert np.array_equal(bits(h(x3[sl])), bits(e3)), lo
+            assert np.array_equal(h(sc[lo:lo + m]), esc), lo
+    finally:
+        del x1, x2, x3
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+def segments_ctx(monkeypatch, mode):
+    """A context whose node kernels use the XCD-segmented site mapping always
+    (mode "1") or never ("0"); the default picks it from 2^24 sites up."""
+    import plfx
+
+    monkeypatch.setenv("PLFX_NODE_SEGMENTS", mode)
+    try:
+        return plfx.Context(0)
+    finally:
+        monkeypatch.delenv("PLFX_NODE_SEGMENTS")
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_plf_dev_xcd_segments_full_compare(ctx, oracle, monkeypatch, dtype):
+    """2^24 + 13 sites through both site mappings of the node kernels -- one
+    window for the whole chip, and eight segments, one per XCD (plf_dna.hpp
+    wave_sites; by default from 2^25 sites f32 / 2^26 f64) -- and the default
+    choice: the WHOLE x3 and every scaler byte bit-exact against the oracle,
+    segment boundaries and the ragged last segment included, with and without
+    the in-kernel sum (two kernel instantiations each)."""
+    import torch
+
+    n = (1 << 24) + 13
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    g = torch.Generator(device="cuda")
+    g.manual_seed(41)
+    x1 = torch.rand(16 * n, dtype=tdt, device="cuda", generator=g)
+    x1.view(n, 16)[0::4] *= 1e-12
+    x2 = torch.rand(16 * n, dtype=tdt, device="cuda", generator=g)
+    EV = torch.rand(16, dtype=tdt, device="cuda", generator=g)
+    L = torch.rand(64, dtype=tdt, device="cuda", generator=g)
+    R = torch.rand(64, dtype=tdt, device="cuda", generator=g)
+    wgt = torch.randint(-2, 4, (n,), dtype=torch.int32, device="cuda", generator=g)
+    h = lambda t: t.cpu().numpy()  # noqa: E731
+    e3, esc, einc = oracle.plf(h(x1), h(x2), h(EV), h(L), h(R), h(wgt), threads=16)
+    on, off = segments_ctx(monkeypatch, "1"), segments_ctx(monkeypatch, "0")
+    try:
+        for label, c in (("default", ctx), ("segments", on), ("one window", off)):
+            for with_sum in (True, False):
+                x3 = torch.empty_like(x1)
+                sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+                s = torch.zeros(1, dtype=torch.int64, device="cuda") if with_sum else None
+                c.plf_dev(x1, x2, x3, EV, L, R, wgt, sc, s)
+                torch.cuda.synchronize()
+                assert np.array_equal(bits(h(x3)), bits(e3)), (label, with_sum)
+                assert np.array_equal(h(sc), esc), (label, with_sum)
+                if with_sum:
+                    assert int(s.item()) == einc
+                del x3, sc
+    finally:
+        on.close()
+        off.close()
+    del x1, x2
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n", [1, 7, 100, 1000, 4097, 65539, 300001])
+def test_plf_dev_xcd_segments_forced_small(ctx, oracle, monkeypatch, n):
+    """The segmented mapping forced on at small and ragged sizes, where most
+    of the eight segments are short or empty (a segment's first site past n):
+    bit-exact against the oracle, f32 and f64, scaler sums exact."""
+    import torch
+
+    on = segments_ctx(monkeypatch, "1")
+    try:
+        for dtype in (np.float32, np.float64):
+            d = oracle.gen_hostmem(n, dtype, 9)
+            e3, esc, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+            t = {k: torch_dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+            x3 = torch.empty_like(t["x1"])
+            sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+            s = torch.zeros(1, dtype=torch.int64, device="cuda")
+            on.plf_dev(t["x1"], t["x2"], x3, t["EV"], t["left"], t["right"], t["wgt"], sc, s)
+            torch.cuda.synchronize()
+            assert np.array_equal(bits(x3.cpu().numpy()), bits(e3))
+            assert np.array_equal(sc.cpu().numpy(), esc)
+            assert int(s.item()) == einc
+    finally:
+        on.close()
+
+
 def test_plf_dev_repeated_calls_and_optional_outputs(ctx, oracle):
     """The in-kernel ticket reduction resets itself: back-to-back launches with
     different weights each report their own sum; outputs are optional."""

@@ -1,0 +1,152 @@
+// size_scaling.hip -- probe (not product code): why does one f64 node call
+// run at 0.67 of 8 TB/s at 5e8 sites (192 GB of CLVs, tools/max_sites.py)
+// but 0.74-0.77 at 2^20-2^22 sites?  Streams the node kernel's memory pattern
+// (2 reads + 1 write of 128 B per site, lane-pair layout: lane l <-> bytes
+// 16l..16l+15 of an 8-site block, non-temporal, 256-thread blocks, 2 x 8-site
+// blocks per wave step) with no arithmetic, over prefixes of three 64-GB
+// buffers, with three site->wave mappings:
+//   stride  the product's: every wave strides over the whole array, so all
+//           waves (on all 8 XCDs) work inside one ~12-MB window of each buffer
+//   xcd     blocks of XCD x (= blockIdx % 8, the dispatcher's round robin)
+//           stride over the x-th eighth of the sites only: each XCD's address
+//           translations cover 1/8 of the pages
+//   blocked every wave its own contiguous range
+//   segS    S = 16, 32, 64 segments: blocks b, b + S, ... stride over the
+//           (b % S)-th S-th of the sites (xcd is S = 8)
+//   chunkK  (first run: not kept) sites cut into chunks of 2^K, chunk j to XCD
+//           j % 8, each XCD striding over its own chunks -- ran like stride
+// GB/s are of the 385 B per site the node kernel moves (the 1-B scaler omitted
+// here, counted in the rate as the product counts it).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/size_scaling.hip -o build/size_scaling
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+constexpr int kWaves = 4;  // 256-thread blocks
+constexpr int U = 2;       // 8-site blocks per wave step (x2 = 16 sites)
+
+template <int K>
+__global__ void __launch_bounds__(256) pass_chunk(const f64x2 *__restrict__ x1,
+                                                  const f64x2 *__restrict__ x2,
+                                                  f64x2 *__restrict__ x3, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t step = 8 * U;
+  const int64_t xcd = blockIdx.x & 7;
+  const int64_t wave = (int64_t)(blockIdx.x >> 3) * kWaves + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)(gridDim.x / 8) * kWaves * step;
+  const int64_t mask = (1ll << K) - 1;
+  for (int64_t v = wave * step;; v += stride) {
+    const int64_t base = ((((v >> K) << 3) + xcd) << K) + (v & mask);  // monotonic in v
+    if (base >= n) break;
+    f64x2 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t s = base + 8 * u < n ? base + 8 * u : n - 8;
+      a[u] = __builtin_nontemporal_load(x1 + s * 8 + lane);
+      b[u] = __builtin_nontemporal_load(x2 + s * 8 + lane);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (base + 8 * u < n) __builtin_nontemporal_store(a[u] * b[u], x3 + (base + 8 * u) * 8 + lane);
+  }
+}
+
+template <int kMode, int S = 8>  // 0 stride, 1 segments (S = 8: one per XCD), 2 blocked
+__global__ void __launch_bounds__(256) pass(const f64x2 *__restrict__ x1, const f64x2 *__restrict__ x2,
+                                            f64x2 *__restrict__ x3, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t step = 8 * U;
+  int64_t first, last, stride;
+  if constexpr (kMode == 0) {
+    const int64_t wave = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    first = wave * step;
+    last = n;
+    stride = (int64_t)gridDim.x * kWaves * step;
+  } else if constexpr (kMode == 1) {
+    const int xcd = blockIdx.x % S;
+    const int64_t blocks_x = gridDim.x / S;  // grid is a multiple of S
+    const int64_t wave = (int64_t)(blockIdx.x / S) * kWaves + (threadIdx.x >> 6);
+    const int64_t per = (n / step + S - 1) / S * step;  // sites of this segment
+    const int64_t lo = xcd * per;
+    first = lo + wave * step;
+    last = lo + per < n ? lo + per : n;
+    stride = blocks_x * kWaves * step;
+  } else {
+    const int64_t wave = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    const int64_t waves = (int64_t)gridDim.x * kWaves;
+    const int64_t per = (n / step + waves - 1) / waves * step;
+    first = wave * per;
+    last = first + per < n ? first + per : n;
+    stride = step;
+  }
+  for (int64_t base = first; base < last; base += stride) {
+    f64x2 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t s = base + 8 * u < n ? base + 8 * u : n - 8;
+      a[u] = __builtin_nontemporal_load(x1 + s * 8 + lane);
+      b[u] = __builtin_nontemporal_load(x2 + s * 8 + lane);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (base + 8 * u < last) __builtin_nontemporal_store(a[u] * b[u], x3 + (base + 8 * u) * 8 + lane);
+  }
+}
+
+int main(int argc, char **argv) {
+  const int64_t nmax = argc > 1 ? std::atoll(argv[1]) : 500000000LL;  // sites
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const size_t bytes = (size_t)nmax * 128;
+  void *p1, *p2, *p3;
+  CK(hipMalloc(&p1, bytes));
+  CK(hipMalloc(&p2, bytes));
+  CK(hipMalloc(&p3, bytes));
+  CK(hipMemset(p1, 0, bytes));
+  CK(hipMemset(p2, 0, bytes));
+  CK(hipMemset(p3, 0, bytes));
+  auto *x1 = static_cast<const f64x2 *>(p1), *x2 = static_cast<const f64x2 *>(p2);
+  auto *x3 = static_cast<f64x2 *>(p3);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int grid = 3 * cus;  // resident 256-thread blocks of the product kernel: 3 per CU (a multiple of 64)
+  auto time1 = [&](auto kern, const char *mode, int64_t n, int64_t off) {
+    // rotate over prefixes at `off` apart so small sizes do not sit in the MALL
+    const int sets = off ? 4 : 1;
+    const int reps = n >= (1 << 26) ? 3 : 20;
+    for (int i = 0; i < 2; i++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, x1, x2, x3, n);
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; i++) {
+      const int64_t o = (i % sets) * off * 8;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, x1 + o, x2 + o, x3 + o, n);
+    }
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / reps, gbs = 385.0 * n / (us * 1e-6) / 1e9;
+    std::printf("n=%-11lld %-8s %11.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", (long long)n, mode, us, gbs,
+                gbs / 8000);
+  };
+  std::vector<int64_t> sizes = {1 << 20, 1 << 22, 1 << 24, 1 << 25, 1 << 26, 1 << 27, 1 << 28, nmax};
+  for (int round = 0; round < 2; round++)
+    for (int64_t n : sizes) {
+      if (n > nmax) continue;
+      const int64_t off = 4 * n <= nmax ? n : 0;  // 4 rotating sets where they fit
+      time1(pass<0>, "stride", n, off);
+      time1(pass<1>, "xcd", n, off);
+      time1(pass<2>, "blocked", n, off);
+      time1(pass<1, 16>, "seg16", n, off);
+      time1(pass<1, 32>, "seg32", n, off);
+      time1(pass<1, 64>, "seg64", n, off);
+    }
+  CK(hipGetLastError());
+  return 0;
+}
