@@ -11,8 +11,9 @@
 //           stride over the x-th eighth of the sites only: each XCD's address
 //           translations cover 1/8 of the pages
 //   blocked every wave its own contiguous range
-//   segS    S = 16, 32, 64 segments: blocks b, b + S, ... stride over the
-//           (b % S)-th S-th of the sites (xcd is S = 8)
+//   segS    (second run: not kept) S = 16, 32, 64 segments -- at best like xcd
+//   tileT   block b takes tiles b, b + G, ... of T contiguous sites (the
+//           protein kernels' shape), its 4 waves the tile's steps in turn
 //   chunkK  (first run: not kept) sites cut into chunks of 2^K, chunk j to XCD
 //           j % 8, each XCD striding over its own chunks -- ran like stride
 // GB/s are of the 385 B per site the node kernel moves (the 1-B scaler omitted
@@ -54,6 +55,32 @@ __global__ void __launch_bounds__(256) pass_chunk(const f64x2 *__restrict__ x1,
 #pragma unroll
     for (int u = 0; u < U; u++)
       if (base + 8 * u < n) __builtin_nontemporal_store(a[u] * b[u], x3 + (base + 8 * u) * 8 + lane);
+  }
+}
+
+// tileT: the protein kernels' shape -- block b takes tiles b, b + G, ... of T
+// contiguous sites; the block's 4 waves take the tile's 16-site steps in turn
+template <int T>
+__global__ void __launch_bounds__(256) pass_tile(const f64x2 *__restrict__ x1,
+                                                 const f64x2 *__restrict__ x2,
+                                                 f64x2 *__restrict__ x3, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  constexpr int64_t step = 8 * U;
+  for (int64_t tile = blockIdx.x; tile * T < n; tile += gridDim.x) {
+    const int64_t t0 = tile * T, t1 = t0 + T < n ? t0 + T : n;
+    for (int64_t base = t0 + w * step; base < t1; base += kWaves * step) {
+      f64x2 a[U], b[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t s = base + 8 * u < n ? base + 8 * u : n - 8;
+        a[u] = __builtin_nontemporal_load(x1 + s * 8 + lane);
+        b[u] = __builtin_nontemporal_load(x2 + s * 8 + lane);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (base + 8 * u < t1) __builtin_nontemporal_store(a[u] * b[u], x3 + (base + 8 * u) * 8 + lane);
+    }
   }
 }
 
@@ -143,9 +170,9 @@ int main(int argc, char **argv) {
       time1(pass<0>, "stride", n, off);
       time1(pass<1>, "xcd", n, off);
       time1(pass<2>, "blocked", n, off);
-      time1(pass<1, 16>, "seg16", n, off);
-      time1(pass<1, 32>, "seg32", n, off);
-      time1(pass<1, 64>, "seg64", n, off);
+      time1(pass_tile<256>, "tile256", n, off);
+      time1(pass_tile<1024>, "tile1k", n, off);
+      time1(pass_tile<4096>, "tile4k", n, off);
     }
   CK(hipGetLastError());
   return 0;
