@@ -16,7 +16,8 @@
 // Rates are GB/s of the 127 x 128 B per site it moves (the pass's bytes).
 // Each placement runs with the grid stride of the product pass and blocked
 // (every wave its own contiguous range of sites); with PLACEMENT_POLICIES set,
-// the strided form with write-back loads and/or stores instead.
+// the strided form with write-back loads and/or stores instead; with
+// PLACEMENT_XCD set, one segment of the sites per XCD instead of blocked.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/tree_placement.hip -o build/tree_placement
 #include <hip/hip_runtime.h>
 
@@ -72,6 +73,37 @@ __global__ void __launch_bounds__(512, 1) pass(Ptrs p, int64_t n) {
   }
 }
 
+// kXcd: blocks b, b + 8, ... (one XCD's) stride over the (b % 8)-th eighth of
+// the sites only -- the node kernels' segmented mapping (plf_dna.hpp
+// wave_sites) applied to the 127-stream pattern
+template <int U>
+__global__ void __launch_bounds__(512, 1) pass_xcd(Ptrs p, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t step = 8 * U;
+  const int64_t wave = (int64_t)(blockIdx.x >> 3) * 8 + (threadIdx.x >> 6);
+  const int64_t stride = (int64_t)(gridDim.x >> 3) * 8 * step;
+  const int64_t per = ((n + step - 1) / step + 7) / 8 * step;
+  const int64_t lo = (int64_t)(blockIdx.x & 7) * per;
+  const int64_t hi = lo + per < n ? lo + per : n;
+  for (int64_t base = lo + wave * step; base < hi; base += stride) {
+    f64x2 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) acc[u] = f64x2{0.0, 0.0};
+#pragma unroll 8
+    for (int s = 0; s < kIn; s++)
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t b = base + 8 * u < n ? base + 8 * u : n - 8;
+        acc[u] += __builtin_nontemporal_load(p.in[s] + b * 8 + lane);
+      }
+#pragma unroll 8
+    for (int o = 0; o < kOut; o++)
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (base + 8 * u < hi) __builtin_nontemporal_store(acc[u], p.out[o] + (base + 8 * u) * 8 + lane);
+  }
+}
+
 int main(int argc, char **argv) {
   const int64_t n = argc > 1 ? std::atol(argv[1]) : (1 << 20);  // sites per CLV
   const size_t clv = (size_t)n * 128;                            // f64, 16 values per site
@@ -115,6 +147,8 @@ int main(int argc, char **argv) {
       time1(name, bufs, pass<2, false, false, true>, "ld-wb");
       time1(name, bufs, pass<2, false, true, false>, "st-wb");
       time1(name, bufs, pass<2, false, false, false>, "both-wb");
+    } else if (std::getenv("PLACEMENT_XCD")) {
+      time1(name, bufs, pass_xcd<2>, "xcd");
     } else {
       time1(name, bufs, pass<2, true>, "blocked");
     }
