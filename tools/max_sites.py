@@ -9,8 +9,9 @@ the sum over the per-site scaler bytes.  Correctness at these sizes is asserted
 bit-exactly by tests/test_gpu_parity.py::test_plf_dev_reference_sweep_maximum;
 this only times it.  One JSON line per case.  --ab: each size also on a
 context with the node kernels' XCD-segmented mapping off (PLFX_NODE_SEGMENTS=0),
-calls alternating between the two contexts on the same buffers; --sizes picks
-other site counts (f64 and f32 at each; f32 alone above 5e8).
+calls alternating between the two contexts on the same buffers; --variants
+adds contexts made with other library env knobs (grid cap, mapping); --sizes
+picks other site counts (f64 and f32 at each; f32 alone above 5e8).
 
   python3 tools/max_sites.py [--calls 5] [--ab] [--sizes 16777216,67108864]
 """
@@ -89,12 +90,27 @@ def main():
     ap.add_argument("--calls", type=int, default=5)
     ap.add_argument("--ab", action="store_true")
     ap.add_argument("--sizes", default=None)
+    ap.add_argument("--variants", default=None,
+                    help="more contexts, 'label:ENV=VAL,...;label2:...' (e.g. PLFX_MAX_BLOCKS, "
+                         "PLFX_NODE_SEGMENTS), timed alternating with the default one")
     a = ap.parse_args()
     ctxs = {"default": plfx.Context(0)}
     if a.ab:
         os.environ["PLFX_NODE_SEGMENTS"] = "0"
         ctxs["unsegmented"] = plfx.Context(0)
         del os.environ["PLFX_NODE_SEGMENTS"]
+    for spec in (a.variants.split(";") if a.variants else []):
+        # label:ENV=VAL,ENV=VAL -- a context made with those library env knobs
+        label, _, envs = spec.partition(":")
+        kv = dict(e.split("=", 1) for e in envs.split(",") if e)
+        old = {k: os.environ.get(k) for k in kv}
+        os.environ.update(kv)
+        ctxs[label] = plfx.Context(0)
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     if a.sizes:
         cases = []
         for n in (int(v) for v in a.sizes.split(",")):

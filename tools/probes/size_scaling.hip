@@ -143,7 +143,12 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const int grid = 3 * cus;  // resident 256-thread blocks of the product kernel: 3 per CU (a multiple of 64)
+  // blocks per CU (argv[2], default 3): 256-thread blocks, so 1..8 = 1..8 waves per SIMD.
+  // The 3 per CU resident for the product's shape (a multiple of 64 blocks);
+  // MODES=sx runs only the stride and xcd mappings.
+  const int bpc = argc > 2 ? std::atoi(argv[2]) : 3;
+  const int grid = bpc * cus;
+  const bool only_sx = std::getenv("MODES") != nullptr;
   auto time1 = [&](auto kern, const char *mode, int64_t n, int64_t off) {
     // rotate over prefixes at `off` apart so small sizes do not sit in the MALL
     const int sets = off ? 4 : 1;
@@ -159,16 +164,25 @@ int main(int argc, char **argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / reps, gbs = 385.0 * n / (us * 1e-6) / 1e9;
-    std::printf("n=%-11lld %-8s %11.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", (long long)n, mode, us, gbs,
-                gbs / 8000);
+    std::printf("bpc=%d n=%-11lld %-8s %11.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", bpc, (long long)n, mode,
+                us, gbs, gbs / 8000);
   };
   std::vector<int64_t> sizes = {1 << 20, 1 << 22, 1 << 24, 1 << 25, 1 << 26, 1 << 27, 1 << 28, nmax};
+  if (const char *s = std::getenv("SIZES")) {  // comma-separated site counts
+    sizes.clear();
+    for (const char *q = s; *q;) {
+      sizes.push_back(std::atoll(q));
+      while (*q && *q != ',') q++;
+      if (*q == ',') q++;
+    }
+  }
   for (int round = 0; round < 2; round++)
     for (int64_t n : sizes) {
       if (n > nmax) continue;
       const int64_t off = 4 * n <= nmax ? n : 0;  // 4 rotating sets where they fit
       time1(pass<0>, "stride", n, off);
       time1(pass<1>, "xcd", n, off);
+      if (only_sx) continue;
       time1(pass<2>, "blocked", n, off);
       time1(pass_tile<256>, "tile256", n, off);
       time1(pass_tile<1024>, "tile1k", n, off);
