@@ -173,7 +173,7 @@ int plfx_plf_f64(plfx_ctx *ctx, const double *x1_start, const double *x2_start,
  * char output) and scaler_sum (int64, = sum scaler*wgt, wgt NULL => 1) are
  * each optional (NULL = not produced / not read).  n may be 0.  From 2^25
  * sites (f32) / 2^26 (f64) the kernel deals the sites to the 8 XCDs as eight
- * contiguous segments instead of one grid-wide stride -- same bits, +5-29 %
+ * contiguous segments instead of one grid-wide stride -- same bits, +1-29 %
  * HBM rate on long CLVs; env PLFX_NODE_SEGMENTS=0/1,
  * read at context creation, forces one mapping or the other. */
 int plfx_plf_dev_f32(plfx_ctx *ctx, const float *x1, const float *x2, float *x3,
