@@ -106,7 +106,8 @@ int cu_count() {
 // profiles/r05_node_segments_ab.log): f32 +3-4 % at 2^25 sites, +9-29 % from
 // 5e7 up; f64 +1 % at 2^26, +5-12 % from 1e8 up -- and both 6-8 % SLOWER at
 // 2^24, equal below.  Returns the segmented launch's grid, a multiple of 8
-// (blocks b and b + 8 share an XCD), or 0: not segmented.
+// (blocks b and b + 8 share an XCD; the grid rounded down, or up to 8 blocks
+// under a smaller cap), or 0: not segmented.
 constexpr int64_t kSegMinSites32 = int64_t(1) << 25, kSegMinSites64 = int64_t(1) << 26;
 int64_t segment_grid(const DnaArgs &a, int64_t gx, int64_t min_sites) {
   if (a.segments == 0 || (a.segments < 0 && a.n < min_sites)) return 0;
