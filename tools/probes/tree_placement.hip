@@ -116,7 +116,11 @@ int main(int argc, char **argv) {
   }
   const size_t gaps[] = {0, 2u << 20, 6u << 20, 68u << 20};
   std::vector<char *> slabs;
+  // PLACEMENT_SEP_ONLY: the 127 separate allocations only (long CLVs: four
+  // 127-CLV slabs would not fit beside them)
+  const bool sep_only = std::getenv("PLACEMENT_SEP_ONLY") != nullptr;
   for (size_t g : gaps) {
+    if (sep_only) break;
     char *s = nullptr;
     CK(hipMalloc((void **)&s, (kIn + kOut) * (clv + g)));
     CK(hipMemset(s, 0, (kIn + kOut) * (clv + g)));
