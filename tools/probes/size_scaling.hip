@@ -84,9 +84,12 @@ __global__ void __launch_bounds__(256) pass_tile(const f64x2 *__restrict__ x1,
   }
 }
 
-template <int kMode, int S = 8>  // 0 stride, 1 segments (S = 8: one per XCD), 2 blocked
+// UU: 8-site blocks per wave trip (2 = 16 sites; the product's f64 kernel
+// covers 32 sites per trip, UU = 4)
+template <int kMode, int S = 8, int UU = U>  // 0 stride, 1 segments (S = 8: one per XCD), 2 blocked
 __global__ void __launch_bounds__(256) pass(const f64x2 *__restrict__ x1, const f64x2 *__restrict__ x2,
                                             f64x2 *__restrict__ x3, int64_t n) {
+  constexpr int U = UU;
   const int lane = threadIdx.x & 63;
   const int64_t step = 8 * U;
   int64_t first, last, stride;
@@ -182,7 +185,11 @@ int main(int argc, char **argv) {
       const int64_t off = 4 * n <= nmax ? n : 0;  // 4 rotating sets where they fit
       time1(pass<0>, "stride", n, off);
       time1(pass<1>, "xcd", n, off);
-      if (only_sx) continue;
+      if (only_sx) {
+        time1(pass<0, 8, 4>, "stride32", n, off);
+        time1(pass<1, 8, 4>, "xcd32", n, off);
+        continue;
+      }
       time1(pass<2>, "blocked", n, off);
       time1(pass_tile<256>, "tile256", n, off);
       time1(pass_tile<1024>, "tile1k", n, off);
