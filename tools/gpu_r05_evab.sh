@@ -1,3 +1,4 @@
+#!/bin/bash
 # Round 5: region events created inside vs before the timed region (needs bench_prev.py = git show <rev>:bench.py at the repo root)
 set -u
 mkdir -p gpurun_out/r05_evab

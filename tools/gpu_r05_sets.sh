@@ -1,3 +1,6 @@
+#!/bin/bash
+# Round 5: protein and node bench lines with 1 vs 2-4 rotating buffer sets (no
+# effect on the rate; profiles/r05_protein_sizes.log context).
 set -u
 OUT=gpurun_out/r05_sets; mkdir -p $OUT
 for spec in "protein 1048576 4" "protein 1048576 1" "protein 4194304 2" "protein 4194304 1" "protein 262144 4" "protein 262144 1" "node 4194304 4" "node 4194304 1" "node 1048576 1"; do
