@@ -129,14 +129,22 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  // PLACEMENT_BPC: 512-thread blocks per CU (default 1 = 2 waves per SIMD, the
+  // six-level pass's occupancy; 2 = 4 waves per SIMD)
+  const int bpc = std::getenv("PLACEMENT_BPC") ? std::atoi(std::getenv("PLACEMENT_BPC")) : 1;
+  {
+    int occ = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pass<2, false>, 512, 0));
+    std::printf("# %d block(s) of 512 per CU requested, %d co-resident\n", bpc, occ);
+  }
   auto time1 = [&](const char *name, const std::vector<void *> &bufs, auto kern, const char *mode) {
     Ptrs p;
     for (int s = 0; s < kIn; s++) p.in[s] = static_cast<const f64x2 *>(bufs[s]);
     for (int o = 0; o < kOut; o++) p.out[o] = static_cast<f64x2 *>(bufs[kIn + o]);
     const int reps = 10;
-    for (int i = 0; i < 2; i++) hipLaunchKernelGGL(kern, dim3(cus), dim3(512), 0, 0, p, n);
+    for (int i = 0; i < 2; i++) hipLaunchKernelGGL(kern, dim3(bpc * cus), dim3(512), 0, 0, p, n);
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < reps; i++) hipLaunchKernelGGL(kern, dim3(cus), dim3(512), 0, 0, p, n);
+    for (int i = 0; i < reps; i++) hipLaunchKernelGGL(kern, dim3(bpc * cus), dim3(512), 0, 0, p, n);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
