@@ -231,6 +231,20 @@ def test_launch_check_against_record_shapes():
     assert bench.launch_check(rec, None)[0]                        # no graph: not checked
 
 
+def test_traffic_not_reported_under_dispatch_knobs(monkeypatch):
+    """A library env knob that changes the dispatched instantiation (the
+    segmented node kernel keeps the base name and the grid, so neither the
+    code stamp nor the launch shapes can tell) withholds `traffic`."""
+    a = bench.parse(["--steps", "1"])
+
+    class W:
+        bytes_per_step = 0
+
+    monkeypatch.setenv("PLFX_NODE_SEGMENTS", "1")
+    r = bench.traffic_record(a, W())
+    assert r["traffic"] is None and "PLFX_NODE_SEGMENTS" in r["traffic_note"]
+
+
 def test_pmc_tools_record_launch_shapes():
     """The PMC record tools read the dispatch shapes from rocprofv3's counter
     CSV (demangled or truncated kernel names), as bench.py compares them."""
