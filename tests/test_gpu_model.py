@@ -145,3 +145,30 @@ def test_pmatrix_rejects_bad_args(ctx):
         ctx.pmatrix(e, r, b, out, convention=7)
     with pytest.raises(plfx.PlfxError):
         ctx.pmatrix(e, r, b, out[:10])
+
+
+def test_device_pmatrix_reproduces_reference_aie_matrices(ctx):
+    """The device P-matrix path with the generator parameters recovered from
+    the reference's AIE stimuli (tests/test_model.py, aie/data/inputEV0.txt,
+    inputbranchleft{0..3}.txt): STATE matrices equal the data's state-space
+    transition matrices to its six printed decimals, and the EIGEN matrices
+    with the library's EV compose to the same STATE matrices (the eigenvector
+    basis drops out)."""
+    import torch
+
+    from test_model import AIE_ALPHA, AIE_EXCH, AIE_T, aie_model
+
+    EV, Pe, Ps = aie_model()
+    e = plfx.model_eigen(AIE_EXCH, EV[:, 0])
+    rates = plfx.gamma_rates(AIE_ALPHA, 4)
+    blen = np.array([AIE_T])
+    st = torch.empty(4 * 16, dtype=torch.float64, device="cuda")
+    eg = torch.empty(4 * 16, dtype=torch.float64, device="cuda")
+    ctx.pmatrix(dev(e), dev(rates), dev(blen), st, states=4, convention=plfx.PMAT_STATE)
+    ctx.pmatrix(dev(e), dev(rates), dev(blen), eg, states=4, convention=plfx.PMAT_EIGEN)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy().reshape(4, 4, 4)
+    eg = eg.cpu().numpy().reshape(4, 4, 4)
+    assert np.abs(st - Ps).max() < 3e-6
+    ev = plfx.model_ev(e, 4, plfx.PMAT_EIGEN).reshape(4, 4)
+    assert np.abs(np.einsum("ckl,ml->ckm", eg, ev) - st).max() < 1e-13
