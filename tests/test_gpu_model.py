@@ -172,3 +172,39 @@ def test_device_pmatrix_reproduces_reference_aie_matrices(ctx):
     assert np.abs(st - Ps).max() < 3e-6
     ev = plfx.model_ev(e, 4, plfx.PMAT_EIGEN).reshape(4, 4)
     assert np.abs(np.einsum("ckl,ml->ckm", eg, ev) - st).max() < 1e-13
+
+
+def test_device_tree_reproduces_reference_aie_golden(ctx):
+    """The reference's AIE known-answer tree (four A tips, z = 0.9 on every
+    branch; see tests/test_model.py) through the device path: eigen-convention
+    P matrices from plfx_pmatrix, the library's EV and tip vectors, the two
+    plf levels on the GPU kernels (f64) -- the cherry and the root equal the
+    reference's aie/data CLVs in state coordinates to the goldens' precision."""
+    import torch
+
+    from conftest import golden
+    from test_model import AIE_ALPHA, AIE_EXCH, AIE_T, aie_model
+
+    k = golden("aie_kat.npz")
+    EV_d = aie_model()[0]
+    V_d = np.linalg.inv(EV_d.T)
+    e = plfx.model_eigen(AIE_EXCH, EV_d[:, 0])
+    V = e[4:20].reshape(4, 4)
+    rates = plfx.gamma_rates(AIE_ALPHA, 4)
+    P = torch.empty(64, dtype=torch.float64, device="cuda")
+    ctx.pmatrix(dev(e), dev(rates), dev(np.array([AIE_T])), P, states=4, convention=plfx.PMAT_EIGEN)
+    EV = dev(plfx.model_ev(e, 4, plfx.PMAT_EIGEN))
+    tip = plfx.model_tip_vectors(e, plfx.PMAT_EIGEN).reshape(16, 4)[1]
+    n = 3  # three identical sites (a ragged wave step)
+    x = dev(np.tile(tip, 4 * n))
+    cherry = torch.empty_like(x)
+    root = torch.empty_like(x)
+    ctx.plf_dev(x, x, cherry, EV, P, P)
+    ctx.plf_dev(cherry, cherry, root, EV, P, P)
+    torch.cuda.synchronize()
+    x1 = k["x1"].astype(np.float64).reshape(4, 4)
+    gold = k["golden"].astype(np.float64).reshape(4, 4)
+    for got, ref in ((cherry, x1), (root, gold)):
+        g = got.cpu().numpy().reshape(n, 4, 4)
+        for s in range(n):
+            assert np.abs(g[s] @ V.T - ref @ V_d.T).max() < 2e-6

@@ -190,3 +190,36 @@ def test_model_alternatives_do_not_reproduce_aie_matrices():
     assert err() < 3e-6
     for e in (err(median=True), err(alpha=0.9), err(alpha=1.1), err(exch=np.ones(6)), err(t=AIE_T * 1.01)):
         assert e > 1e-4, e
+
+
+def test_model_reproduces_reference_aie_golden_tree():
+    """The AIE known-answer test of the reference (aie/data: inputdata*,
+    golden*) is a four-taxon tree: its input CLVs are plf() of two A tips
+    (a cherry, in eigen coordinates) and its golden output plf() of two such
+    cherries, all four branches at z = 0.9.  Built from the library's model
+    (eigen-convention tip vectors, P matrices and EV for the recovered
+    parameters), the same tree gives the reference's CLVs -- compared in
+    state coordinates, x = V x~, where the eigenvector basis drops out -- to
+    the goldens' printed precision."""
+    from conftest import golden
+
+    k = golden("aie_kat.npz")
+    EV_d, Pe_d, _ = aie_model()
+    V_d = np.linalg.inv(EV_d.T)  # the data's V (EV[k][l] = Vinv[l][k])
+    pi = EV_d[:, 0]
+    e = plfx.model_eigen(AIE_EXCH, pi)
+    lam, V, Vi = split(e, 4)
+    r = plfx.gamma_rates(AIE_ALPHA, 4)
+    Pe = np.stack([V * np.exp(lam * rc * AIE_T)[None, :] for rc in r])  # PMAT_EIGEN
+    EV = plfx.model_ev(e, 4, plfx.PMAT_EIGEN).reshape(4, 4)
+    tip = plfx.model_tip_vectors(e, plfx.PMAT_EIGEN).reshape(16, 4)[1]  # code 1 = A
+
+    def plf1(xl, xr):  # plf() for one site, per category (plf.cpp:29-50)
+        return np.stack([EV.T @ ((Pe[c] @ xl[c]) * (Pe[c] @ xr[c])) for c in range(4)])
+
+    cherry = plf1(np.tile(tip, (4, 1)), np.tile(tip, (4, 1)))
+    root = plf1(cherry, cherry)
+    x1 = k["x1"].astype(np.float64).reshape(4, 4)
+    gold = k["golden"].astype(np.float64).reshape(4, 4)
+    assert np.abs(cherry @ V.T - x1 @ V_d.T).max() < 2e-6
+    assert np.abs(root @ V.T - gold @ V_d.T).max() < 2e-6
