@@ -1,9 +1,10 @@
 """GPU tests of P-matrix generation (plfx.h section 9)
 and of the whole likelihood pipeline built from it: GTR+Gamma4 eigensystem ->
 device P matrices -> traversal (tips as state codes) -> root lnL, against an
-independent numpy Felsenstein pruning that uses scipy.linalg.expm.  The
-reference has no model code: "parity unpinned" against it; the bar is the
-north-star f64 tolerance, 1e-10 relative."""
+independent numpy Felsenstein pruning that uses scipy.linalg.expm (the bar:
+the north-star f64 tolerance, 1e-10 relative), and the reference's own AIE
+stimuli -- a GTR + Gamma4 model's matrices and a four-taxon known-answer tree
+-- reproduced through the device path (the last two tests)."""
 import numpy as np
 import pytest
 

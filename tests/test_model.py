@@ -1,10 +1,11 @@
 """CPU tests of the host-side model setup (plfx.h
 section 9): GTR eigensystem and Yang (1994) discrete-Gamma rates.  The
 reference has no model code (its P/EV inputs are random or precomputed), so
-these are pinned by independent implementations -- scipy.linalg.expm,
+these are checked against independent implementations -- scipy.linalg.expm,
 scipy.stats.gamma / scipy.special.gammainc -- and the published Yang (1994)
-table; "parity unpinned" against the reference itself.  Host-only functions of
-libplfx: no GPU is touched."""
+table, and pinned by the reference's own AIE stimuli, which are such a model's
+matrices (the tests at the end).  Host-only functions of libplfx: no GPU is
+touched."""
 import numpy as np
 import pytest
 
