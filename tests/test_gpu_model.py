@@ -209,3 +209,41 @@ def test_device_tree_reproduces_reference_aie_golden(ctx):
         g = got.cpu().numpy().reshape(n, 4, 4)
         for s in range(n):
             assert np.abs(g[s] @ V.T - ref @ V_d.T).max() < 2e-6
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_traversal_with_coded_tips_reproduces_reference_aie_golden(ctx, dtype):
+    """The same known-answer tree through plfx_traverse with coded tips (four
+    A tips as uint8 state codes, the library's eigen-convention tip-vector
+    table, one P-matrix pair per inner node from plfx_pmatrix): the root CLV
+    equals the reference's golden in state coordinates (f64 to the goldens'
+    six decimals, f32 to float rounding)."""
+    import torch
+
+    from conftest import golden
+    from test_model import AIE_ALPHA, AIE_EXCH, AIE_T, aie_model
+
+    k = golden("aie_kat.npz")
+    EV_d = aie_model()[0]
+    V_d = np.linalg.inv(EV_d.T)
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+    e = plfx.model_eigen(AIE_EXCH, EV_d[:, 0])
+    V = e[4:20].reshape(4, 4)
+    rates = plfx.gamma_rates(AIE_ALPHA, 4)
+    n = 37
+    # slots 0-3 tips, 4-5 cherries, 6 root; ops: [parent, child1, child2, pmat pair]
+    ops = np.array([[4, 0, 1, 0], [5, 2, 3, 0], [6, 4, 5, 0]], np.int32)
+    pm = torch.empty(2 * 64, dtype=tdt, device="cuda")
+    ctx.pmatrix(dev(e), dev(rates), dev(np.array([AIE_T, AIE_T])), pm, states=4,
+                convention=plfx.PMAT_EIGEN)
+    EV = dev(plfx.model_ev(e, 4, plfx.PMAT_EIGEN)).to(tdt)
+    tipvec = dev(plfx.model_tip_vectors(e, plfx.PMAT_EIGEN)).to(tdt)
+    codes = torch.full((n,), 1, dtype=torch.uint8, device="cuda")  # bit 0 = A
+    clv = [None] * 4 + [torch.empty(16 * n, dtype=tdt, device="cuda") for _ in range(3)]
+    ctx.traverse(ops, clv, pm, EV, n, tips=[codes] * 4 + [None] * 3, tipvec=tipvec)
+    torch.cuda.synchronize()
+    root = clv[6].cpu().numpy().astype(np.float64).reshape(n, 4, 4)
+    gold = k["golden"].astype(np.float64).reshape(4, 4)
+    tol = 2e-6 if dtype == "f64" else 2e-5
+    for s in range(n):
+        assert np.abs(root[s] @ V.T - gold @ V_d.T).max() < tol, s
