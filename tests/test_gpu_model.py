@@ -217,7 +217,8 @@ def test_traversal_with_coded_tips_reproduces_reference_aie_golden(ctx, dtype):
     A tips as uint8 state codes, the library's eigen-convention tip-vector
     table, one P-matrix pair per inner node from plfx_pmatrix): the root CLV
     equals the reference's golden in state coordinates (f64 to the goldens'
-    six decimals, f32 to float rounding)."""
+    six decimals, f32 to float rounding), and so does its root lnL with the
+    eigen-convention root weights."""
     import torch
 
     from conftest import golden
@@ -247,3 +248,11 @@ def test_traversal_with_coded_tips_reproduces_reference_aie_golden(ctx, dtype):
     tol = 2e-6 if dtype == "f64" else 2e-5
     for s in range(n):
         assert np.abs(root[s] @ V.T - gold @ V_d.T).max() < tol, s
+    # the root lnL with the eigen-convention root weights (w = V^T pi) equals
+    # n x log of the golden's state-space likelihood, sum_c 1/4 sum_s pi_s x_s
+    w = dev(plfx.model_root_weights(e, EV_d[:, 0], plfx.PMAT_EIGEN))
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    ctx.root_lnl(clv[6], n, out, catw=dev(np.full(4, 0.25)), freq=w)
+    torch.cuda.synchronize()
+    ref = n * np.log(np.sum(0.25 * (gold @ V_d.T) @ EV_d[:, 0]))
+    assert abs(out.item() - ref) < (1e-5 if dtype == "f64" else 1e-4) * abs(ref)
