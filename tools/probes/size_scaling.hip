@@ -14,6 +14,7 @@
 //   segS    (second run: not kept) S = 16, 32, 64 segments -- at best like xcd
 //   tileT   block b takes tiles b, b + G, ... of T contiguous sites (the
 //           protein kernels' shape), its 4 waves the tile's steps in turn
+//   queueC  (QUEUE=1 with MODES) chunks of 2^C sites from a device-wide counter
 //   chunkK  (first run: not kept) sites cut into chunks of 2^K, chunk j to XCD
 //           j % 8, each XCD striding over its own chunks -- ran like stride
 // GB/s are of the 385 B per site the node kernel moves (the 1-B scaler omitted
@@ -86,6 +87,50 @@ __global__ void __launch_bounds__(256) pass_tile(const f64x2 *__restrict__ x1,
 
 // UU: 8-site blocks per wave trip (2 = 16 sites; the product's f64 kernel
 // covers 32 sites per trip, UU = 4)
+// queueC: blocks take chunks of 2^C contiguous sites from a device-wide
+// counter (one returning atomic per chunk, thread 0, broadcast through LDS);
+// the block's 4 waves take the chunk's 16-site steps in turn.  `ctr` is zero
+// at launch and reset by the last block out (done counter).
+template <int C>
+__global__ void __launch_bounds__(256) pass_queue(const f64x2 *__restrict__ x1,
+                                                  const f64x2 *__restrict__ x2,
+                                                  f64x2 *__restrict__ x3, int64_t n,
+                                                  unsigned long long *ctr) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  constexpr int64_t step = 8 * U;
+  const int64_t nchunks = (n + (1ll << C) - 1) >> C;
+  __shared__ long long chunk;
+  for (;;) {
+    if (threadIdx.x == 0)
+      chunk = (long long)__hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const long long c = chunk;
+    __syncthreads();
+    if (c >= nchunks) break;
+    const int64_t t0 = c << C, t1 = t0 + (1ll << C) < n ? t0 + (1ll << C) : n;
+    for (int64_t base = t0 + w * step; base < t1; base += kWaves * step) {
+      f64x2 a[U], b[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t s = base + 8 * u < n ? base + 8 * u : n - 8;
+        a[u] = __builtin_nontemporal_load(x1 + s * 8 + lane);
+        b[u] = __builtin_nontemporal_load(x2 + s * 8 + lane);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (base + 8 * u < t1) __builtin_nontemporal_store(a[u] * b[u], x3 + (base + 8 * u) * 8 + lane);
+    }
+  }
+  if (threadIdx.x == 0) {
+    const unsigned long long d = __hip_atomic_fetch_add(ctr + 16, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == gridDim.x - 1) {
+      __hip_atomic_store(ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 16, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <int kMode, int S = 8, int UU = U>  // 0 stride, 1 segments (S = 8: one per XCD), 2 blocked
 __global__ void __launch_bounds__(256) pass(const f64x2 *__restrict__ x1, const f64x2 *__restrict__ x2,
                                             f64x2 *__restrict__ x3, int64_t n) {
@@ -170,6 +215,26 @@ int main(int argc, char **argv) {
     std::printf("bpc=%d n=%-11lld %-8s %11.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", bpc, (long long)n, mode,
                 us, gbs, gbs / 8000);
   };
+  unsigned long long *ctr = nullptr;
+  CK(hipMalloc(&ctr, 4096));
+  CK(hipMemset(ctr, 0, 4096));
+  auto timeq = [&](auto kern, const char *mode, int64_t n, int64_t off) {
+    const int sets = off ? 4 : 1;
+    const int reps = n >= (1 << 26) ? 3 : 20;
+    for (int i = 0; i < 2; i++) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, x1, x2, x3, n, ctr);
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; i++) {
+      const int64_t o = (i % sets) * off * 8;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, x1 + o, x2 + o, x3 + o, n, ctr);
+    }
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / reps, gbs = 385.0 * n / (us * 1e-6) / 1e9;
+    std::printf("bpc=%d n=%-11lld %-8s %11.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", bpc, (long long)n, mode,
+                us, gbs, gbs / 8000);
+  };
   std::vector<int64_t> sizes = {1 << 20, 1 << 22, 1 << 24, 1 << 25, 1 << 26, 1 << 27, 1 << 28, nmax};
   if (const char *s = std::getenv("SIZES")) {  // comma-separated site counts
     sizes.clear();
@@ -186,8 +251,13 @@ int main(int argc, char **argv) {
       time1(pass<0>, "stride", n, off);
       time1(pass<1>, "xcd", n, off);
       if (only_sx) {
-        time1(pass<0, 8, 4>, "stride32", n, off);
-        time1(pass<1, 8, 4>, "xcd32", n, off);
+        if (std::getenv("QUEUE")) {
+          timeq(pass_queue<14>, "queue14", n, off);
+          timeq(pass_queue<16>, "queue16", n, off);
+        } else {
+          time1(pass<0, 8, 4>, "stride32", n, off);
+          time1(pass<1, 8, 4>, "xcd32", n, off);
+        }
         continue;
       }
       time1(pass<2>, "blocked", n, off);
