@@ -1245,8 +1245,9 @@ struct DeepDesc {
   int64_t *ss[63];
 };
 
-template <int D, bool kSum, bool NTL, int U, int kThreads, int kTips = 0, bool kDyn = false>
-__global__ void __launch_bounds__(kThreads, 1)
+template <int D, bool kSum, bool NTL, int U, int kThreads, int kTips = 0, bool kDyn = false,
+          int kMinW = 1>
+__global__ void __launch_bounds__(kThreads, kMinW)
 plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
                         const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
                         const double *__restrict__ tipvec = nullptr) {

@@ -105,13 +105,14 @@ int cu_count() {
 // buffers, calls alternating (tools/max_sites.py --ab, three boxes,
 // profiles/r05_node_segments_ab.log): f32 +3-4 % at 2^25 sites, +9-29 % from
 // 5e7 up; f64 +1 % at 2^26, +5-12 % from 1e8 up -- and both 6-8 % SLOWER at
-// 2^24, equal below.  Returns the segmented launch's grid, a multiple of 8
-// (blocks b and b + 8 share an XCD; the grid rounded down, or up to 8 blocks
-// under a smaller cap), or 0: not segmented.
+// 2^24, equal below.  Returns the segmented launch's grid -- the capped grid
+// gx rounded down to a multiple of 8 (blocks b and b + 8 share an XCD) -- or
+// 0: not segmented.  Never more blocks than gx: below 8 (a small node, or a
+// PLFX_MAX_BLOCKS cap < 8) the one-window mapping runs instead.
 constexpr int64_t kSegMinSites32 = int64_t(1) << 25, kSegMinSites64 = int64_t(1) << 26;
 int64_t segment_grid(const DnaArgs &a, int64_t gx, int64_t min_sites) {
-  if (a.segments == 0 || (a.segments < 0 && a.n < min_sites)) return 0;
-  return gx >= 8 ? gx - gx % 8 : 8;
+  if (a.segments == 0 || (a.segments < 0 && a.n < min_sites) || gx < 8) return 0;
+  return gx - gx % 8;
 }
 
 template <typename T, bool kSum>

@@ -622,7 +622,18 @@ int plfx_ctx_create_ex(int device, unsigned flags, plfx_ctx **out) {
     if (v > 0) ctx->max_blocks = v;
   }
   if (const char *env = std::getenv("PLFX_FUSE")) ctx->fuse = std::atoi(env);
-  if (const char *env = std::getenv("PLFX_NODE_SEGMENTS")) ctx->node_segments = std::atoi(env) > 0 ? 1 : 0;
+  // PLFX_NODE_SEGMENTS: "1" on, "0" off, "-1" / "auto" / unset by size; any
+  // other value is refused (a typo must not silently switch the mapping)
+  if (const char *env = std::getenv("PLFX_NODE_SEGMENTS")) {
+    if (!std::strcmp(env, "1")) ctx->node_segments = 1;
+    else if (!std::strcmp(env, "0")) ctx->node_segments = 0;
+    else if (!std::strcmp(env, "-1") || !std::strcmp(env, "auto") || !*env) ctx->node_segments = -1;
+    else {
+      (void)hipStreamDestroy(ctx->stream);
+      delete ctx;
+      return PLFX_ERR_INVALID;
+    }
+  }
   // the workspace pool: kWsPool entries (reduction words zeroed before return,
   // tip/tip tables), and the tables' constant code arrays
   auto undo = [&](int code) {

@@ -174,8 +174,11 @@ int plfx_plf_f64(plfx_ctx *ctx, const double *x1_start, const double *x2_start,
  * each optional (NULL = not produced / not read).  n may be 0.  From 2^25
  * sites (f32) / 2^26 (f64) the kernel deals the sites to the 8 XCDs as eight
  * contiguous segments instead of one grid-wide stride -- same bits, +1-29 %
- * HBM rate on long CLVs; env PLFX_NODE_SEGMENTS=0/1,
- * read at context creation, forces one mapping or the other. */
+ * HBM rate on long CLVs; env PLFX_NODE_SEGMENTS,
+ * read at context creation: "1" forces the segments, "0" the one window,
+ * "-1" / "auto" / "" keep the choice by size; any other value makes context
+ * creation fail with PLFX_ERR_INVALID.  Segments need 8 blocks: under a grid
+ * cap below 8 (PLFX_MAX_BLOCKS) the one window runs. */
 int plfx_plf_dev_f32(plfx_ctx *ctx, const float *x1, const float *x2, float *x3,
                      const float *EV, int64_t n, const float *left,
                      const float *right, const int32_t *wgt, uint8_t *scaler,

@@ -260,3 +260,49 @@ def test_pmc_tools_record_launch_shapes():
     assert pt.shapes(ROOT / "profiles" / "r04_node_pmc_fetch.csv", "plf_dna_f64_pair_kernel") == [[262144, 256]]
     tree = ps.launch_shapes(ROOT / "profiles" / "r04_tree64_pmc_fetch.csv")
     assert tree["plf_dna_f64_deep_kernel"] == [[131072, 512]]
+
+
+def test_sub_records_arguments():
+    """The default invocation's sub-records: configs[3] / [2] at --sites,
+    configs[4] at --sites / 4 (2^18 by default) with at least 200 timed steps
+    after 300 warm-up ones, exact only for protein_exact; opt-outs parse."""
+    a = bench.parse(["--steps", "20", "--warmup", "5"])
+    assert bench.SUB_RECORDS == ("nodes512", "tree64", "protein", "protein_exact")
+    t = bench.sub_args(a, "tree64")
+    assert (t.workload, t.sites, t.steps, t.warmup, t.exact, t.tips) == ("tree64", 1 << 20, 20, 5, False, False)
+    p = bench.sub_args(a, "protein")
+    assert (p.workload, p.sites, p.steps, p.warmup, p.exact) == ("protein", 1 << 18, 200, 300, False)
+    e = bench.sub_args(a, "protein_exact")
+    assert e.exact and e.sites == 1 << 18 and bench.traffic_name(e) == "protein_exact"
+    assert bench.traffic_key(t) == "tree64:f64:fma:dense:fuse3:sites1048576"
+    assert bench.traffic_key(p) == "protein:f64:fma:dense:fuse3:sites262144"
+    assert a.workload == "node" and a.steps == 20  # the line's own arguments are untouched
+    b = bench.parse(["--no-tree64", "--no-protein", "--corrupt-rank", "1"])
+    assert b.no_tree64 and b.no_protein and b.corrupt_rank == 1
+    assert bench.parse([]).corrupt_rank == -1
+
+
+def test_common_start_only_on_one_node():
+    """the agreed start instant only when every rank shares this
+    node's CLOCK_MONOTONIC and the clocks agree within 1 s; ranks on several
+    machines (LOCAL_WORLD_SIZE < WORLD_SIZE) or far-apart clocks start on
+    their own after the barrier, never spinning on another machine's clock."""
+    assert bench.use_common_start(10.0005, 10.0, 8, {"LOCAL_WORLD_SIZE": "8"})
+    assert bench.use_common_start(10.0005, 10.0, 2, {})
+    assert not bench.use_common_start(10.0005, 10.0, 16, {"LOCAL_WORLD_SIZE": "8"})
+    assert not bench.use_common_start(86400.0, 10.0, 8, {"LOCAL_WORLD_SIZE": "8"})
+    assert not bench.use_common_start(1.0, 1.0, 8, {"LOCAL_WORLD_SIZE": "x"})
+
+
+def test_flip_bit_and_window_offsets():
+    """The --corrupt-rank hook flips exactly the lowest bit of one element."""
+    import torch
+
+    t = torch.arange(8, dtype=torch.float64)
+    before = t.clone()
+    bench.flip_bit(t, 5)
+    diff = (t.view(torch.int64) ^ before.view(torch.int64)).tolist()
+    assert diff == [0, 0, 0, 0, 0, 1, 0, 0]
+    f = torch.ones(4, dtype=torch.float32)
+    bench.flip_bit(f, 0)
+    assert f[0].item() != 1.0 and f[1:].eq(1).all()

@@ -287,11 +287,12 @@ def test_plf_dev_xcd_segments_full_compare(ctx, oracle, monkeypatch, dtype):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("n", [1, 7, 100, 1000, 4097, 65539, 300001])
+@pytest.mark.parametrize("n", [1, 7, 100, 1000, 1025, 4097, 65539, 300001])
 def test_plf_dev_xcd_segments_forced_small(ctx, oracle, monkeypatch, n):
-    """The segmented mapping forced on at small and ragged sizes, where most
-    of the eight segments are short or empty (a segment's first site past n):
-    bit-exact against the oracle, f32 and f64, scaler sums exact."""
+    """The segmented mapping forced on at small and ragged sizes, where the
+    eight segments are short or ragged (below 8 blocks of work, n <= 1024 f64,
+    the one window runs instead): bit-exact against the oracle, f32 and f64,
+    scaler sums exact."""
     import torch
 
     on = segments_ctx(monkeypatch, "1")
@@ -310,6 +311,73 @@ def test_plf_dev_xcd_segments_forced_small(ctx, oracle, monkeypatch, n):
             assert int(s.item()) == einc
     finally:
         on.close()
+
+
+def _captured_grids(call):
+    """[(kernel name, workgroups, workgroup size)] of the launches `call`
+    makes, read from the kernel nodes of a captured graph (what the graph
+    will dispatch), then the graph is replayed once."""
+    import torch
+
+    import bench
+
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g, stream=st):
+        call(st.cuda_stream)
+    out = [(name, grid // wg, wg) for name, grid, wg in bench.graph_kernel_launches(g)]
+    g.instantiate()
+    with torch.cuda.stream(st):
+        g.replay()
+    torch.cuda.synchronize()
+    del g
+    return out
+
+
+@pytest.mark.parametrize("cap", [4, 12])
+def test_segment_grid_never_exceeds_block_cap(oracle, monkeypatch, cap):
+    """with the segments forced on (PLFX_NODE_SEGMENTS=1)
+    and a grid cap (PLFX_MAX_BLOCKS), the node kernel never launches more
+    blocks than the cap -- below 8 the one-window mapping runs, at 12 the
+    segmented grid is 8 -- and stays bit-exact, f32 and f64, at 2^20 sites
+    (where the uncapped grid is far larger).  Invalid env values are refused."""
+    import torch
+
+    import plfx
+
+    monkeypatch.setenv("PLFX_MAX_BLOCKS", str(cap))
+    monkeypatch.setenv("PLFX_NODE_SEGMENTS", "1")
+    c = plfx.Context(0)
+    monkeypatch.delenv("PLFX_MAX_BLOCKS")
+    monkeypatch.delenv("PLFX_NODE_SEGMENTS")
+    n = 1 << 20
+    try:
+        for dtype in (np.float32, np.float64):
+            d = oracle.gen_hostmem(n, dtype, 17)
+            e3, esc, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+            t = {k: torch_dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+            x3 = torch.empty_like(t["x1"])
+            sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+            s = torch.zeros(1, dtype=torch.int64, device="cuda")
+            grids = _captured_grids(lambda sh: c.plf_dev(t["x1"], t["x2"], x3, t["EV"], t["left"], t["right"],
+                                                         t["wgt"], sc, s, stream=sh))
+            node = [x for x in grids if x[0] and "plf_dna" in x[0]]
+            assert len(node) == 1, grids
+            assert node[0][1] == (8 if cap >= 8 else cap), grids
+            assert np.array_equal(bits(x3.cpu().numpy()), bits(e3))
+            assert np.array_equal(sc.cpu().numpy(), esc) and int(s.item()) == einc
+            del t, x3, sc, s
+    finally:
+        c.close()
+    for bad in ("2", "yes", "on"):
+        monkeypatch.setenv("PLFX_NODE_SEGMENTS", bad)
+        with pytest.raises(Exception):
+            plfx.Context(0)
+    for good in ("auto", "-1", "0"):
+        monkeypatch.setenv("PLFX_NODE_SEGMENTS", good)
+        plfx.Context(0).close()
+    monkeypatch.delenv("PLFX_NODE_SEGMENTS")
 
 
 def test_plf_dev_repeated_calls_and_optional_outputs(ctx, oracle):
