@@ -147,7 +147,10 @@ constexpr size_t kWsEntryBytes = kWsBytes + kLnlPartialBytes + kLnlTicketBytes;
 // scaler bytes, in every workspace entry (written by the table kernel before
 // each use, so never zeroed), and the two constant 576-code arrays (combo
 // k = code1 * 24 + code2) once per context.  Allocated with the entries, so
-// a stream's first tip/tip call -- also inside a capture -- takes the tables.
+// a stream's first tip/tip call -- also inside a capture -- takes the tables;
+// under PLFX_CTX_LAZY_TABLES they are allocated on an entry's first tip/tip
+// call instead, and that first call is refused (PLFX_ERR_INVALID) inside a
+// capture.
 constexpr size_t kTtCodeBytes = 2048;
 constexpr size_t kTtTabBytes = (size_t)plfx::kProtCombos * 80 * sizeof(double);
 constexpr size_t kTtScBytes = 1024;

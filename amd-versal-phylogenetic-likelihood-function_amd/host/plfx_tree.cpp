@@ -21,11 +21,13 @@
 // entry; every GPU sweeps the whole tree over its own site block (its P
 // matrices, traversal and root lnL).  The per-GPU lnL and the per-node scaler
 // totals are then summed by ONE RCCL all-reduce over the listed GPUs
-// (--reduce rccl, the default: ncclCommInitAll over the list, a grouped
+// (--reduce rccl, the default when the list names at least two distinct GPUs:
+// ncclCommInitAll over the list, a grouped
 // ncclAllReduce of f64 lnL + int64[inner nodes] on the GPUs' streams,
 // plfx_rccl.hpp) -- the north star's single all-reduce over xGMI -- or, with
-// --reduce host, copied back and added on the host in list order (a device
-// may then be listed twice: two contexts on one GPU; RCCL refuses that).  The
+// --reduce host -- the default for one GPU or a list that repeats a GPU --
+// copied back and added on the host in list order (a device may then be
+// listed twice: two contexts on one GPU; RCCL refuses that).  The
 // reduction that ran is printed ("reduce = ...").  Same value as one GPU up
 // to the summation order.
 //
@@ -89,7 +91,8 @@ struct Opts {
   double alpha = 0.5;
   uint32_t seed = 20250117u;
   std::vector<int> devices{0};
-  bool rccl = true;  // --reduce rccl (default) | host
+  int reduce = -1;  // --reduce rccl (1) | host (0); default (-1): rccl over >= 2 distinct GPUs, else host
+  bool rccl = false;  // resolved from `reduce` and the device list
 };
 
 // One GPU's share: its context, its site block [off, off + n) and the device
@@ -365,8 +368,8 @@ int main(int argc, char **argv) {
       o.fma = true;
     } else if (a == "--reduce") {
       const std::string v = next();
-      if (v == "rccl") o.rccl = true;
-      else if (v == "host") o.rccl = false;
+      if (v == "rccl") o.reduce = 1;
+      else if (v == "host") o.reduce = 0;
       else die("bad reduction " + v + " (rccl|host)");
     } else if (a == "--devices") {
       o.devices.clear();
@@ -388,5 +391,11 @@ int main(int argc, char **argv) {
   }
   if (o.taxa < 2 || (o.taxa & (o.taxa - 1))) die("taxa must be a power of 2 >= 2");
   if (o.sites < 1 || o.sweeps < 1) die("sites and sweeps must be >= 1");
+  {
+    std::vector<int> d = o.devices;
+    std::sort(d.begin(), d.end());
+    const bool distinct = std::adjacent_find(d.begin(), d.end()) == d.end();
+    o.rccl = o.reduce == 1 || (o.reduce < 0 && distinct && d.size() >= 2);
+  }
   return o.f64 ? run<double>(o) : run<float>(o);
 }

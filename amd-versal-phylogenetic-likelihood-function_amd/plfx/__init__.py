@@ -174,9 +174,30 @@ class Context:
                                 "(no gfx950 device visible?)")
         self.h = h
         self.device = device
+        self._used = {}  # torch streams this context ran on: released at close()
+
+    def _sh(self, stream):
+        """The hipStream_t of `stream` (None: torch's current stream on the
+        context's device), remembering torch streams so that close() can
+        release their workspaces (plfx_ctx_release_stream) and destroy stays
+        off the device-wide wait.  Raw integer handles are not remembered (the
+        stream may be destroyed before the context): release those yourself."""
+        if stream is None:
+            import torch
+
+            stream = torch.cuda.current_stream(self.device)
+        if not isinstance(stream, int):
+            self._used[stream.cuda_stream] = stream
+        return _stream_handle(stream, self.device)
 
     def close(self):
         if getattr(self, "h", None):
+            for st in list(getattr(self, "_used", {}).values()):
+                try:  # refused (and left to destroy) while the stream is being captured
+                    self._L.plfx_ctx_release_stream(self.h, C.c_void_p(st.cuda_stream))
+                except Exception:
+                    pass
+            self._used = {}
             self._L.plfx_ctx_destroy(self.h)
             self.h = None
 
@@ -202,7 +223,9 @@ class Context:
     def release_stream(self, stream):
         """Wait for `stream` and return its scaler-sum workspace to the pool
         (plfx_ctx_release_stream)."""
-        self._check(self._L.plfx_ctx_release_stream(self.h, _stream_handle(stream, self.device)))
+        h = _stream_handle(stream, self.device)
+        self._check(self._L.plfx_ctx_release_stream(self.h, h))
+        self._used.pop(h.value, None)
 
     def _check(self, rc):
         if rc != OK:
@@ -263,7 +286,7 @@ class Context:
         fn = self._L.plfx_plf_dev_f32 if dt == torch.float32 else self._L.plfx_plf_dev_f64
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         self._check(fn(self.h, p(x1), p(x2), p(x3), p(EV), n, p(left), p(right), p(wgt),
-                       p(scaler), p(scaler_sum), _stream_handle(stream, self.device)))
+                       p(scaler), p(scaler_sum), self._sh(stream)))
 
     def bind_plf_dev(self, x1, x2, x3, EV, left, right, wgt=None, scaler=None, scaler_sum=None,
                      n=None):
@@ -288,7 +311,7 @@ class Context:
         def run(stream=None):
             if self.h is None:  # args carry the handle: a closed context's would dangle
                 raise PlfxError(ERR_INVALID, "launcher used after its context was closed")
-            check(fn(*args, _stream_handle(stream, self.device)))
+            check(fn(*args, self._sh(stream)))
 
         run.tensors = held
         return run
@@ -312,7 +335,7 @@ class Context:
         self._check(self._L.plfx_instance_run(self.h, p(in_left), p(in_right), p(out_clv),
                                               p(out_scaler), n, int(window_size), int(layout),
                                               F32 if dt == torch.float32 else F64,
-                                              _stream_handle(stream, self.device)))
+                                              self._sh(stream)))
 
     def instance_run_host(self, in_left, in_right, out_clv, out_scaler, alignment_sites,
                           window_size, layout):
@@ -362,7 +385,7 @@ class Context:
         self._check(self._L.plfx_plf_dev_gen(self.h, F32 if dt == torch.float32 else F64, int(states),
                                              FMA if fma else EXACT, p(x1), p(x2), p(x3), p(EV), n,
                                              p(left), p(right), p(wgt), p(scaler), p(scaler_sum),
-                                             _stream_handle(stream, self.device)))
+                                             self._sh(stream)))
 
     # -- (6) batched nodes / traversal ---------------------------------------
     def plf_batch_dev(self, nodes, EV, n, wgt=None, stream=None, states=4):
@@ -395,7 +418,7 @@ class Context:
             raise PlfxError(ERR_INVALID, f"EV must be a contiguous device tensor of {states * states} values")
         self._check(self._L.plfx_plf_batch_dev(self.h, F32 if dt == torch.float32 else F64, states, arr,
                                                len(nodes), C.c_void_p(EV.data_ptr()), int(n),
-                                               C.c_void_p(ptr(wgt)), _stream_handle(stream, self.device)))
+                                               C.c_void_p(ptr(wgt)), self._sh(stream)))
 
     def bind_plf_batch_dev(self, nodes, EV, n, wgt=None, states=4):
         """Validate once (as plf_batch_dev) and return a launcher
@@ -413,7 +436,7 @@ class Context:
         arr = (Node * len(nodes))(*[Node(ptr(nd["x1"]), ptr(nd["x2"]), ptr(nd["x3"]), ptr(nd["left"]),
                                          ptr(nd["right"]), ptr(nd.get("scaler")),
                                          ptr(nd.get("scaler_sum"))) for nd in nodes])
-        fn, h, check, dev = self._L.plfx_plf_batch_dev, self.h, self._check, self.device
+        fn, h, check = self._L.plfx_plf_batch_dev, self.h, self._check
         args = (F32 if EV.dtype == torch.float32 else F64, states, arr, len(nodes),
                 C.c_void_p(EV.data_ptr()), int(n), C.c_void_p(ptr(wgt)))
 
@@ -422,7 +445,7 @@ class Context:
         def run(stream=None):
             if ctx.h is None:  # h would dangle
                 raise PlfxError(ERR_INVALID, "launcher used after its context was closed")
-            check(fn(h, *args, _stream_handle(stream, dev)))
+            check(fn(h, *args, ctx._sh(stream)))
 
         run.tensors = ([dict(nd) for nd in nodes], EV, wgt)  # raw pointers in arr / args
         return run
@@ -489,7 +512,7 @@ class Context:
             C.c_void_p(EV.data_ptr()), int(n),
             C.c_void_p(None if wgt is None else wgt.data_ptr()), sc,
             C.c_void_p(None if scaler_sums is None else scaler_sums.data_ptr()),
-            self._tipvec(tipvec, dt, states), _stream_handle(stream, self.device)))
+            self._tipvec(tipvec, dt, states), self._sh(stream)))
 
     @staticmethod
     def _tipvec(tipvec, dt, states=4):
@@ -529,7 +552,7 @@ class Context:
         self._check(self._L.plfx_plf_tips_dev_gen(
             self.h, F32 if dt == torch.float32 else F64, states, FMA if fma else EXACT, p(tip1),
             p(x1), p(tip2), p(x2), p(x3), p(EV), int(n), p(left), p(right), p(wgt), p(scaler),
-            p(scaler_sum), self._tipvec(tipvec, dt, states), _stream_handle(stream, self.device)))
+            p(scaler_sum), self._tipvec(tipvec, dt, states), self._sh(stream)))
 
     def last_schedule(self):
         """The schedule the last traverse() on this context chose
@@ -558,7 +581,7 @@ class Context:
         self._check(self._L.plfx_pmatrix(
             self.h, F32 if out.dtype == torch.float32 else F64, S, convention,
             C.c_void_p(eigen.data_ptr()), C.c_void_p(rates.data_ptr()), ncat,
-            C.c_void_p(blen.data_ptr()), nb, C.c_void_p(out.data_ptr()), _stream_handle(stream, self.device)))
+            C.c_void_p(blen.data_ptr()), nb, C.c_void_p(out.data_ptr()), self._sh(stream)))
 
     # -- (7) root log-likelihood --------------------------------------------
     def root_lnl(self, x, n, out, catw=None, freq=None, wgt=None, scaler_sums=None,
@@ -584,7 +607,7 @@ class Context:
         nsums = 0 if scaler_sums is None else scaler_sums.numel()
         self._check(self._L.plfx_root_lnl(self.h, F32 if x.dtype == torch.float32 else F64, states,
                                           p(x), int(n), p(catw), p(freq), p(wgt), p(scaler_sums),
-                                          nsums, p(out), p(site_lnl), _stream_handle(stream, self.device)))
+                                          nsums, p(out), p(site_lnl), self._sh(stream)))
 
     # -- (4) scaler reduction ----------------------------------------------
     def scaler_sum(self, scaler, wgt, out_sum, n=None, stream=None):
@@ -597,7 +620,7 @@ class Context:
         _check_aux(n, wgt, scaler, out_sum)
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         self._check(self._L.plfx_scaler_sum(self.h, p(scaler), p(wgt), int(n), p(out_sum),
-                                            _stream_handle(stream, self.device)))
+                                            self._sh(stream)))
 
 
 def _stream_handle(stream, device=None):

@@ -891,3 +891,34 @@ def test_bound_launcher_after_close_raises(oracle):
     for r in (run, runb):
         with pytest.raises(plfx.PlfxError):
             r()
+
+
+def test_context_releases_its_torch_streams_on_close(oracle):
+    """a Context remembers the torch streams it ran on and
+    releases their workspaces at close() (plfx_ctx_release_stream), so
+    destroy does not fall back to a device-wide wait; raw integer handles are
+    not remembered; release_stream() forgets the stream."""
+    import torch
+
+    import plfx
+
+    n = 4099
+    d = oracle.gen_hostmem(n, np.float64, 3)
+    t = {k: torch.from_numpy(d[k]).cuda() for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+    x3 = torch.empty_like(t["x1"])
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    c = plfx.Context(0)
+    args = (t["x1"], t["x2"], x3, t["EV"], t["left"], t["right"], t["wgt"], None, s)
+    c.plf_dev(*args, stream=a)
+    c.plf_dev(*args, stream=b)
+    c.plf_dev(*args, stream=b.cuda_stream)   # raw handle: not remembered
+    c.plf_dev(*args)                          # torch's current stream
+    assert set(c._used) == {a.cuda_stream, b.cuda_stream, torch.cuda.current_stream().cuda_stream}
+    c.release_stream(a)
+    assert a.cuda_stream not in c._used
+    torch.cuda.synchronize()
+    c.close()
+    assert c._used == {} and c.h is None
+    e3, _, _ = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+    assert np.array_equal(x3.cpu().numpy().view(np.uint64), e3.view(np.uint64))

@@ -233,7 +233,8 @@ def test_plf_dev_reference_sweep_maximum(ctx, oracle, dtype, n):
 
 def segments_ctx(monkeypatch, mode):
     """A context whose node kernels use the XCD-segmented site mapping always
-    (mode "1") or never ("0"); the default picks it from 2^24 sites up."""
+    (mode "1") or never ("0"); the default picks it by size, from 2^25 sites
+    up in f32 and 2^26 in f64 (plf_kernels.hip kSegMinSites32 / 64)."""
     import plfx
 
     monkeypatch.setenv("PLFX_NODE_SEGMENTS", mode)

@@ -648,7 +648,11 @@ def test_tree_driver_rccl_allreduce():
     for k in (0, 4):
         (a, ea), (b, eb) = out[("rccl", k)], out[("host", k)]
         assert abs(a - b) <= 1e-12 * abs(b) and ea == eb and ea > 0
-    assert "RCCL" in _run_driver(exe, 16, 5000, 1, "--devices", 0).stdout  # the default is rccl
+    # the default: RCCL over >= 2 distinct GPUs, else the host sum (ADVICE r05:
+    # a one-GPU run or a repeated list does not depend on RCCL initialising)
+    assert "reduce = host (1 part" in _run_driver(exe, 16, 5000, 1, "--devices", 0).stdout
+    rep = _run_driver(exe, 16, 5000, 1, "--devices", "0,0")
+    assert rep.returncode == 0 and "reduce = host (2 parts" in rep.stdout
     bad = _run_driver(exe, 16, 5000, 1, "--devices", "0,0", "--reduce", "rccl")
     assert bad.returncode != 0 and "distinct GPUs" in bad.stderr
 

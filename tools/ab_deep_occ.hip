@@ -11,8 +11,11 @@
 // product's placement went 0.644 -> 0.775 from 1 to 2 blocks/CU
 // (tools/probes/tree_placement.hip, profiles/r05_probe_tree_bpc.log).
 //
-// Placement is the product's: one hipMalloc per CLV (what the bench's torch
-// tensors get).  Inputs: tips U[0,1), P and EV U[0,1) x 0.25 (bench.py
+// Four placements of the 127 CLVs in one process (one hipMalloc per CLV --
+// the bench's -- in allocation order and reversed; one slab; the slab with a
+// 6-MiB gap per CLV), since the pass's rate moves with where the buffers'
+// pages fall and a box shows only some of the behaviours in one
+// layout.  Inputs: tips U[0,1), P and EV U[0,1) x 0.25 (bench.py
 // Tree64Workload), wgt = 1, scaler sums on.  Variants alternate in one
 // process; every variant's 63 CLVs and 63 scaler sums must equal the
 // product's bit for bit (checked each round).
@@ -22,6 +25,7 @@
 //   build/ab_deep_occ [log2 sites] [rounds]
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -63,31 +67,52 @@ Variant make(const char *name) {
   return v;
 }
 
+// the pass's 127 CLVs placed one of four ways (tools/probes/tree_placement.hip:
+// the same code runs 0.64-0.79 of 8 TB/s by placement alone)
+enum Place { kSep, kSepRev, kSlab, kSlabGap6M, kPlaces };
+const char *kPlaceName[] = {"sep", "sep-rev", "slab", "slab+6M"};
+
+struct Tree {
+  DeepDesc d;
+  std::vector<void *> allocs;
+};
+
+Tree place(Place p, size_t clv_bytes) {
+  Tree t;
+  memset(&t.d, 0, sizeof(t.d));
+  void *bufs[127];
+  if (p == kSep || p == kSepRev) {
+    for (int i = 0; i < 127; i++) {
+      CK(hipMalloc(&bufs[i], clv_bytes));
+      t.allocs.push_back(bufs[i]);
+    }
+    if (p == kSepRev) std::reverse(bufs, bufs + 127);
+  } else {
+    const size_t gap = p == kSlabGap6M ? (size_t)6 << 20 : 0, step = clv_bytes + gap;
+    char *slab;
+    CK(hipMalloc(&slab, 127 * step));
+    t.allocs.push_back(slab);
+    for (int i = 0; i < 127; i++) bufs[i] = slab + i * step;
+  }
+  for (int i = 0; i < 64; i++) t.d.g[i] = bufs[i];
+  for (int i = 0; i < 63; i++) t.d.x[i] = bufs[64 + i];
+  return t;
+}
+
 int main(int argc, char **argv) {
   const int lg = argc > 1 ? atoi(argv[1]) : 20;
-  const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 3;
   const int64_t n = int64_t(1) << lg;
   const size_t clv = (size_t)n * 16;
   std::mt19937_64 rng(6464);
   std::uniform_real_distribution<double> U01(0.0, 1.0);
 
-  DeepDesc d;
-  memset(&d, 0, sizeof(d));
+  std::vector<Tree> trees;
+  for (int p = 0; p < kPlaces; p++) trees.push_back(place((Place)p, clv * 8));
   std::vector<double> h(clv);
-  std::vector<void *> bufs;
   for (int i = 0; i < 64; i++) {
     for (auto &x : h) x = U01(rng);
-    void *p;
-    CK(hipMalloc(&p, clv * 8));
-    CK(hipMemcpy(p, h.data(), clv * 8, hipMemcpyHostToDevice));
-    d.g[i] = p;
-    bufs.push_back(p);
-  }
-  for (int i = 0; i < 63; i++) {
-    void *p;
-    CK(hipMalloc(&p, clv * 8));
-    d.x[i] = p;
-    bufs.push_back(p);
+    for (auto &t : trees) CK(hipMemcpy((void *)t.d.g[i], h.data(), clv * 8, hipMemcpyHostToDevice));
   }
   std::vector<double> hm(126 * 64), hev(16);
   for (auto &x : hm) x = U01(rng) * 0.25;
@@ -97,10 +122,12 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(dm, hm.data(), hm.size() * 8, hipMemcpyHostToDevice));
   CK(hipMalloc(&dev_ev, 16 * 8));
   CK(hipMemcpy(dev_ev, hev.data(), 16 * 8, hipMemcpyHostToDevice));
-  for (int i = 0; i < 126; i++) d.mat[i] = dm + 64 * i;
   int64_t *sums;
   CK(hipMalloc(&sums, 63 * 8));
-  for (int i = 0; i < 63; i++) d.ss[i] = sums + i;
+  for (auto &t : trees) {
+    for (int i = 0; i < 126; i++) t.d.mat[i] = dm + 64 * i;
+    for (int i = 0; i < 63; i++) t.d.ss[i] = sums + i;
+  }
   std::vector<int32_t> hw(n, 1);
   int32_t *wgt;
   CK(hipMalloc(&wgt, n * 4));
@@ -120,60 +147,63 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e1));
   const double bytes = (64.0 * 128 + 63.0 * 128 + 4) * n;
 
-  auto launch = [&](const Variant &v) {
+  auto launch = [&](const Variant &v, Tree &t) {
     const int64_t per_block = 8 * 8 * v.U;
     int64_t gx = (n + per_block - 1) / per_block;
     if (gx > v.resident) gx = v.resident;
-    void *args[] = {&d, &dev_ev, &wgt, (void *)&n, &ws, nullptr};
     const double *tv = nullptr;
-    args[5] = &tv;
+    void *args[] = {&t.d, &dev_ev, &wgt, (void *)&n, &ws, &tv};
     CK(hipMemsetAsync(sums, 0, 63 * 8, s));
     CK(hipLaunchKernel(v.fn, dim3((unsigned)gx), dim3(512), args, 0, s));
   };
 
-  // reference outputs: the product variant
+  // reference outputs: the product variant on the first placement
   std::vector<std::vector<double>> ref(63, std::vector<double>(clv));
   std::vector<int64_t> rsum(63), got_sum(63);
   std::vector<double> got(clv);
-  launch(vs[0]);
+  launch(vs[0], trees[0]);
   CK(hipStreamSynchronize(s));
-  for (int i = 0; i < 63; i++) CK(hipMemcpy(ref[i].data(), d.x[i], clv * 8, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 63; i++) CK(hipMemcpy(ref[i].data(), trees[0].d.x[i], clv * 8, hipMemcpyDeviceToHost));
   CK(hipMemcpy(rsum.data(), sums, 63 * 8, hipMemcpyDeviceToHost));
   int64_t events = 0;
   for (auto x : rsum) events += x;
   printf("# n = 2^%d sites, %.3f GB per pass, scaler events %lld\n", lg, bytes / 1e9, (long long)events);
 
-  std::vector<double> best(nv, 1e30), tot(nv, 0.0);
+  std::vector<double> tot(nv * kPlaces, 0.0);
   for (int r = 0; r < rounds; r++) {
-    for (int k = 0; k < nv; k++) {
-      for (int w = 0; w < 3; w++) launch(vs[k]);  // warm (same buffers, same results)
-      const int reps = 10;
-      CK(hipEventRecord(e0, s));
-      for (int i = 0; i < reps; i++) launch(vs[k]);
-      CK(hipEventRecord(e1, s));
-      CK(hipEventSynchronize(e1));
-      float ms = 0;
-      CK(hipEventElapsedTime(&ms, e0, e1));
-      const double us = ms * 1e3 / reps;
-      tot[k] += us;
-      if (us < best[k]) best[k] = us;
-      // bit-for-bit against the product
-      bool same = true;
-      CK(hipMemcpy(got_sum.data(), sums, 63 * 8, hipMemcpyDeviceToHost));
-      same = got_sum == rsum;
-      for (int i = 0; i < 63 && same; i += (r == 0 ? 1 : 9)) {
-        CK(hipMemcpy(got.data(), d.x[i], clv * 8, hipMemcpyDeviceToHost));
-        same = memcmp(got.data(), ref[i].data(), clv * 8) == 0;
+    for (int p = 0; p < kPlaces; p++) {
+      for (int k = 0; k < nv; k++) {
+        for (int w = 0; w < 3; w++) launch(vs[k], trees[p]);  // warm (same buffers, same results)
+        const int reps = 10;
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < reps; i++) launch(vs[k], trees[p]);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const double us = ms * 1e3 / reps;
+        tot[p * nv + k] += us;
+        // bit-for-bit against the product (every CLV in round 0, every 9th after)
+        CK(hipMemcpy(got_sum.data(), sums, 63 * 8, hipMemcpyDeviceToHost));
+        bool same = got_sum == rsum;
+        for (int i = 0; i < 63 && same; i += (r == 0 ? 1 : 9)) {
+          CK(hipMemcpy(got.data(), trees[p].d.x[i], clv * 8, hipMemcpyDeviceToHost));
+          same = memcmp(got.data(), ref[i].data(), clv * 8) == 0;
+        }
+        printf("%-8s %-14s round %d  %8.1f us  %7.1f GB/s  %.3f of 8 TB/s  %s\n", kPlaceName[p], vs[k].name, r,
+               us, bytes / (us * 1e-6) / 1e9, bytes / (us * 1e-6) / 8e12, same ? "bit-exact" : "MISMATCH");
+        fflush(stdout);
+        if (!same) return 2;
       }
-      printf("%-14s round %d  %8.1f us  %7.1f GB/s  %.3f of 8 TB/s  %s\n", vs[k].name, r, us,
-             bytes / (us * 1e-6) / 1e9, bytes / (us * 1e-6) / 8e12, same ? "bit-exact" : "MISMATCH");
-      fflush(stdout);
-      if (!same) return 2;
     }
   }
-  for (int k = 0; k < nv; k++)
-    printf("# %-14s mean %8.1f us (%.3f)  best %8.1f us (%.3f)\n", vs[k].name, tot[k] / rounds,
-           bytes / (tot[k] / rounds * 1e-6) / 8e12, best[k], bytes / (best[k] * 1e-6) / 8e12);
-  for (auto p : bufs) CK(hipFree(p));
+  for (int p = 0; p < kPlaces; p++)
+    for (int k = 0; k < nv; k++) {
+      const double us = tot[p * nv + k] / rounds;
+      printf("# %-8s %-14s mean %8.1f us  %.3f of 8 TB/s\n", kPlaceName[p], vs[k].name, us,
+             bytes / (us * 1e-6) / 8e12);
+    }
+  for (auto &t : trees)
+    for (auto q : t.allocs) CK(hipFree(q));
   return 0;
 }
