@@ -104,12 +104,15 @@ int cu_count() {
 // DnaArgs::segments.  The thresholds are measured, segmented vs not on the same
 // buffers, calls alternating (tools/max_sites.py --ab, three boxes,
 // profiles/r05_node_segments_ab.log): f32 +3-4 % at 2^25 sites, +9-29 % from
-// 5e7 up; f64 +1 % at 2^26, +5-12 % from 1e8 up -- and both 6-8 % SLOWER at
-// 2^24, equal below.  Returns the segmented launch's grid -- the capped grid
+// 5e7 up; f64 -2 to +1 % at 2^25, +1 % at 2^26, +5-12 % from 1e8 up -- and both
+// 6-8 % SLOWER at 2^24, equal below.  Round 6 (tools/node_placement.py, three
+// fresh buffer sets per size in one process, profiles/r06_node_placement*.log):
+// f64 at 5e7 sites +8-9 % with segments (0.74-0.77 vs 0.68-0.71), so f64 now
+// switches from 2^25 as f32 does.  Returns the segmented launch's grid -- the capped grid
 // gx rounded down to a multiple of 8 (blocks b and b + 8 share an XCD) -- or
 // 0: not segmented.  Never more blocks than gx: below 8 (a small node, or a
 // PLFX_MAX_BLOCKS cap < 8) the one-window mapping runs instead.
-constexpr int64_t kSegMinSites32 = int64_t(1) << 25, kSegMinSites64 = int64_t(1) << 26;
+constexpr int64_t kSegMinSites32 = int64_t(1) << 25, kSegMinSites64 = int64_t(1) << 25;
 int64_t segment_grid(const DnaArgs &a, int64_t gx, int64_t min_sites) {
   if (a.segments == 0 || (a.segments < 0 && a.n < min_sites) || gx < 8) return 0;
   return gx - gx % 8;

@@ -172,7 +172,7 @@ int plfx_plf_f64(plfx_ctx *ctx, const double *x1_start, const double *x2_start,
 /* All pointers are device pointers.  wgt, scaler (uint8 per site, the s2mm
  * char output) and scaler_sum (int64, = sum scaler*wgt, wgt NULL => 1) are
  * each optional (NULL = not produced / not read).  n may be 0.  From 2^25
- * sites (f32) / 2^26 (f64) the kernel deals the sites to the 8 XCDs as eight
+ * sites (f32 and f64) the kernel deals the sites to the 8 XCDs as eight
  * contiguous segments instead of one grid-wide stride -- same bits, +1-29 %
  * HBM rate on long CLVs; env PLFX_NODE_SEGMENTS,
  * read at context creation: "1" forces the segments, "0" the one window,

@@ -234,7 +234,7 @@ def test_plf_dev_reference_sweep_maximum(ctx, oracle, dtype, n):
 def segments_ctx(monkeypatch, mode):
     """A context whose node kernels use the XCD-segmented site mapping always
     (mode "1") or never ("0"); the default picks it by size, from 2^25 sites
-    up in f32 and 2^26 in f64 (plf_kernels.hip kSegMinSites32 / 64)."""
+    up in f32 and f64 (plf_kernels.hip kSegMinSites32 / 64)."""
     import plfx
 
     monkeypatch.setenv("PLFX_NODE_SEGMENTS", mode)
@@ -248,7 +248,7 @@ def segments_ctx(monkeypatch, mode):
 def test_plf_dev_xcd_segments_full_compare(ctx, oracle, monkeypatch, dtype):
     """2^24 + 13 sites through both site mappings of the node kernels -- one
     window for the whole chip, and eight segments, one per XCD (plf_dna.hpp
-    wave_sites; by default from 2^25 sites f32 / 2^26 f64) -- and the default
+    wave_sites; by default from 2^25 sites, f32 and f64) -- and the default
     choice: the WHOLE x3 and every scaler byte bit-exact against the oracle,
     segment boundaries and the ragged last segment included, with and without
     the in-kernel sum (two kernel instantiations each)."""

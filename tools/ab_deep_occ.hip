@@ -22,7 +22,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //     -I amd-versal-phylogenetic-likelihood-function_amd/csrc tools/ab_deep_occ.hip -o build/ab_deep_occ
-//   build/ab_deep_occ [log2 sites] [rounds]
+//   build/ab_deep_occ [log2 sites] [rounds] [placement index: 0 sep, 1 sep-rev, 2 slab, 3 slab+6M]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -102,13 +102,14 @@ Tree place(Place p, size_t clv_bytes) {
 int main(int argc, char **argv) {
   const int lg = argc > 1 ? atoi(argv[1]) : 20;
   const int rounds = argc > 2 ? atoi(argv[2]) : 3;
+  const int only = argc > 3 ? atoi(argv[3]) : -1;  // one placement (its index) or all
   const int64_t n = int64_t(1) << lg;
   const size_t clv = (size_t)n * 16;
   std::mt19937_64 rng(6464);
   std::uniform_real_distribution<double> U01(0.0, 1.0);
 
   std::vector<Tree> trees;
-  for (int p = 0; p < kPlaces; p++) trees.push_back(place((Place)p, clv * 8));
+  for (int p = 0; p < kPlaces; p++) trees.push_back(place((Place)p, clv * 8));  // all: same pages as a full run
   std::vector<double> h(clv);
   for (int i = 0; i < 64; i++) {
     for (auto &x : h) x = U01(rng);
@@ -172,6 +173,7 @@ int main(int argc, char **argv) {
   std::vector<double> tot(nv * kPlaces, 0.0);
   for (int r = 0; r < rounds; r++) {
     for (int p = 0; p < kPlaces; p++) {
+      if (only >= 0 && p != only) continue;
       for (int k = 0; k < nv; k++) {
         for (int w = 0; w < 3; w++) launch(vs[k], trees[p]);  // warm (same buffers, same results)
         const int reps = 10;
@@ -199,6 +201,7 @@ int main(int argc, char **argv) {
   }
   for (int p = 0; p < kPlaces; p++)
     for (int k = 0; k < nv; k++) {
+      if (only >= 0 && p != only) continue;
       const double us = tot[p * nv + k] / rounds;
       printf("# %-8s %-14s mean %8.1f us  %.3f of 8 TB/s\n", kPlaceName[p], vs[k].name, us,
              bytes / (us * 1e-6) / 8e12);
