@@ -123,21 +123,6 @@ __device__ inline void block_ticket_sum(long long v, unsigned long long *wsu, in
   ticket_publish(tot, wsu, out);
 }
 
-// the same for a block of kW waves
-template <int kW>
-__device__ inline void block_ticket_sum_w(long long v, unsigned long long *wsu, int64_t *out) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  __shared__ long long partw[kW];
-  if ((threadIdx.x & 63) == 0) partw[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  long long tot = 0;
-#pragma unroll
-  for (int i = 0; i < kW; i++) tot += partw[i];
-  ticket_publish(tot, wsu, out);
-}
-
 // Three independent sums (consecutive kWsWords regions of ws), published by
 // threads 0..2 in parallel.
 __device__ inline void block_ticket_sum3(long long v0, long long v1, long long v2,
@@ -1260,9 +1245,8 @@ struct DeepDesc {
   int64_t *ss[63];
 };
 
-template <int D, bool kSum, bool NTL, int U, int kThreads, int kTips = 0, bool kDyn = false,
-          int kMinW = 1>
-__global__ void __launch_bounds__(kThreads, kMinW)
+template <int D, bool kSum, bool NTL, int U, int kThreads, int kTips = 0, bool kDyn = false>
+__global__ void __launch_bounds__(kThreads, 1)
 plf_dna_f64_deep_kernel(const DeepDesc d, const double *__restrict__ EV,
                         const int32_t *__restrict__ wgt, int64_t n, unsigned long long *ws,
                         const double *__restrict__ tipvec = nullptr) {

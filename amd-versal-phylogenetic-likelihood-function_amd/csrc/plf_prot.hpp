@@ -124,69 +124,6 @@ __device__ __forceinline__ void tile_store(T *__restrict__ g, int64_t base, int6
   }
 }
 
-// tile_fetch / tile_put for a 256-thread tile group of a larger block
-// (thread tid of the group; plf_prot_lds_kernel kTiles > 1)
-template <typename T>
-__device__ __forceinline__ void tile_fetch_g(const T *__restrict__ g, int64_t base, int64_t n,
-                                             typename ProtTile<T>::V (&v)[ProtTile<T>::kChunks / kBlock],
-                                             unsigned tid) {
-  using PT = ProtTile<T>;
-  constexpr int K = PT::kChunks / kBlock;
-  const typename PT::V *src = reinterpret_cast<const typename PT::V *>(g + base * 80);
-  const int64_t lim = (n - base) * PT::kChunksPerSite;  // chunks of valid sites (<= 0: none)
-#pragma unroll
-  for (int i = 0; i < K; i++) {
-    const int j = tid + i * kBlock;
-    v[i] = typename PT::V{};
-    if (j < lim) v[i] = __builtin_nontemporal_load(src + j);
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void tile_put_g(typename ProtTile<T>::V *lds,
-                                           const typename ProtTile<T>::V (&v)[ProtTile<T>::kChunks / kBlock],
-                                           unsigned tid) {
-  using PT = ProtTile<T>;
-#pragma unroll
-  for (int i = 0; i < PT::kChunks / kBlock; i++) {
-    const int j = tid + i * kBlock;
-    const int s = j / PT::kChunksPerSite, q = j - s * PT::kChunksPerSite;
-    lds[s * PT::kStride + q] = v[i];
-  }
-}
-
-// tile_store with plf()'s rescale applied on the way out (f64): chunk j of
-// site s = j / 40 is multiplied by 2^32 (one exact v_ldexp by 32 or 0 per
-// value) when bit s of `scaled` is set
-__device__ __forceinline__ void tile_store_scaled(double *__restrict__ g, int64_t base, int64_t n,
-                                                  const f64x2 *lds, unsigned tid, unsigned long long scaled) {
-  using PT = ProtTile<double>;
-  constexpr int K = PT::kChunks / kBlock;
-  f64x2 *dst = reinterpret_cast<f64x2 *>(g + base * 80);
-  f64x2 v[K];
-#pragma unroll
-  for (int i = 0; i < K; i++) {
-    const int j = tid + i * kBlock;
-    const int s = j / PT::kChunksPerSite, q = j - s * PT::kChunksPerSite;
-    v[i] = lds[s * PT::kStride + q];
-    int e = ((scaled >> s) & 1ull) ? 32 : 0;
-    asm volatile("" : "+v"(e));
-    v[i].x = ldexp(v[i].x, e);
-    v[i].y = ldexp(v[i].y, e);
-  }
-  if (base + 64 <= n) {
-#pragma unroll
-    for (int i = 0; i < K; i++) __builtin_nontemporal_store(v[i], dst + tid + i * kBlock);
-  } else {
-    const int64_t lim = (n - base) * PT::kChunksPerSite;
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-      const int j = tid + i * kBlock;
-      if (j < lim) __builtin_nontemporal_store(v[i], dst + j);
-    }
-  }
-}
-
 // this lane's (site, category) row of 20 values <-> the LDS tile
 template <typename T>
 __device__ __forceinline__ void row_read(const typename ProtTile<T>::V *lds, int site, int c,
@@ -322,11 +259,7 @@ __device__ __forceinline__ void tab_fetch(const T *__restrict__ x, const uint8_t
 // kE3S: phase 3's EV rows by scalar loads (SGPR operands) instead of LDS
 // broadcasts: 145.8 vs 148.8 us at 2^18 f64 (profiles/r02_tune_protein_exact_rows.log).
 // kTab: as prot_mfma_body's (children staged from their combination tables).
-// kTiles > 1 (dense children only): kTiles x 64 sites per block trip, one
-// group of 4 waves per 64-site tile, the matrices shared by the groups in LDS
-// (3 tiles: 12 waves of one 768-thread block, 155 KB of LDS -- 3 waves per
-// SIMD where the 256-thread form's 70.8 KB per block allows 2).
-template <typename T, bool kSum, int kTips, int kRows, bool kE3S, bool kTab = false, int kTiles = 1>
+template <typename T, bool kSum, int kTips, int kRows, bool kE3S, bool kTab = false>
 __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T *__restrict__ x2,
                                               T *__restrict__ x3, const T *__restrict__ EV,
                                               const T *__restrict__ left, const T *__restrict__ right,
@@ -342,17 +275,13 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
   using PT = ProtTile<T>;
   using V = typename PT::V;
   constexpr int E = 16 / (int)sizeof(T);          // elements per 16-B LDS read
-  constexpr int kPh3 = kTiles > 1 ? 4 : (sizeof(T) == 8 ? 10 : 20);  // phase-3 chains per pass
+  constexpr int kPh3 = sizeof(T) == 8 ? 10 : 20;  // phase-3 chains per pass
   static_assert(kRows % E == 0 && S % kRows == 0, "kRows: a divisor of 20, whole 16-B reads");
   constexpr int RV = kRows / E, PV = kPh3 / E, kDist = 2;
-  static_assert(kTiles == 1 || (kTips == 0 && !kTab), "tile groups: dense children");
-  constexpr int kThreads = kBlock * kTiles;
-  const unsigned tid = threadIdx.x & (kBlock - 1);                  // thread in its tile group
-  const int tg = __builtin_amdgcn_readfirstlane(threadIdx.x / kBlock);  // tile group
   __shared__ T tabs[(T1 ? 1 : 0) + (T2 ? 1 : 0) + (T1 ? 0 : 1)][T1 ? 4 * kProtCodes * 20 : 1];
   if constexpr (T1) build_prot_tip_table<T, false>(left, tipvec, tabs[0]);
   if constexpr (T2) build_prot_tip_table<T, false>(right, tipvec, tabs[1]);
-  const int c = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   // P_L[4][400] (unless x1 is a tip) | P_R[4][400] (unless x2 is a tip) | EV[400]
   // in T elements; a tip child's matrix lives in its table instead
@@ -360,19 +289,17 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
   __shared__ V mats[(oE + S * S) / E];
   {
     T *md = reinterpret_cast<T *>(mats);
-    for (int i = threadIdx.x; i < 4 * S * S; i += kThreads) {  // P[c][k][l] -> [c][k/kRows][l][k%kRows]
+    for (int i = threadIdx.x; i < 4 * S * S; i += kBlock) {  // P[c][k][l] -> [c][k/kRows][l][k%kRows]
       const int cc = i / (S * S), r = i - cc * S * S, k = r / S, l = r - k * S;
       const int d = cc * S * S + (k / kRows) * (S * kRows) + l * kRows + (k % kRows);
       if constexpr (!T1) md[d] = left[i];
       if constexpr (!T2) md[oR + d] = right[i];
     }
-    for (int i = threadIdx.x; i < S * S; i += kThreads) md[oE + i] = EV[i];
+    for (int i = threadIdx.x; i < S * S; i += kBlock) md[oE + i] = EV[i];
   }
   const T m = Num<T>::minlik();
-  __shared__ V tiles[kTiles][64 * PT::kStride];
-  __shared__ unsigned long long small_masks[kTiles][kWavesPerBlock];
-  V *const tile = tiles[tg];
-  unsigned long long *const small_mask = small_masks[tg];
+  __shared__ V tile[64 * PT::kStride];
+  __shared__ unsigned long long small_mask[kWavesPerBlock];
   long long acc = 0;
   __syncthreads();
   // phases 1/2: M = the category's group-transposed matrix, x = the child's 20
@@ -413,67 +340,17 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
       for (int j = 0; j < kRows; j++) fn(gk * kRows + j, u[j]);
     }
   };
-  // kTiles > 1: the child's row x[l] straight from the LDS tile (one b128
-  // read per column pair, one pair ahead) instead of 20 registers per row --
-  // the registers that let 3 waves per SIMD fit 168 VGPRs
-  constexpr bool kXL = kTiles > 1;
-  static_assert(!kXL || sizeof(T) == 8, "tile groups: f64");
-  auto gphase_l = [&](const V *M, const V *xr, auto &&fn) {
-    int o = 0;
-    T tok = T(0);
-#pragma unroll
-    for (int gk = 0; gk < S / kRows; gk++) {
-      const V *G = M + gk * S * RV;
-      V ring[kDist + 1][RV];
-      V xq[2];
-      T u[kRows];
-      asm volatile("" : "+v"(o) : "v"(tok));
-#pragma unroll
-      for (int l = 0; l < kDist; l++)
-#pragma unroll
-        for (int j = 0; j < RV; j++) ring[l][j] = G[o + l * RV + j];
-      xq[0] = xr[o];
-#pragma unroll
-      for (int l = 0; l < S; l++) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (l + kDist < S) {
-#pragma unroll
-          for (int j = 0; j < RV; j++) ring[(l + kDist) % (kDist + 1)][j] = G[o + (l + kDist) * RV + j];
-        }
-        if (l % 2 == 0 && l + 2 < S) xq[(l / 2 + 1) % 2] = xr[o + l / 2 + 1];
-        const V *col = ring[l % (kDist + 1)];
-        const T xl = l % 2 == 0 ? xq[(l / 2) % 2].x : xq[(l / 2) % 2].y;
-        T pr[kRows];
-#pragma unroll
-        for (int j = 0; j < kRows; j++) pr[j] = xl * col[j / E][j % E];
-        pin_chains(pr);
-#pragma unroll
-        for (int j = 0; j < kRows; j++) u[j] = l == 0 ? pr[j] : u[j] + pr[j];
-        pin_chains(u);
-        tok = u[kRows - 1];
-      }
-#pragma unroll
-      for (int j = 0; j < kRows; j++) fn(gk * kRows + j, u[j]);
-    }
-  };
   constexpr bool kAnyDense = !(T1 && T2);
   const T *FD = T1 ? x2 : x1;  // the trip's first dense child
-  const int64_t stride = (int64_t)gridDim.x * 64 * kTiles;
-  const int64_t base0 = ((int64_t)blockIdx.x * kTiles + tg) * 64;
+  const int64_t stride = (int64_t)gridDim.x * 64;
   constexpr int K = PT::kChunks / kBlock;
   V pf[K];  // unused (and eliminated) when both children are tips
   if constexpr (kTab) {
-    if (base0 < n) tab_fetch<T>(x1, t1a, t1b, base0, n, pf);
+    if ((int64_t)blockIdx.x * 64 < n) tab_fetch<T>(x1, t1a, t1b, (int64_t)blockIdx.x * 64, n, pf);
   } else if constexpr (kAnyDense) {
-    if (base0 < n) {
-      if constexpr (kXL) tile_fetch_g<T>(FD, base0, n, pf, tid);
-      else tile_fetch<T>(FD, base0, n, pf);
-    }
+    if ((int64_t)blockIdx.x * 64 < n) tile_fetch<T>(FD, (int64_t)blockIdx.x * 64, n, pf);
   }
-  // block-uniform trip count (the trips hold block barriers): a tile group
-  // past n runs its last trip on no sites (no loads, stores or scaler bytes)
-  for (int64_t bb = (int64_t)blockIdx.x * kTiles * 64; bb < n; bb += stride) {
-    const int64_t base = bb + (int64_t)tg * 64;
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
     int off = 0;
     asm volatile("" : "+v"(off));
     const V *mL = mats + off + c * (S * S / E), *mR = mats + off + (oR + c * S * S) / E,
@@ -489,28 +366,19 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
     // stage a dense child's tile from the prefetch registers, then fetch the
     // next tile in the sequence
     auto stage = [&](const T *next, int64_t nbase) {
-      if constexpr (kXL) tile_put_g<T>(tile, pf, tid);
-      else tile_put<T>(tile, pf);
+      tile_put<T>(tile, pf);
       __syncthreads();
       if constexpr (kTab) {
         const bool one = next == x1;
         if (nbase < n) tab_fetch<T>(next, one ? t1a : t2a, one ? t1b : t2b, nbase, n, pf);
       } else {
-        if (nbase < n) {
-          if constexpr (kXL) tile_fetch_g<T>(next, nbase, n, pf, tid);
-          else tile_fetch<T>(next, nbase, n, pf);
-        }
+        if (nbase < n) tile_fetch<T>(next, nbase, n, pf);
       }
     };
     if constexpr (T1) {  // tip: U from the table row of the site's code
       const T *r = tabs[0] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x1)[sq]) * 20;
 #pragma unroll
       for (int k = 0; k < S; k++) U[k] = r[k];
-    } else if constexpr (kXL) {
-      const V *xr = tile + lane * PT::kStride + c * (PT::kChunksPerSite / 4);
-      stage(x2, base);
-      gphase_l(mL, xr, [&](int k, T u) { U[k] = u; });
-      __syncthreads();  // every wave done with the tile before the next stage fills it
     } else {
       T a[S];
       // next in the sequence: this trip's x2, or the next trip's x1 when x2 is a tip
@@ -523,11 +391,6 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
       const T *r = tabs[1] + c * kProtCodes * 20 + prot_code(reinterpret_cast<const uint8_t *>(x2)[sq]) * 20;
 #pragma unroll
       for (int k = 0; k < S; k++) U[k] = U[k] * r[k];
-    } else if constexpr (kXL) {
-      const V *xr = tile + lane * PT::kStride + c * (PT::kChunksPerSite / 4);
-      stage(FD, base + stride);
-      gphase_l(mR, xr, [&](int k, T u) { U[k] = U[k] * u; });
-      __syncthreads();
     } else {
       T b[S];
       stage(FD, base + stride);  // next: the next trip's first dense child
@@ -536,10 +399,7 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
       gphase(mR, b, [&](int k, T u) { U[k] = U[k] * u; });
     }
     // phase 3: O[l] = sum_k U[k] * EV[k][l] from +0.0, kPh3 chains per pass
-    // (kXL: each pass's values go straight to the tile, unscaled, and into
-    // the site's small test; the rescale is applied by tile_store_scaled)
-    T O[kXL ? 1 : S];
-    bool small = base + lane < n;
+    T O[S];
     {
       int o = 0;
       T tok = T(0);
@@ -583,36 +443,18 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
           pin_chains(v);
           tok = v[kPh3 - 1];
         }
-        if constexpr (kXL) {
-          V *xw = tile + lane * PT::kStride + c * (PT::kChunksPerSite / 4) + h * (kPh3 / E);
 #pragma unroll
-          for (int j = 0; j < kPh3; j++) small = small && (Num<T>::abs(v[j]) < m);
-#pragma unroll
-          for (int j = 0; j < kPh3; j += 2) xw[j / 2] = V{v[j], v[j + 1]};
-        } else {
-#pragma unroll
-          for (int j = 0; j < kPh3; j++) O[h * kPh3 + j] = v[j];
-        }
+        for (int j = 0; j < kPh3; j++) O[h * kPh3 + j] = v[j];
       }
     }
-    if constexpr (!kXL) {
+    bool small = base + lane < n;
 #pragma unroll
-      for (int l = 0; l < S; l++) small = small && (Num<T>::abs(O[l]) < m);
-    }
+    for (int l = 0; l < S; l++) small = small && (Num<T>::abs(O[l]) < m);
     const unsigned long long mk = __ballot(small);
     if (lane == 0) small_mask[c] = mk;
     __syncthreads();  // also: every wave is done reading x2 from the tile
     const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
     const bool sc = (all >> lane) & 1ull;
-    if constexpr (kXL) {
-      const int64_t site = base + lane;
-      if (site < n && c == 0) {
-        if (scaler) scaler[site] = (uint8_t)sc;
-        if (kSum && sc) acc += wsite;
-      }
-      tile_store_scaled(x3, base, n, tile, tid, all);
-      __syncthreads();  // tile and small_mask are reused by the next trip
-    } else {
     // x 2^32 on a scaled site as one v_ldexp by 32 or 0 per value (exact
     // either way: the same bits as the multiply-and-select, one VALU
     // instruction per value instead of three)
@@ -632,22 +474,18 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
     __syncthreads();
     tile_store<T>(x3, base, n, tile);
     __syncthreads();  // tile and small_mask are reused by the next trip
-    }
   }
-  if constexpr (kSum) {
-    if constexpr (kTiles > 1) block_ticket_sum_w<kWavesPerBlock * kTiles>(acc, ws, scaler_sum);
-    else block_ticket_sum(acc, ws, scaler_sum);
-  }
+  if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
 
-template <typename T, bool kSum, int kMinWaves, int kTips, int kRows, bool kE3S, int kTiles = 1>
-__global__ void __launch_bounds__(kBlock * kTiles, kMinWaves)
+template <typename T, bool kSum, int kMinWaves, int kTips, int kRows, bool kE3S>
+__global__ void __launch_bounds__(kBlock, kMinWaves)
 plf_prot_lds_kernel(const T *__restrict__ x1, const T *__restrict__ x2, T *__restrict__ x3,
                     const T *__restrict__ EV, const T *__restrict__ left, const T *__restrict__ right,
                     const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
                     unsigned long long *ws, int64_t *scaler_sum, const T *__restrict__ tipvec = nullptr) {
-  prot_lds_body<T, kSum, kTips, kRows, kE3S, false, kTiles>(x1, x2, x3, EV, left, right, wgt, scaler, n,
-                                                            ws, scaler_sum, tipvec);
+  prot_lds_body<T, kSum, kTips, kRows, kE3S>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws,
+                                              scaler_sum, tipvec);
 }
 
 template <typename T, bool kSum, int kMinWaves, int kTips, int kRows, bool kE3S>
@@ -773,7 +611,7 @@ __device__ __forceinline__ void prot_mfma_body(const double *__restrict__ x1, co
   using PT = ProtTile<double>;
   constexpr int kRow = 2 * PT::kStride;  // doubles per site in the LDS tile (82)
   constexpr int K = PT::kChunks / kBlock;
-  const int c = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lo16 = lane & 15, g = lane >> 4;
   f64x2 pf[K];
@@ -1108,7 +946,7 @@ __device__ __forceinline__ void prot_mfma32_body(const float *__restrict__ x1, c
   using PT = ProtTile<float>;
   constexpr int kRow = 4 * PT::kStride;  // floats per site in the LDS tile (84)
   constexpr int K = PT::kChunks / kBlock;
-  const int c = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lo16 = lane & 15, g = lane >> 4;
   const int64_t stride = (int64_t)gridDim.x * 64;

@@ -27,3 +27,5 @@ for k in "10, true, 1>" "10, true, 3>" "4, true, 3>" "2, true, 3>"; do
   tag=$(echo "$k" | tr -dc '0-9')
   python3 $R/tools/pmc_summary.py $OUT/prot_$tag.json "$k" $(find $OUT -path "*prot*" -name "*counter_collection.csv") --note "plf_prot_lds_kernel<double, true, *, 0, $k at 2^18 sites, build/ab_prot_tiles 262144"
 done
+# keep the summaries only (gpurun copies back at most 64 MiB)
+rm -rf $OUT/deep[0-9]* $OUT/prot[0-9]*
