@@ -620,14 +620,17 @@ def test_destroy_waits_for_its_streams_not_the_device(oracle):
     torch.cuda._sleep(50_000_000)
     torch.cuda.synchronize()
     rate = 50_000_000 / max(time.perf_counter() - t0, 1e-4)
-    for release in (True, False):
+    # explicit: the caller releases `mine`; tracked: a torch stream, which
+    # Context.close() releases itself; raw: an integer handle,
+    # never remembered, so the workspace is still held at destroy
+    for mode in ("explicit", "tracked", "raw"):
         s = torch.zeros(4, dtype=torch.int64, device="cuda")
         torch.cuda.synchronize()
         c = plfx.Context(0)
         for i in range(4):
             c.plf_dev(t["x1"], t["x2"], o3, t["EV"], t["left"], t["right"], t["wgt"], None, s[i:i + 1],
-                      stream=mine)
-        if release:
+                      stream=mine.cuda_stream if mode == "raw" else mine)
+        if mode == "explicit":
             c.release_stream(mine)
         with torch.cuda.stream(other):  # keep `other` busy for ~1.5 s
             torch.cuda._sleep(int(1.5 * rate))
@@ -636,8 +639,8 @@ def test_destroy_waits_for_its_streams_not_the_device(oracle):
         t0 = time.perf_counter()
         c.close()
         dt = time.perf_counter() - t0
-        if release:
-            assert not busy.query(), "close() waited for an unrelated stream"
+        if mode != "raw":
+            assert not busy.query(), f"close() waited for an unrelated stream ({mode})"
             assert dt < 0.5
         else:
             assert busy.query(), "close() with a held workspace must wait for the device"
