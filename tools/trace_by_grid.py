@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Per-kernel, per-launch-shape summary of a rocprofv3 kernel-trace CSV.
+
+The driver's default command launches the headline node kernel for the
+timed region AND, through the host-array leg (plfx_plf_f64 in chunks) and the
+CPU-baseline checks, at other grid sizes, so the --stats average of a kernel
+mixes launches of different sizes.  This groups the plfx dispatches by
+(kernel, grid, workgroup) and prints count / average / min / max duration,
+and -- for the longest run of back-to-back dispatches of one shape, the
+timed graph's replay -- the average over that run alone.  One JSON document.
+
+  python3 tools/trace_by_grid.py KERNEL_TRACE_CSV [OUT_JSON]
+"""
+import collections
+import csv
+import json
+import statistics as st
+import sys
+
+
+def main():
+    path = sys.argv[1]
+    def ours(name):  # full (--stats) or truncated (trace) kernel names
+        base = name.replace("void ", "").replace("plfx::dev::", "")
+        return base.startswith(("plf_", "root_lnl", "scaler_sum", "pmat", "tiptip", "prot_"))
+
+    rows = [r for r in csv.DictReader(open(path)) if ours(r["Kernel_Name"])]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    groups = collections.defaultdict(list)
+    pos = {id(r): i for i, r in enumerate(rows)}
+    for r in rows:
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("plfx::dev::", "")
+        grid = (int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"]))
+        wg = int(r["Workgroup_Size_X"]) * int(r["Workgroup_Size_Y"]) * int(r["Workgroup_Size_Z"])
+        groups[(name, grid, wg)].append(r)
+    out = []
+    for (name, grid, wg), rs in sorted(groups.items(), key=lambda kv: -len(kv[1])):
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rs]
+        # the longest run of consecutive dispatches of this shape (dispatch ids adjacent
+        # among all plfx dispatches): the replayed graph of the timed region
+        ids = [pos[id(r)] for r in rs]
+        best, cur = [0], [0]
+        for i in range(1, len(ids)):
+            cur = cur + [i] if ids[i] == ids[i - 1] + 1 else [i]
+            if len(cur) > len(best):
+                best = cur
+        run = [d[i] for i in best]
+        out.append({"kernel": name, "grid": grid, "workgroup": wg, "dispatches": len(d),
+                    "avg_us": round(st.mean(d), 3), "min_us": round(min(d), 3), "max_us": round(max(d), 3),
+                    "longest_consecutive_run": len(run), "run_avg_us": round(st.mean(run), 3)})
+    doc = {"trace": path, "groups": out}
+    s = json.dumps(doc, indent=1)
+    if len(sys.argv) > 2:
+        open(sys.argv[2], "w").write(s)
+    print(s)
+
+
+if __name__ == "__main__":
+    main()
