@@ -1,5 +1,5 @@
 #!/bin/bash
-# Copy one tools/gpu_r03_full.sh session (gpurun_out/<session>/<workload>/...)
+# Copy one measurement session of tools/measure.sh runs (gpurun_out/<session>/<workload>/...)
 # into profiles/ as <tag>_<workload>_*: the bench line, rocprofv3 kernel stats
 # (and trace / counter CSVs when they came back) and the HBM traffic record
 # that bench.py reads as roofline.traffic.
