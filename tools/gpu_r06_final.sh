@@ -30,6 +30,7 @@ step bench_driver_rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o r
 cd $R
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/bench_driver_kernel_stats.csv \;
 python3 tools/trace_by_grid.py $(find $OUT/prof -name "*kernel_trace.csv") $OUT/bench_driver_kernels_by_grid.json > /dev/null
+gzip -c $(find $OUT/prof -name "*kernel_trace.csv") > $OUT/bench_driver_kernel_trace.csv.gz
 rm -rf $OUT/prof
 step rehearse_gloo2_full 900 env PLFX_DIST_BACKEND=gloo python3 -u bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline
 grep '^{' $OUT/rehearse_gloo2_full.log > $OUT/rehearse_gloo2_full.json

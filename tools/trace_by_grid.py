@@ -6,8 +6,9 @@ timed region AND, through the host-array leg (plfx_plf_f64 in chunks) and the
 CPU-baseline checks, at other grid sizes, so the --stats average of a kernel
 mixes launches of different sizes.  This groups the plfx dispatches by
 (kernel, grid, workgroup) and prints count / average / min / max duration,
-and -- for the longest run of back-to-back dispatches of one shape, the
-timed graph's replay -- the average over that run alone.  One JSON document.
+and -- for the longest run of back-to-back dispatches of one shape with no
+other dispatch between them (the timed graph's replay; the host-array leg's
+launches sit between copy blits) -- the average over that run alone.  One JSON document.
 
   python3 tools/trace_by_grid.py KERNEL_TRACE_CSV [OUT_JSON]
 """
@@ -24,10 +25,10 @@ def main():
         base = name.replace("void ", "").replace("plfx::dev::", "")
         return base.startswith(("plf_", "root_lnl", "scaler_sum", "pmat", "tiptip", "prot_"))
 
-    rows = [r for r in csv.DictReader(open(path)) if ours(r["Kernel_Name"])]
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    every = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    pos = {id(r): i for i, r in enumerate(every)}  # position among ALL dispatches (blits included)
+    rows = [r for r in every if ours(r["Kernel_Name"])]
     groups = collections.defaultdict(list)
-    pos = {id(r): i for i, r in enumerate(rows)}
     for r in rows:
         name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("plfx::dev::", "")
         grid = (int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"]))
@@ -36,8 +37,9 @@ def main():
     out = []
     for (name, grid, wg), rs in sorted(groups.items(), key=lambda kv: -len(kv[1])):
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rs]
-        # the longest run of consecutive dispatches of this shape (dispatch ids adjacent
-        # among all plfx dispatches): the replayed graph of the timed region
+        # the longest run of back-to-back dispatches of this shape with nothing else
+        # between them (no blit, no other kernel): the replayed graph of the timed
+        # region, not the host-array leg's launches between its copies
         ids = [pos[id(r)] for r in rs]
         best, cur = [0], [0]
         for i in range(1, len(ids)):
