@@ -243,6 +243,15 @@ def test_traffic_not_reported_under_dispatch_knobs(monkeypatch):
     monkeypatch.setenv("PLFX_NODE_SEGMENTS", "1")
     r = bench.traffic_record(a, W())
     assert r["traffic"] is None and "PLFX_NODE_SEGMENTS" in r["traffic_note"]
+    # values that keep the default dispatch do not withhold it
+    for v in ("auto", "-1", ""):
+        monkeypatch.setenv("PLFX_NODE_SEGMENTS", v)
+        assert "knob" not in bench.traffic_record(a, W())["traffic_note"]
+    monkeypatch.delenv("PLFX_NODE_SEGMENTS")
+    monkeypatch.setenv("PLFX_MAX_BLOCKS", "0")
+    assert "knob" not in bench.traffic_record(a, W())["traffic_note"]
+    monkeypatch.setenv("PLFX_MAX_BLOCKS", "64")
+    assert "PLFX_MAX_BLOCKS" in bench.traffic_record(a, W())["traffic_note"]
 
 
 def test_pmc_tools_record_launch_shapes():
