@@ -632,6 +632,7 @@ plf_dna_batch_kernel(const NodeBatch nodes, const T *__restrict__ EV,
       (const uint8_t *)d.x2, tipvec);
 }
 
+#ifndef PLFX_SECONDARY_TU  // the one non-template kernel: defined in plf_kernels.hip only
 __global__ void __launch_bounds__(kBlock)
 scaler_sum_kernel(const uint8_t *__restrict__ scaler, const int32_t *__restrict__ wgt, int64_t n,
                   unsigned long long *ws, int64_t *out) {
@@ -641,6 +642,7 @@ scaler_sum_kernel(const uint8_t *__restrict__ scaler, const int32_t *__restrict_
     acc += (long long)scaler[j] * (wgt ? (long long)wgt[j] : 1ll);
   block_ticket_sum(acc, ws, out);
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Fused level pair ("triple"): parent P of two inner nodes A, B that are

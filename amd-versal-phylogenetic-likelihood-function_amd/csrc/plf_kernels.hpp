@@ -33,6 +33,10 @@ hipError_t launch_plf_dna_f64(const DnaArgs &a, int max_blocks, hipStream_t s);
 // Protein (S=20, C=4) kernel; fma selects fused multiply-add.
 hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks, hipStream_t s,
                            int tips = 0, const void *tipvec = nullptr);
+// Protein f64 in FMA mode on the VALU with LDS-tiled matrices (plf_prot_valu.hip,
+// PLFX_FMA | PLFX_VALU): bit-identical to the matrix-core FMA kernel, dense
+// children, one node.
+hipError_t launch_plf_prot_valu_f64(const DnaArgs &a, int max_blocks, hipStream_t s);
 
 // Batched nodes (<= kMaxBatch per launch) sharing EV, n, wgt.  dtype: 0 f32, 1 f64.
 // tips: 0 dense children; 1 x1 of every node is a tip (uint8 state codes);

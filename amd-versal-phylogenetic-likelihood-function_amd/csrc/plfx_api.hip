@@ -791,7 +791,10 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
                      int64_t *scaler_sum, void *stream) {
   PLFX_BIND(ctx);
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
-  if (flags & ~PLFX_FMA) return fail(ctx, PLFX_ERR_INVALID, "bad flags %d", flags);
+  if (flags & ~(PLFX_FMA | PLFX_VALU)) return fail(ctx, PLFX_ERR_INVALID, "bad flags %d", flags);
+  const bool valu = (flags & PLFX_VALU) != 0;
+  if (valu && (!(flags & PLFX_FMA) || states != 20 || dtype != PLFX_F64))
+    return fail(ctx, PLFX_ERR_INVALID, "PLFX_VALU: protein (states 20), f64, with PLFX_FMA only");
   if (states == 4) {
     return dtype == PLFX_F32
                ? plf_dev<float>(ctx, (const float *)x1, (const float *)x2, (float *)x3,
@@ -812,8 +815,9 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
   }
   PLFX_WS(ctx, s, w);
   plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, w->ws, n};
-  hipError_t e = plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "plf_prot launch");
+  hipError_t e = valu ? plfx::launch_plf_prot_valu_f64(a, ctx->max_blocks, s)
+                      : plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s);
+  if (e != hipSuccess) return hip_fail(ctx, e, valu ? "plf_prot_valu launch" : "plf_prot launch");
   return PLFX_OK;
 }
 

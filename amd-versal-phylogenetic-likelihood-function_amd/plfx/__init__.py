@@ -59,6 +59,7 @@ STREAM_PER_THREAD = 2  # hipStreamPerThread
 SCHED_KEYS = ("deep6", "deep5", "deep4", "septets", "triples", "unfused", "launches")
 PMAT_STATE, PMAT_EIGEN = 0, 1
 EXACT, FMA = 0, 1
+VALU = 2  # with FMA: protein f64 on the VALU, P matrices tiled in LDS (not the matrix cores)
 PROT_CODES = 24  # protein tip codes: rows of the tip-vector table (plfx.h section 8)
 CTX_LAZY_TABLES = 1  # PLFX_CTX_LAZY_TABLES
 
@@ -361,9 +362,12 @@ class Context:
                                                    F32 if dt == np.float32 else F64))
 
     def plf_dev_gen(self, x1, x2, x3, EV, left, right, states, wgt=None, scaler=None,
-                    scaler_sum=None, n=None, fma=False, stream=None):
+                    scaler_sum=None, n=None, fma=False, stream=None, valu=False):
         """Any built state count (4 DNA, 20 protein), 4 Gamma categories, on
-        torch device tensors: x[site][cat][state], P [cat][k][l], EV [k][l]."""
+        torch device tensors: x[site][cat][state], P [cat][k][l], EV [k][l].
+        fma: PLFX_FMA; valu (with fma, protein f64): the same fused chains on
+        the VALU with LDS-tiled matrices instead of the matrix cores
+        (PLFX_VALU; bit-identical)."""
         import torch
 
         V = 4 * states
@@ -383,7 +387,8 @@ class Context:
         _check_aux(n, wgt, scaler, scaler_sum)
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
         self._check(self._L.plfx_plf_dev_gen(self.h, F32 if dt == torch.float32 else F64, int(states),
-                                             FMA if fma else EXACT, p(x1), p(x2), p(x3), p(EV), n,
+                                             (FMA if fma else EXACT) | (VALU if valu else 0),
+                                             p(x1), p(x2), p(x3), p(EV), n,
                                              p(left), p(right), p(wgt), p(scaler), p(scaler_sum),
                                              self._sh(stream)))
 

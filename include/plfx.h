@@ -197,9 +197,12 @@ int plfx_plf_dev_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *
  * multiply-add (one rounding per term, within 1e-12 relative in f64; protein
  * only, on the matrix cores -- v_mfma_f64_16x16x4 / v_mfma_f32_16x16x4 are
  * k-ordered fma chains, so the result is bit-identical to a fused VALU loop;
- * DNA is always exact). */
+ * DNA is always exact).  PLFX_FMA | PLFX_VALU (protein f64, plfx_plf_dev_gen
+ * only): the same fused chains on the VALU with the P matrices tiled in LDS
+ * -- BASELINE configs[4]'s "matvec, not MFMA" -- bit-identical to PLFX_FMA. */
 #define PLFX_EXACT 0
 #define PLFX_FMA 1
+#define PLFX_VALU 2
 int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void *x1,
                      const void *x2, void *x3, const void *EV, int64_t n, const void *left,
                      const void *right, const int32_t *wgt, uint8_t *scaler,

@@ -192,8 +192,10 @@ def test_codeobj_walks_every_bundle(tmp_path):
     data += new
     p = tmp_path / "libtwo.so"
     p.write_bytes(bytes(data))
-    assert len(codeobj.gfx950_code_objects(p)) == 1
-    for k in ("plf_dna_f64_pair_kernel", "plf_dna_kernel", "root_lnl_kernel"):
+    # one code object per HIP translation unit of libplfx (plf_kernels.hip,
+    # plf_prot_valu.hip), the host-only bundle contributing none
+    assert len(codeobj.gfx950_code_objects(p)) == len(codeobj.gfx950_code_objects(lib)) == 2
+    for k in ("plf_dna_f64_pair_kernel", "plf_dna_kernel", "root_lnl_kernel", "plf_prot_valu_fma_kernel"):
         assert codeobj.kernel_code_sha256(p, k) == codeobj.kernel_code_sha256(lib, k)
 
 

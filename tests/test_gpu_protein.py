@@ -39,14 +39,14 @@ def gen(n, dtype, seed):
     return [a.astype(dtype) for a in (x1, x2, EV, left, right)] + [w]
 
 
-def run(ctx, x1, x2, EV, left, right, w, n, fma):
+def run(ctx, x1, x2, EV, left, right, w, n, fma, valu=False):
     import torch
 
     t = [dev(a) for a in (x1, x2, EV, left, right, w)]
     x3 = torch.empty(V * n, dtype=t[0].dtype, device="cuda")
     sc = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
     s = torch.full((1,), -1, dtype=torch.int64, device="cuda")
-    ctx.plf_dev_gen(t[0], t[1], x3, t[2], t[3], t[4], S, t[5], sc, s, n=n, fma=fma)
+    ctx.plf_dev_gen(t[0], t[1], x3, t[2], t[3], t[4], S, t[5], sc, s, n=n, fma=fma, valu=valu)
     torch.cuda.synchronize()
     return x3.cpu().numpy(), sc.cpu().numpy()[:n], int(s.item())
 
@@ -937,3 +937,57 @@ def test_protein_five_dna_blocks_equal_reference(ctx, oracle, dtype, fma, n):
         assert np.array_equal(bits(outs[b]), bits(refs[b])), b
     assert len(set(incs)) == 1 and s == incs[0]
     assert np.array_equal(sc, rsc)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 257, 4097, 3 * (1 << 16) + 5, 1 << 18])
+def test_protein_valu_fma_bits(ctx, oracle, n):
+    """PLFX_FMA | PLFX_VALU (plf_prot_valu.hip: the LDS-tiled matvecs of the
+    exact kernel with every multiply-add fused, BASELINE configs[4]'s "matvec,
+    not MFMA"): bit-identical to the oracle's fma() restatement and to the
+    matrix-core FMA kernel, scaler bytes and the weighted sum exact; ragged
+    tiles, several trips per block and the full 2^18 size."""
+    x1, x2, EV, left, right, w = gen(n, np.float64, 900 + n % 97)
+    v3, vsc, vs = run(ctx, x1, x2, EV, left, right, w, n, fma=True, valu=True)
+    m3, msc, ms = run(ctx, x1, x2, EV, left, right, w, n, fma=True)
+    assert np.array_equal(bits(v3), bits(m3)) and np.array_equal(vsc, msc) and vs == ms
+    f3, fsc, finc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
+    assert np.array_equal(bits(v3), bits(f3))
+    assert np.array_equal(vsc, fsc) and vs == finc
+    assert fsc.sum() > 0 or n < 4
+
+
+def test_protein_valu_fma_signed_zeros_and_flags(ctx, oracle):
+    """The VALU FMA chains start from +0.0 as the fma() restatement does, on
+    inputs full of +-0.0 and underflowing products; PLFX_VALU is refused
+    without PLFX_FMA, in f32 and for DNA."""
+    import torch
+
+    import plfx
+
+    rng = np.random.default_rng(11)
+    n = 1000
+
+    def field(size):
+        v = rng.random(size) - 0.5
+        r = rng.random(size)
+        v[r < 0.3] = 0.0
+        v[(r >= 0.3) & (r < 0.5)] = -0.0
+        v[(r >= 0.5) & (r < 0.55)] *= np.finfo(np.float64).tiny
+        return v
+
+    x1, x2, EV, left, right = field(V * n), field(V * n), field(S * S), field(CAT * S * S), field(CAT * S * S)
+    w = rng.integers(0, 4, n).astype(np.int32)
+    x3, sc, s = run(ctx, x1, x2, EV, left, right, w, n, fma=True, valu=True)
+    e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
+    assert np.array_equal(bits(x3), bits(e3))
+    assert np.array_equal(sc, esc) and s == einc
+    t = [dev(a) for a in (x1, x2, EV, left, right)]
+    out = torch.empty_like(t[0])
+    with pytest.raises(plfx.PlfxError):
+        ctx.plf_dev_gen(t[0], t[1], out, t[2], t[3], t[4], S, fma=False, valu=True)
+    f = [dev(a.astype(np.float32)) for a in (x1, x2, EV, left, right)]
+    with pytest.raises(plfx.PlfxError):
+        ctx.plf_dev_gen(f[0], f[1], torch.empty_like(f[0]), f[2], f[3], f[4], S, fma=True, valu=True)
+    d = [dev(a) for a in (x1[:16 * n], x2[:16 * n], EV[:16], left[:64], right[:64])]
+    with pytest.raises(plfx.PlfxError):
+        ctx.plf_dev_gen(d[0], d[1], torch.empty_like(d[0]), d[2], d[3], d[4], 4, fma=True, valu=True)
