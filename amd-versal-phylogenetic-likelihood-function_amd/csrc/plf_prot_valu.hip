@@ -37,7 +37,39 @@ namespace dev {
 // time, kRows independent chains per wave, the columns in chunks of 4 so each
 // row's four values are one scalar load), U[k] *= the same over x2 and P_R,
 // x3[l] = fma-chain_k U[k] EV[k][l] from +0.0 (10 states at a time).
-template <bool kSum, int kRows, int kMinW, int kCols>
+// the child tile's store with plf()'s rescale applied on the way out: chunk j
+// of site s = j / 40 times 2^32 (one exact v_ldexp by 32 or 0 per value) when
+// bit s of `scaled` is set (kOT: phase 3 writes its values unscaled)
+__device__ __forceinline__ void tile_store_scaled(double *__restrict__ g, int64_t base, int64_t n,
+                                                  const f64x2 *lds, unsigned long long scaled) {
+  using PT = ProtTile<double>;
+  constexpr int K = PT::kChunks / kBlock;
+  f64x2 *dst = reinterpret_cast<f64x2 *>(g + base * 80);
+  f64x2 v[K];
+#pragma unroll
+  for (int i = 0; i < K; i++) {
+    const int j = threadIdx.x + i * kBlock;
+    const int st = j / PT::kChunksPerSite, q = j - st * PT::kChunksPerSite;
+    v[i] = lds[st * PT::kStride + q];
+    int e = ((scaled >> st) & 1ull) ? 32 : 0;
+    asm volatile("" : "+v"(e));
+    v[i].x = ldexp(v[i].x, e);
+    v[i].y = ldexp(v[i].y, e);
+  }
+  if (base + 64 <= n) {
+#pragma unroll
+    for (int i = 0; i < K; i++) __builtin_nontemporal_store(v[i], dst + threadIdx.x + i * kBlock);
+  } else {
+    const int64_t lim = (n - base) * PT::kChunksPerSite;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      const int j = threadIdx.x + i * kBlock;
+      if (j < lim) __builtin_nontemporal_store(v[i], dst + j);
+    }
+  }
+}
+
+template <bool kSum, int kRows, int kMinW, int kCols, bool kOT = false, bool kDyn = false>
 __global__ void __launch_bounds__(kBlock, kMinW)
 plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                          double *__restrict__ x3, const double *__restrict__ EV,
@@ -114,7 +146,14 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
   constexpr int K = PT::kChunks / kBlock;
   V pf[K];
   if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(x1, (int64_t)blockIdx.x * 64, n, pf);
-  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
+  // kDyn: tiles after each block's first two come from the device-wide queue
+  // of the matrix-core kernel (plf_prot.hpp ProtQueue: thread 0 publishes the
+  // next trip's tile in qslot before the trip's first barrier and dequeues the
+  // one after it during the trip), so the blocks' trip counts even out
+  ProtQueue pq(ws, n, kDyn);
+  __shared__ long long qslot;
+  auto trip = [&](const int64_t base) -> int64_t {
+    int64_t next = base + stride;
     double U[S];
     const int64_t sq = base + lane < n ? base + lane : n - 1;
     const int wsite = kSum ? wgt_at(wgt, sq, ws) : 0;
@@ -122,6 +161,7 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
       double a[S];
       tile_put<double>(tile, pf);
       __syncthreads();
+      if constexpr (kDyn) next = qslot;
       tile_fetch<double>(x2, base, n, pf);  // this trip's x2 while phase 1 runs
       row_read<double>(tile, lane, c, a);
       __syncthreads();
@@ -131,13 +171,16 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
       double b[S];
       tile_put<double>(tile, pf);
       __syncthreads();
-      if (base + stride < n) tile_fetch<double>(x1, base + stride, n, pf);  // the next trip's x1
+      if (next < n) tile_fetch<double>(x1, next, n, pf);  // the next trip's x1
+      if constexpr (kDyn) pq.dequeue();
       row_read<double>(tile, lane, c, b);
       __syncthreads();
       dot(PR, b, [&](int k, double u) { U[k] = U[k] * u; });
     }
-    // phase 3: O[l] = sum_k U[k] * EV[k][l], fused, from +0.0
-    double O[S];
+    // phase 3: O[l] = sum_k U[k] * EV[k][l], fused, from +0.0 (kOT: each pass's
+    // values straight to the tile, unscaled, and into the site's small test)
+    double O[kOT ? 1 : S];
+    bool small = base + lane < n;
     {
       double tok = 0.0;
 #pragma unroll
@@ -155,31 +198,55 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
           pin_chains(v);
           tok = v[kPh3 - 1];
         }
+        if constexpr (kOT) {
+          V *xw = tile + lane * PT::kStride + c * (PT::kChunksPerSite / 4) + h * (kPh3 / 2);
 #pragma unroll
-        for (int j = 0; j < kPh3; j++) O[h * kPh3 + j] = v[j];
+          for (int j = 0; j < kPh3; j++) small = small && (__builtin_fabs(v[j]) < m);
+#pragma unroll
+          for (int j = 0; j < kPh3; j += 2) xw[j / 2] = V{v[j], v[j + 1]};
+        } else {
+#pragma unroll
+          for (int j = 0; j < kPh3; j++) O[h * kPh3 + j] = v[j];
+        }
       }
     }
-    bool small = base + lane < n;
+    if constexpr (!kOT) {
 #pragma unroll
-    for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
+      for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
+    }
     const unsigned long long mk = __ballot(small);
     if (lane == 0) small_mask[c] = mk;
     __syncthreads();  // also: every wave is done reading x2 from the tile
     const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
     const bool sc = (all >> lane) & 1ull;
-    int e = sc ? 32 : 0;  // x 2^32 as one exact v_ldexp per value (plf_prot.hpp)
-    asm volatile("" : "+v"(e));
-#pragma unroll
-    for (int l = 0; l < S; l++) O[l] = ldexp(O[l], e);
-    row_write<double>(tile, lane, c, O);
     const int64_t site = base + lane;
     if (site < n && c == 0) {
       if (scaler) scaler[site] = (uint8_t)sc;
       if (kSum && sc) acc += wsite;
     }
-    __syncthreads();
-    tile_store<double>(x3, base, n, tile);
+    if constexpr (kOT) {
+      tile_store_scaled(x3, base, n, tile, all);
+    } else {
+      int e = sc ? 32 : 0;  // x 2^32 as one exact v_ldexp per value (plf_prot.hpp)
+      asm volatile("" : "+v"(e));
+#pragma unroll
+      for (int l = 0; l < S; l++) O[l] = ldexp(O[l], e);
+      row_write<double>(tile, lane, c, O);
+      __syncthreads();
+      tile_store<double>(x3, base, n, tile);
+    }
     __syncthreads();  // tile and small_mask are reused by the next trip
+    return next;
+  };
+  if constexpr (kDyn) {
+    int64_t base = (int64_t)blockIdx.x * 64;
+    for (int i = 0; base < n; i++) {
+      if (threadIdx.x == 0) qslot = pq.next_base(i);
+      base = trip(base);
+    }
+    pq.finish();
+  } else {
+    for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) trip(base);
   }
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
@@ -192,9 +259,10 @@ namespace {
 // wave; blocks per CU (launch bounds: kMinW waves per SIMD); kCols: 0 = chunks
 // of 4 columns loaded after the previous chunk, else double-buffered chunks
 // of kCols columns.  PLFX_VALU_FORM (A/B only) picks a form at first use.
-template <bool kSum, int kRows, int kMinW, int kCols>
+template <bool kSum, int kRows, int kMinW, int kCols, bool kOT = false, bool kDyn = false>
 hipError_t launch_valu_k(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  auto kernel = &dev::plf_prot_valu_fma_kernel<kSum, kRows, kMinW, kCols>;
+  if (kDyn && !a.ws) return hipErrorInvalidValue;
+  auto kernel = &dev::plf_prot_valu_fma_kernel<kSum, kRows, kMinW, kCols, kOT, kDyn>;
   static int resident = 0;
   if (!resident) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -228,6 +296,11 @@ hipError_t launch_valu_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
     case 4: return launch_valu_k<kSum, 10, 3, 1>(a, max_blocks, s);
     case 5: return launch_valu_k<kSum, 5, 2, 0>(a, max_blocks, s);
     case 6: return launch_valu_k<kSum, 10, 2, 0>(a, max_blocks, s);
+    case 7: return launch_valu_k<kSum, 5, 3, 0, true>(a, max_blocks, s);
+    case 8: return launch_valu_k<kSum, 5, 3, 1, true>(a, max_blocks, s);
+    case 9: return launch_valu_k<kSum, 5, 3, 2, false, true>(a, max_blocks, s);
+    case 10: return launch_valu_k<kSum, 5, 3, 0, false, true>(a, max_blocks, s);
+    case 11: return launch_valu_k<kSum, 4, 3, 2, false, true>(a, max_blocks, s);
     default: return launch_valu_k<kSum, 5, 3, 0>(a, max_blocks, s);
   }
 }

@@ -278,13 +278,17 @@ def test_sub_records_arguments():
     configs[4] at --sites / 4 (2^18 by default) with at least 200 timed steps
     after 300 warm-up ones, exact only for protein_exact; opt-outs parse."""
     a = bench.parse(["--steps", "20", "--warmup", "5"])
-    assert bench.SUB_RECORDS == ("nodes512", "tree64", "protein", "protein_exact")
+    assert bench.SUB_RECORDS == ("nodes512", "tree64", "protein", "protein_valu", "protein_exact")
     t = bench.sub_args(a, "tree64")
     assert (t.workload, t.sites, t.steps, t.warmup, t.exact, t.tips) == ("tree64", 1 << 20, 20, 5, False, False)
     p = bench.sub_args(a, "protein")
     assert (p.workload, p.sites, p.steps, p.warmup, p.exact) == ("protein", 1 << 18, 200, 300, False)
     e = bench.sub_args(a, "protein_exact")
     assert e.exact and e.sites == 1 << 18 and bench.traffic_name(e) == "protein_exact"
+    v = bench.sub_args(a, "protein_valu")
+    assert v.valu and not v.exact and v.steps == 200 and bench.traffic_name(v) == "protein_valu"
+    assert bench.traffic_key(v) == "protein:f64:valu:dense:fuse3:sites262144"
+    assert not p.valu
     assert bench.traffic_key(t) == "tree64:f64:fma:dense:fuse3:sites1048576"
     assert bench.traffic_key(p) == "protein:f64:fma:dense:fuse3:sites262144"
     assert a.workload == "node" and a.steps == 20  # the line's own arguments are untouched

@@ -31,6 +31,7 @@ def _bench(*args, expect_rc=0):
     (("--workload", "tree64", "--fuse", "2", "--sites", "4099"), 63),
     (("--workload", "protein", "--sites", "4099"), 1),
     (("--workload", "protein", "--exact", "--sites", "4099"), 1),
+    (("--workload", "protein", "--valu", "--sites", "4099"), 1),
     (("--workload", "protein", "--tips", "--sites", "4099"), 1),
     (("--workload", "protein", "--dtype", "f32", "--sites", "4099"), 1),
     (("--workload", "nodes512", "--nodes", "6", "--sites", "4099"), 6),
@@ -57,6 +58,7 @@ def test_default_invocation_f32_with_every_sub_record():
         assert c[k]["dtype"] == "f32"
     for p in (c["protein"], c["protein"]["exact"]):
         assert p["check"] == "ok" and p["check_windows"] == 1 and p["dtype"] == "f32"
+    assert "valu_fma" not in c["protein"]  # the VALU FMA form is f64 only
 
 
 def test_corrupted_single_rank_line_fails():
@@ -68,5 +70,5 @@ def test_corrupted_single_rank_line_fails():
     assert c["windows_mismatched"] == 1
     for k in ("nodes512", "tree64"):
         assert c[k]["check"] == "CHECK_FAILED" and c[k]["windows_mismatched"] == 1
-    for p in (c["protein"], c["protein"]["exact"]):
+    for p in (c["protein"], c["protein"]["valu_fma"], c["protein"]["exact"]):
         assert p["windows_mismatched"] == 1 and p["check"] == "CHECK_FAILED"

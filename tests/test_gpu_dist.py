@@ -158,10 +158,12 @@ def _assert_checked(d, world, nodes):
     for k, n in expect.items():
         assert c[k]["check"] == "ok" and c[k]["check_windows"] == n and c[k]["windows_mismatched"] == 0, k
     assert c["tree64"]["scaler_events_all_ranks"] > 0 and c["tree64"]["value"] > 0
-    for p in (c["protein"], c["protein"]["exact"]):
+    for p in (c["protein"], c["protein"]["valu_fma"], c["protein"]["exact"]):
         assert p["check"] == "ok" and p["check_windows"] == world and p["windows_mismatched"] == 0
         assert p["steps"] >= 200 and p["value_device"] >= p["value"] > 0
-    assert "valu" in c["protein"]["exact"] and "valu" not in c["protein"]
+    # the exact record carries its VALU floor (roofline-style `valu` dict)
+    assert isinstance(c["protein"]["exact"].get("valu"), dict) and "bound" in c["protein"]["exact"]["valu"]
+    assert "not MFMA" in c["protein"]["valu_fma"]["workload"]
 
 
 def test_nodes512_full_size_windows(oracle):
@@ -261,5 +263,5 @@ def test_corrupted_rank_fails_every_check():
     assert c["check_windows"] == 2 and c["windows_mismatched"] == 1
     for k in ("nodes512", "tree64"):
         assert c[k]["check"] == "CHECK_FAILED" and c[k]["windows_mismatched"] == 1, k
-    for p in (c["protein"], c["protein"]["exact"]):
+    for p in (c["protein"], c["protein"]["valu_fma"], c["protein"]["exact"]):
         assert p["check"] == "CHECK_FAILED" and p["windows_mismatched"] == 1
