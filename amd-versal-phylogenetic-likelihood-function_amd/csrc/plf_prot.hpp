@@ -259,12 +259,7 @@ __device__ __forceinline__ void tab_fetch(const T *__restrict__ x, const uint8_t
 // kE3S: phase 3's EV rows by scalar loads (SGPR operands) instead of LDS
 // broadcasts: 145.8 vs 148.8 us at 2^18 f64 (profiles/r02_tune_protein_exact_rows.log).
 // kTab: as prot_mfma_body's (children staged from their combination tables).
-// kFma: every multiply-add fused in the same order (u = fma(x[l], P[k][l], u)
-// from +0.0, x3 = fma(U[k], EV[k][l], x3) from +0.0): the oracle's fma
-// restatement and bit for bit the matrix-core kernels' k-ordered chains, at
-// half the VALU instructions -- configs[4]'s "matvec, not MFMA" in FMA mode
-// (plf_prot_valu.hip).
-template <typename T, bool kSum, int kTips, int kRows, bool kE3S, bool kTab = false, bool kFma = false>
+template <typename T, bool kSum, int kTips, int kRows, bool kE3S, bool kTab = false>
 __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T *__restrict__ x2,
                                               T *__restrict__ x3, const T *__restrict__ EV,
                                               const T *__restrict__ left, const T *__restrict__ right,
@@ -332,17 +327,12 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
         const V *col = ring[l % (kDist + 1)];
         // all kRows products, then all kRows adds: no add waits on the
         // multiply just before it (chains start at q0: site_cat, plf_dna.hpp)
-        if constexpr (kFma) {
+        T pr[kRows];
 #pragma unroll
-          for (int j = 0; j < kRows; j++) u[j] = madd<T, true>(x[l], col[j / E][j % E], l == 0 ? T(0) : u[j]);
-        } else {
-          T pr[kRows];
+        for (int j = 0; j < kRows; j++) pr[j] = x[l] * col[j / E][j % E];
+        pin_chains(pr);
 #pragma unroll
-          for (int j = 0; j < kRows; j++) pr[j] = x[l] * col[j / E][j % E];
-          pin_chains(pr);
-#pragma unroll
-          for (int j = 0; j < kRows; j++) u[j] = l == 0 ? pr[j] : u[j] + pr[j];
-        }
+        for (int j = 0; j < kRows; j++) u[j] = l == 0 ? pr[j] : u[j] + pr[j];
         pin_chains(u);
         tok = u[kRows - 1];
       }
@@ -433,14 +423,6 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
             for (int j = 0; j < PV; j++) ring[(k + 2) % 3][j] = G[o + (S / E) * (k + 2) + j];
           }
           const V *e = ring[k % 3];
-          if constexpr (kFma) {
-            static_assert(kE3S, "FMA: EV rows as SGPR operands");
-            int so = 0;
-            asm volatile("" : "+s"(so) : "v"(tok));
-            const T *er = EV + so + k * S + h * kPh3;
-#pragma unroll
-            for (int j = 0; j < kPh3; j++) v[j] = madd<T, true>(U[k], er[j], v[j]);
-          } else {
           T pr[kPh3];
           if constexpr (kE3S) {
             // EV row k straight from global memory at a wave-uniform address:
@@ -458,7 +440,6 @@ __device__ __forceinline__ void prot_lds_body(const T *__restrict__ x1, const T 
           pin_chains(pr);
 #pragma unroll
           for (int j = 0; j < kPh3; j++) v[j] += pr[j];
-          }
           pin_chains(v);
           tok = v[kPh3 - 1];
         }

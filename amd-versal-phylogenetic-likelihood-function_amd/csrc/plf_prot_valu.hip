@@ -1,22 +1,38 @@
 // plf_prot_valu.hip -- BASELINE configs[4] as its config line words it: a
-// protein (S = 20) inner node with the 20x20 P matrices tiled in LDS and the
-// matvecs on the VALU, not the matrix cores, in FMA mode (PLFX_FMA |
-// PLFX_VALU): plf()'s loop (app/src/plf.cpp:19-65 with 4 -> 20) with every
-// multiply-add fused in the same order, u = fma(x[l], P[k][l], u) and
-// x3 = fma(U[k], EV[k][l], x3) from +0.0.  That is the oracle's fma
-// restatement and, bit for bit, what the matrix-core kernels compute (their
-// v_mfma_f64 tiles are k-ordered fma chains), at half the VALU instructions
-// of the exact mode's separate roundings.  The body is the exact kernel's
-// (plf_prot.hpp prot_lds_body: wave = category, lane = site, child tiles
-// staged through LDS, matrices broadcast from LDS, EV rows as SGPR operands,
-// ballot rescale) with kFma set.  Its own translation unit, so the other
-// kernels' code objects (and the PMC records stamped with them) stay as they
-// are.
+// protein (S = 20) inner node, f64, the matvecs on the VALU, not the matrix
+// cores, in FMA mode (PLFX_FMA | PLFX_VALU): plf()'s loop
+// (app/src/plf.cpp:19-65 with 4 -> 20) with every multiply-add fused in the
+// same order, u = fma(x[l], P[k][l], u) and x3 = fma(U[k], EV[k][l], x3) from
+// +0.0.  That is the oracle's fma restatement and, bit for bit, what the
+// matrix-core kernels compute (their v_mfma_f64 tiles are k-ordered fma
+// chains), at half the VALU instructions of the exact mode's separate
+// roundings.  Its own translation unit, so the other kernels' code objects
+// (and the PMC records stamped with them) stay as they are.
+//
+// Wave = category c, lane = site of a 64-site tile; each child tile is staged
+// through LDS with coalesced non-temporal loads (plf_prot.hpp tile_fetch /
+// tile_put / row_read, the exact kernel's padded layout) and the next one is
+// in flight in registers during the current phase.  The matrices are NOT in
+// LDS: P_c and EV rows are wave-uniform, so they are scalar loads straight
+// from global memory used as SGPR operands.  With the matrices broadcast from
+// LDS (the exact kernel's form with fused chains) each ds_read_b128 fed only
+// two fma and the LDS, shared by the CU's four SIMDs, bound it at 0.55 of
+// 8 TB/s; with scalar operands LDS holds only the 41-KB tile and three blocks
+// (3 waves per SIMD) share a CU: 0.60-0.62 (profiles/r06_protein_valu_forms.log:
+// twelve forms A/B'd on two boxes -- row groups of 4/5/10, column chunks
+// loaded after the previous one or double-buffered, 2 vs 3 waves per SIMD,
+// phase 3 straight to the tile, the device-wide tile queue; the forms are in
+// plf_prot_valu.hip@68b50fc).
+// Phases: U[k] = fma-chain_l x1[l] P_L[k][l] (kRows rows k at a time: kRows
+// independent chains per wave; the columns in chunks of kCols, the next
+// chunk's scalar loads issued before this chunk's fma), U[k] *= the same over
+// x2 and P_R, x3[l] = fma-chain_k U[k] EV[k][l] (10 states at a time); then
+// plf()'s scale test as a wave ballot per category, combined over the block's
+// four waves in LDS, and the rescale as one exact v_ldexp per value.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdint>
-#include <cstdlib>
 
 #define PLFX_SECONDARY_TU  // plf_dna.hpp's non-template kernel lives in plf_kernels.hip
 #include "plf_kernels.hpp"
@@ -25,51 +41,7 @@
 namespace plfx {
 namespace dev {
 
-// Wave = category c, lane = site of a 64-site tile (as the exact kernel), but
-// the P matrices are read as SGPR operands -- wave-uniform scalar loads of
-// P_c rows straight from global memory (the scalar cache holds the 25.6 KB of
-// P_L / P_R) -- instead of LDS broadcasts: in FMA mode each LDS read fed only
-// two fma, and the LDS, shared by the CU's four SIMDs, became the binding unit
-// (the LDS-matrix form ran 0.55 of 8 TB/s, profiles/r06_protein_valu_*.log).
-// EV rows come the same way (phase 3).  LDS then holds only the staged child
-// tile (41 KB), so kMinW = 3 blocks of 4 waves can share a CU.
-// Phases: U[k] = fma-chain_l x1[l] P_L[k][l] from +0.0 (kRows rows k at a
-// time, kRows independent chains per wave, the columns in chunks of 4 so each
-// row's four values are one scalar load), U[k] *= the same over x2 and P_R,
-// x3[l] = fma-chain_k U[k] EV[k][l] from +0.0 (10 states at a time).
-// the child tile's store with plf()'s rescale applied on the way out: chunk j
-// of site s = j / 40 times 2^32 (one exact v_ldexp by 32 or 0 per value) when
-// bit s of `scaled` is set (kOT: phase 3 writes its values unscaled)
-__device__ __forceinline__ void tile_store_scaled(double *__restrict__ g, int64_t base, int64_t n,
-                                                  const f64x2 *lds, unsigned long long scaled) {
-  using PT = ProtTile<double>;
-  constexpr int K = PT::kChunks / kBlock;
-  f64x2 *dst = reinterpret_cast<f64x2 *>(g + base * 80);
-  f64x2 v[K];
-#pragma unroll
-  for (int i = 0; i < K; i++) {
-    const int j = threadIdx.x + i * kBlock;
-    const int st = j / PT::kChunksPerSite, q = j - st * PT::kChunksPerSite;
-    v[i] = lds[st * PT::kStride + q];
-    int e = ((scaled >> st) & 1ull) ? 32 : 0;
-    asm volatile("" : "+v"(e));
-    v[i].x = ldexp(v[i].x, e);
-    v[i].y = ldexp(v[i].y, e);
-  }
-  if (base + 64 <= n) {
-#pragma unroll
-    for (int i = 0; i < K; i++) __builtin_nontemporal_store(v[i], dst + threadIdx.x + i * kBlock);
-  } else {
-    const int64_t lim = (n - base) * PT::kChunksPerSite;
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-      const int j = threadIdx.x + i * kBlock;
-      if (j < lim) __builtin_nontemporal_store(v[i], dst + j);
-    }
-  }
-}
-
-template <bool kSum, int kRows, int kMinW, int kCols, bool kOT = false, bool kDyn = false>
+template <bool kSum, int kRows, int kCols, int kMinW>
 __global__ void __launch_bounds__(kBlock, kMinW)
 plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
                          double *__restrict__ x3, const double *__restrict__ EV,
@@ -77,7 +49,7 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
                          const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
                          unsigned long long *ws, int64_t *scaler_sum) {
   constexpr int S = 20, kPh3 = 10;
-  static_assert(S % kRows == 0, "kRows divides 20");
+  static_assert(S % kRows == 0 && S % kCols == 0, "row groups and column chunks divide 20");
   using PT = ProtTile<double>;
   using V = typename PT::V;
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -86,56 +58,35 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
   __shared__ V tile[64 * PT::kStride];
   __shared__ unsigned long long small_mask[kWavesPerBlock];
   long long acc = 0;
-  // sum_l x[l] * P[k][l] for the kRows rows of each group, fused, from +0.0;
-  // P = this wave's category's matrix (wave-uniform: scalar loads)
+  // fn(k, sum_l x[l] * P[k][l]) for every row k, fused, from +0.0; P = this
+  // wave's category's matrix (wave-uniform: scalar loads, SGPR operands)
   auto dot = [&](const double *P, const double (&x)[S], auto &&fn) {
-    double tok = 0.0;
 #pragma unroll
     for (int gk = 0; gk < S / kRows; gk++) {
       const double *G = P + gk * kRows * S;
-      double u[kRows];
-      if constexpr (kCols == 0) {
-        // chunks of 4 columns, each chunk's loads after the previous chunk's chains
+      double u[kRows], cur[kRows][kCols], nxt[kRows][kCols];
 #pragma unroll
-        for (int lc = 0; lc < S; lc += 4) {
-          int so = 0;
-          asm volatile("" : "+s"(so) : "v"(tok));
-          const double *pr = G + so + lc;
+      for (int j = 0; j < kRows; j++)
 #pragma unroll
-          for (int l = 0; l < 4; l++)
+        for (int q = 0; q < kCols; q++) cur[j][q] = G[j * S + q];
 #pragma unroll
-            for (int j = 0; j < kRows; j++)
-              u[j] = __builtin_fma(x[lc + l], pr[j * S + l], lc + l == 0 ? 0.0 : u[j]);
-          pin_chains(u);
-          tok = u[kRows - 1];
-        }
-      } else {
-        // chunks of kCols columns, the next chunk's scalar loads issued before
-        // this chunk's fused multiply-adds
-        double cur[kRows][kCols], nxt[kRows][kCols];
-#pragma unroll
-        for (int j = 0; j < kRows; j++)
-#pragma unroll
-          for (int q = 0; q < kCols; q++) cur[j][q] = G[j * S + q];
-#pragma unroll
-        for (int lc = 0; lc < S; lc += kCols) {
-          if (lc + kCols < S) {
-#pragma unroll
-            for (int j = 0; j < kRows; j++)
-#pragma unroll
-              for (int q = 0; q < kCols; q++) nxt[j][q] = G[j * S + lc + kCols + q];
-          }
-#pragma unroll
-          for (int q = 0; q < kCols; q++)
-#pragma unroll
-            for (int j = 0; j < kRows; j++)
-              u[j] = __builtin_fma(x[lc + q], cur[j][q], lc + q == 0 ? 0.0 : u[j]);
-          pin_chains(u);
+      for (int lc = 0; lc < S; lc += kCols) {
+        if (lc + kCols < S) {
 #pragma unroll
           for (int j = 0; j < kRows; j++)
 #pragma unroll
-            for (int q = 0; q < kCols; q++) cur[j][q] = nxt[j][q];
+            for (int q = 0; q < kCols; q++) nxt[j][q] = G[j * S + lc + kCols + q];
         }
+#pragma unroll
+        for (int q = 0; q < kCols; q++)
+#pragma unroll
+          for (int j = 0; j < kRows; j++)
+            u[j] = __builtin_fma(x[lc + q], cur[j][q], lc + q == 0 ? 0.0 : u[j]);
+        pin_chains(u);
+#pragma unroll
+        for (int j = 0; j < kRows; j++)
+#pragma unroll
+          for (int q = 0; q < kCols; q++) cur[j][q] = nxt[j][q];
       }
 #pragma unroll
       for (int j = 0; j < kRows; j++) fn(gk * kRows + j, u[j]);
@@ -144,16 +95,9 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
   const double *PL = left + c * S * S, *PR = right + c * S * S;
   const int64_t stride = (int64_t)gridDim.x * 64;
   constexpr int K = PT::kChunks / kBlock;
-  V pf[K];
+  V pf[K];  // the next child tile in flight
   if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(x1, (int64_t)blockIdx.x * 64, n, pf);
-  // kDyn: tiles after each block's first two come from the device-wide queue
-  // of the matrix-core kernel (plf_prot.hpp ProtQueue: thread 0 publishes the
-  // next trip's tile in qslot before the trip's first barrier and dequeues the
-  // one after it during the trip), so the blocks' trip counts even out
-  ProtQueue pq(ws, n, kDyn);
-  __shared__ long long qslot;
-  auto trip = [&](const int64_t base) -> int64_t {
-    int64_t next = base + stride;
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
     double U[S];
     const int64_t sq = base + lane < n ? base + lane : n - 1;
     const int wsite = kSum ? wgt_at(wgt, sq, ws) : 0;
@@ -161,7 +105,6 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
       double a[S];
       tile_put<double>(tile, pf);
       __syncthreads();
-      if constexpr (kDyn) next = qslot;
       tile_fetch<double>(x2, base, n, pf);  // this trip's x2 while phase 1 runs
       row_read<double>(tile, lane, c, a);
       __syncthreads();
@@ -171,16 +114,13 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
       double b[S];
       tile_put<double>(tile, pf);
       __syncthreads();
-      if (next < n) tile_fetch<double>(x1, next, n, pf);  // the next trip's x1
-      if constexpr (kDyn) pq.dequeue();
+      if (base + stride < n) tile_fetch<double>(x1, base + stride, n, pf);  // the next trip's x1
       row_read<double>(tile, lane, c, b);
       __syncthreads();
-      dot(PR, b, [&](int k, double u) { U[k] = U[k] * u; });
+      dot(PR, b, [&](int k, double u) { U[k] = U[k] * u; });  // prod[k] = umpL[k] * umpR[k]
     }
-    // phase 3: O[l] = sum_k U[k] * EV[k][l], fused, from +0.0 (kOT: each pass's
-    // values straight to the tile, unscaled, and into the site's small test)
-    double O[kOT ? 1 : S];
-    bool small = base + lane < n;
+    // phase 3: O[l] = sum_k U[k] * EV[k][l], fused, from +0.0
+    double O[S];
     {
       double tok = 0.0;
 #pragma unroll
@@ -191,62 +131,38 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
 #pragma unroll
         for (int k = 0; k < S; k++) {
           int so = 0;
-          asm volatile("" : "+s"(so) : "v"(tok));
+          asm volatile("" : "+s"(so) : "v"(tok));  // EV row k after the previous row's chains
           const double *er = EV + so + k * S + h * kPh3;
 #pragma unroll
           for (int j = 0; j < kPh3; j++) v[j] = __builtin_fma(U[k], er[j], v[j]);
           pin_chains(v);
           tok = v[kPh3 - 1];
         }
-        if constexpr (kOT) {
-          V *xw = tile + lane * PT::kStride + c * (PT::kChunksPerSite / 4) + h * (kPh3 / 2);
 #pragma unroll
-          for (int j = 0; j < kPh3; j++) small = small && (__builtin_fabs(v[j]) < m);
-#pragma unroll
-          for (int j = 0; j < kPh3; j += 2) xw[j / 2] = V{v[j], v[j + 1]};
-        } else {
-#pragma unroll
-          for (int j = 0; j < kPh3; j++) O[h * kPh3 + j] = v[j];
-        }
+        for (int j = 0; j < kPh3; j++) O[h * kPh3 + j] = v[j];
       }
     }
-    if constexpr (!kOT) {
+    bool small = base + lane < n;
 #pragma unroll
-      for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
-    }
+    for (int l = 0; l < S; l++) small = small && (__builtin_fabs(O[l]) < m);
     const unsigned long long mk = __ballot(small);
     if (lane == 0) small_mask[c] = mk;
     __syncthreads();  // also: every wave is done reading x2 from the tile
     const unsigned long long all = small_mask[0] & small_mask[1] & small_mask[2] & small_mask[3];
     const bool sc = (all >> lane) & 1ull;
+    int e = sc ? 32 : 0;  // x 2^32 as one exact v_ldexp per value (plf_prot.hpp)
+    asm volatile("" : "+v"(e));
+#pragma unroll
+    for (int l = 0; l < S; l++) O[l] = ldexp(O[l], e);
+    row_write<double>(tile, lane, c, O);
     const int64_t site = base + lane;
     if (site < n && c == 0) {
       if (scaler) scaler[site] = (uint8_t)sc;
       if (kSum && sc) acc += wsite;
     }
-    if constexpr (kOT) {
-      tile_store_scaled(x3, base, n, tile, all);
-    } else {
-      int e = sc ? 32 : 0;  // x 2^32 as one exact v_ldexp per value (plf_prot.hpp)
-      asm volatile("" : "+v"(e));
-#pragma unroll
-      for (int l = 0; l < S; l++) O[l] = ldexp(O[l], e);
-      row_write<double>(tile, lane, c, O);
-      __syncthreads();
-      tile_store<double>(x3, base, n, tile);
-    }
+    __syncthreads();
+    tile_store<double>(x3, base, n, tile);
     __syncthreads();  // tile and small_mask are reused by the next trip
-    return next;
-  };
-  if constexpr (kDyn) {
-    int64_t base = (int64_t)blockIdx.x * 64;
-    for (int i = 0; base < n; i++) {
-      if (threadIdx.x == 0) qslot = pq.next_base(i);
-      base = trip(base);
-    }
-    pq.finish();
-  } else {
-    for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) trip(base);
   }
   if constexpr (kSum) block_ticket_sum(acc, ws, scaler_sum);
 }
@@ -255,14 +171,13 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
 
 namespace {
 
-// rows per chain group (phases 1 and 2): kRows independent fma chains per
-// wave; blocks per CU (launch bounds: kMinW waves per SIMD); kCols: 0 = chunks
-// of 4 columns loaded after the previous chunk, else double-buffered chunks
-// of kCols columns.  PLFX_VALU_FORM (A/B only) picks a form at first use.
-template <bool kSum, int kRows, int kMinW, int kCols, bool kOT = false, bool kDyn = false>
-hipError_t launch_valu_k(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  if (kDyn && !a.ws) return hipErrorInvalidValue;
-  auto kernel = &dev::plf_prot_valu_fma_kernel<kSum, kRows, kMinW, kCols, kOT, kDyn>;
+// 5 rows per chain group, 2-column double-buffered chunks, 3 waves per SIMD
+// (profiles/r06_protein_valu_forms.log, form 2)
+constexpr int kValuRows = 5, kValuCols = 2, kValuMinW = 3;
+
+template <bool kSum>
+hipError_t launch_valu_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
+  auto kernel = &dev::plf_prot_valu_fma_kernel<kSum, kValuRows, kValuCols, kValuMinW>;
   static int resident = 0;
   if (!resident) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -280,29 +195,6 @@ hipError_t launch_valu_k(const DnaArgs &a, int max_blocks, hipStream_t s) {
                      (const double *)a.x2, (double *)a.x3, (const double *)a.EV, (const double *)a.left,
                      (const double *)a.right, a.wgt, a.scaler, a.n, a.ws, a.scaler_sum);
   return hipGetLastError();
-}
-
-template <bool kSum>
-hipError_t launch_valu_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  static int form = -1;
-  if (form < 0) {
-    const char *e = std::getenv("PLFX_VALU_FORM");
-    form = e ? std::atoi(e) : 0;
-  }
-  switch (form) {
-    case 1: return launch_valu_k<kSum, 5, 3, 1>(a, max_blocks, s);
-    case 2: return launch_valu_k<kSum, 5, 3, 2>(a, max_blocks, s);
-    case 3: return launch_valu_k<kSum, 4, 3, 1>(a, max_blocks, s);
-    case 4: return launch_valu_k<kSum, 10, 3, 1>(a, max_blocks, s);
-    case 5: return launch_valu_k<kSum, 5, 2, 0>(a, max_blocks, s);
-    case 6: return launch_valu_k<kSum, 10, 2, 0>(a, max_blocks, s);
-    case 7: return launch_valu_k<kSum, 5, 3, 0, true>(a, max_blocks, s);
-    case 8: return launch_valu_k<kSum, 5, 3, 1, true>(a, max_blocks, s);
-    case 9: return launch_valu_k<kSum, 5, 3, 2, false, true>(a, max_blocks, s);
-    case 10: return launch_valu_k<kSum, 5, 3, 0, false, true>(a, max_blocks, s);
-    case 11: return launch_valu_k<kSum, 4, 3, 2, false, true>(a, max_blocks, s);
-    default: return launch_valu_k<kSum, 5, 3, 0>(a, max_blocks, s);
-  }
 }
 
 }  // namespace
