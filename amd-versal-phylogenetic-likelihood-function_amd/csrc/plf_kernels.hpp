@@ -37,6 +37,9 @@ hipError_t launch_plf_prot(int dtype, bool fma, const DnaArgs &a, int max_blocks
 // PLFX_FMA | PLFX_VALU): bit-identical to the matrix-core FMA kernel, dense
 // children, one node.
 hipError_t launch_plf_prot_valu_f64(const DnaArgs &a, int max_blocks, hipStream_t s);
+// Protein f64 in exact mode with the matrices as scalar operands
+// (plf_prot_valu_exact.hip): bit-identical to the LDS-matrix exact kernel.
+hipError_t launch_plf_prot_valu_exact_f64(const DnaArgs &a, int max_blocks, hipStream_t s);
 
 // Batched nodes (<= kMaxBatch per launch) sharing EV, n, wgt.  dtype: 0 f32, 1 f64.
 // tips: 0 dense children; 1 x1 of every node is a tip (uint8 state codes);

@@ -793,8 +793,8 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
   if (flags & ~(PLFX_FMA | PLFX_VALU)) return fail(ctx, PLFX_ERR_INVALID, "bad flags %d", flags);
   const bool valu = (flags & PLFX_VALU) != 0;
-  if (valu && (!(flags & PLFX_FMA) || states != 20 || dtype != PLFX_F64))
-    return fail(ctx, PLFX_ERR_INVALID, "PLFX_VALU: protein (states 20), f64, with PLFX_FMA only");
+  if (valu && (states != 20 || dtype != PLFX_F64))
+    return fail(ctx, PLFX_ERR_INVALID, "PLFX_VALU: protein (states 20), f64 only");
   if (states == 4) {
     return dtype == PLFX_F32
                ? plf_dev<float>(ctx, (const float *)x1, (const float *)x2, (float *)x3,
@@ -815,8 +815,10 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
   }
   PLFX_WS(ctx, s, w);
   plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, w->ws, n};
-  hipError_t e = valu ? plfx::launch_plf_prot_valu_f64(a, ctx->max_blocks, s)
-                      : plfx::launch_plf_prot(dtype, (flags & PLFX_FMA) != 0, a, ctx->max_blocks, s);
+  const bool fma = (flags & PLFX_FMA) != 0;
+  hipError_t e = !valu ? plfx::launch_plf_prot(dtype, fma, a, ctx->max_blocks, s)
+                 : fma ? plfx::launch_plf_prot_valu_f64(a, ctx->max_blocks, s)
+                       : plfx::launch_plf_prot_valu_exact_f64(a, ctx->max_blocks, s);
   if (e != hipSuccess) return hip_fail(ctx, e, valu ? "plf_prot_valu launch" : "plf_prot launch");
   return PLFX_OK;
 }

@@ -193,8 +193,9 @@ def test_codeobj_walks_every_bundle(tmp_path):
     p = tmp_path / "libtwo.so"
     p.write_bytes(bytes(data))
     # one code object per HIP translation unit of libplfx (plf_kernels.hip,
-    # plf_prot_valu.hip), the host-only bundle contributing none
-    assert len(codeobj.gfx950_code_objects(p)) == len(codeobj.gfx950_code_objects(lib)) == 2
+    # plf_prot_valu.hip, plf_prot_valu_exact.hip), the host-only bundle
+    # contributing none
+    assert len(codeobj.gfx950_code_objects(p)) == len(codeobj.gfx950_code_objects(lib)) == 3
     for k in ("plf_dna_f64_pair_kernel", "plf_dna_kernel", "root_lnl_kernel", "plf_prot_valu_fma_kernel"):
         assert codeobj.kernel_code_sha256(p, k) == codeobj.kernel_code_sha256(lib, k)
 

@@ -959,7 +959,7 @@ def test_protein_valu_fma_bits(ctx, oracle, n):
 def test_protein_valu_fma_signed_zeros_and_flags(ctx, oracle):
     """The VALU FMA chains start from +0.0 as the fma() restatement does, on
     inputs full of +-0.0 and underflowing products; PLFX_VALU is refused
-    without PLFX_FMA, in f32 and for DNA."""
+    in f32 and for DNA; in exact mode the same form gives plf()'s bits."""
     import torch
 
     import plfx
@@ -981,13 +981,29 @@ def test_protein_valu_fma_signed_zeros_and_flags(ctx, oracle):
     e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
     assert np.array_equal(bits(x3), bits(e3))
     assert np.array_equal(sc, esc) and s == einc
-    t = [dev(a) for a in (x1, x2, EV, left, right)]
-    out = torch.empty_like(t[0])
-    with pytest.raises(plfx.PlfxError):
-        ctx.plf_dev_gen(t[0], t[1], out, t[2], t[3], t[4], S, fma=False, valu=True)
+    # exact mode with the scalar-operand matrices: plf()'s loop bit for bit
+    x3, sc, s = run(ctx, x1, x2, EV, left, right, w, n, fma=False, valu=True)
+    e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w)
+    assert np.array_equal(bits(x3), bits(e3))
+    assert np.array_equal(sc, esc) and s == einc
     f = [dev(a.astype(np.float32)) for a in (x1, x2, EV, left, right)]
     with pytest.raises(plfx.PlfxError):
         ctx.plf_dev_gen(f[0], f[1], torch.empty_like(f[0]), f[2], f[3], f[4], S, fma=True, valu=True)
     d = [dev(a) for a in (x1[:16 * n], x2[:16 * n], EV[:16], left[:64], right[:64])]
     with pytest.raises(plfx.PlfxError):
         ctx.plf_dev_gen(d[0], d[1], torch.empty_like(d[0]), d[2], d[3], d[4], 4, fma=True, valu=True)
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 4097, 3 * (1 << 16) + 5, 1 << 18])
+def test_protein_valu_exact_bits(ctx, oracle, n):
+    """PLFX_EXACT | PLFX_VALU (plf_prot_valu_exact.hip: plf()'s separate
+    roundings with the matrices as scalar operands, 3 waves per SIMD):
+    bit-identical to plf()'s double loop (the oracle) and to the LDS-matrix
+    exact kernel, scaler bytes and weighted sum exact."""
+    x1, x2, EV, left, right, w = gen(n, np.float64, 700 + n % 89)
+    v3, vsc, vs = run(ctx, x1, x2, EV, left, right, w, n, fma=False, valu=True)
+    l3, lsc, ls = run(ctx, x1, x2, EV, left, right, w, n, fma=False)
+    assert np.array_equal(bits(v3), bits(l3)) and np.array_equal(vsc, lsc) and vs == ls
+    e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w)
+    assert np.array_equal(bits(v3), bits(e3))
+    assert np.array_equal(vsc, esc) and vs == einc
