@@ -55,20 +55,13 @@ hipError_t launch_k(const DnaArgs &a, int max_blocks, hipStream_t s) {
   return hipGetLastError();
 }
 
+// 4 rows per chain group, 2-column double-buffered scalar chunks, 3 waves per
+// SIMD: 130.0-130.5 us at 2^18 sites against the LDS-matrix kernel's 143.6-143.9
+// on the same box (profiles/r06_protein_exact_forms.log, form 3; five forms
+// A/B'd, plf_prot_valu_exact.hip@5ad7aa8)
 template <bool kSum>
 hipError_t launch_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  static int form = -1;
-  if (form < 0) {
-    const char *e = std::getenv("PLFX_EXACT_FORM");
-    form = e ? std::atoi(e) : 1;
-  }
-  switch (form) {
-    case 2: return launch_k<kSum, 5, 1, 3>(a, max_blocks, s);
-    case 3: return launch_k<kSum, 4, 2, 3>(a, max_blocks, s);
-    case 4: return launch_k<kSum, 10, 2, 2>(a, max_blocks, s);
-    case 5: return launch_k<kSum, 5, 2, 2>(a, max_blocks, s);
-    default: return launch_k<kSum, 5, 2, 3>(a, max_blocks, s);
-  }
+  return launch_k<kSum, 4, 2, 3>(a, max_blocks, s);
 }
 
 }  // namespace

@@ -815,10 +815,12 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
   }
   PLFX_WS(ctx, s, w);
   plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, w->ws, n};
+  // f64 exact: the scalar-operand kernel (plf_prot_valu_exact.hip, 3 waves per
+  // SIMD; +10 % over the LDS-matrix kernel, same bits) with or without PLFX_VALU
   const bool fma = (flags & PLFX_FMA) != 0;
-  hipError_t e = !valu ? plfx::launch_plf_prot(dtype, fma, a, ctx->max_blocks, s)
-                 : fma ? plfx::launch_plf_prot_valu_f64(a, ctx->max_blocks, s)
-                       : plfx::launch_plf_prot_valu_exact_f64(a, ctx->max_blocks, s);
+  hipError_t e = dtype == PLFX_F64 && !fma ? plfx::launch_plf_prot_valu_exact_f64(a, ctx->max_blocks, s)
+                 : valu                    ? plfx::launch_plf_prot_valu_f64(a, ctx->max_blocks, s)
+                                           : plfx::launch_plf_prot(dtype, fma, a, ctx->max_blocks, s);
   if (e != hipSuccess) return hip_fail(ctx, e, valu ? "plf_prot_valu launch" : "plf_prot launch");
   return PLFX_OK;
 }

@@ -198,8 +198,9 @@ int plfx_plf_dev_f64(plfx_ctx *ctx, const double *x1, const double *x2, double *
  * only, on the matrix cores -- v_mfma_f64_16x16x4 / v_mfma_f32_16x16x4 are
  * k-ordered fma chains, so the result is bit-identical to a fused VALU loop;
  * DNA is always exact).  PLFX_FMA | PLFX_VALU (protein f64, plfx_plf_dev_gen
- * only): the same fused chains on the VALU with the P matrices tiled in LDS
- * -- BASELINE configs[4]'s "matvec, not MFMA" -- bit-identical to PLFX_FMA. */
+ * only): the same fused chains on the VALU, the P matrices as scalar operands
+ * -- BASELINE configs[4]'s "matvec, not MFMA" -- bit-identical to PLFX_FMA.
+ * Exact mode is always on the VALU (PLFX_VALU accepted, no effect). */
 #define PLFX_EXACT 0
 #define PLFX_FMA 1
 #define PLFX_VALU 2

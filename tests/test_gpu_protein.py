@@ -996,14 +996,27 @@ def test_protein_valu_fma_signed_zeros_and_flags(ctx, oracle):
 
 @pytest.mark.parametrize("n", [1, 63, 65, 4097, 3 * (1 << 16) + 5, 1 << 18])
 def test_protein_valu_exact_bits(ctx, oracle, n):
-    """PLFX_EXACT | PLFX_VALU (plf_prot_valu_exact.hip: plf()'s separate
-    roundings with the matrices as scalar operands, 3 waves per SIMD):
-    bit-identical to plf()'s double loop (the oracle) and to the LDS-matrix
-    exact kernel, scaler bytes and weighted sum exact."""
+    """The f64 exact node (plf_prot_valu_exact.hip: plf()'s separate
+    roundings with the matrices as scalar operands, 3 waves per SIMD; the
+    default for exact f64, PLFX_VALU or not): bit-identical to plf()'s double
+    loop (the oracle) and to the LDS-matrix exact kernel, which still serves
+    batched and tip nodes (one batched launch of this node below), scaler
+    bytes and weighted sum exact."""
+    import torch
+
     x1, x2, EV, left, right, w = gen(n, np.float64, 700 + n % 89)
     v3, vsc, vs = run(ctx, x1, x2, EV, left, right, w, n, fma=False, valu=True)
-    l3, lsc, ls = run(ctx, x1, x2, EV, left, right, w, n, fma=False)
-    assert np.array_equal(bits(v3), bits(l3)) and np.array_equal(vsc, lsc) and vs == ls
+    d3, dsc, ds = run(ctx, x1, x2, EV, left, right, w, n, fma=False)
+    assert np.array_equal(bits(v3), bits(d3)) and np.array_equal(vsc, dsc) and vs == ds
+    t = [dev(a) for a in (x1, x2, EV, left, right, w)]
+    l3 = torch.empty_like(t[0])
+    lsc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ls = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.plf_batch_dev([dict(x1=t[0], x2=t[1], x3=l3, left=t[3], right=t[4], scaler=lsc, scaler_sum=ls)],
+                      t[2], n, wgt=t[5], states=S)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(v3), bits(l3.cpu().numpy())) and np.array_equal(vsc, lsc.cpu().numpy())
+    assert vs == int(ls.item())
     e3, esc, einc = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w)
     assert np.array_equal(bits(v3), bits(e3))
     assert np.array_equal(vsc, esc) and vs == einc
