@@ -6,6 +6,8 @@ import subprocess
 import sys
 import time
 
+import pytest
+
 from conftest import ROOT
 
 sys.path.insert(0, str(ROOT))
@@ -322,3 +324,24 @@ def test_flip_bit_and_window_offsets():
     f = torch.ones(4, dtype=torch.float32)
     bench.flip_bit(f, 0)
     assert f[0].item() != 1.0 and f[1:].eq(1).all()
+
+
+def test_region_lanes():
+    """Lanes: the node and protein workloads (independent nodes on rotating
+    buffer sets) alternate their steps over 2 streams by default; a workload
+    without lanes, an odd set count or a count not dividing the sets is
+    refused when asked for more; --lanes 1 is the single launch stream; the
+    sub-records keep --lanes only for protein."""
+    from types import SimpleNamespace as NS
+
+    a = bench.parse([])
+    assert a.lanes is None
+    assert bench.region_lanes(NS(lanes=2, R=4), a) == 2
+    assert bench.region_lanes(NS(R=1), a) == 1  # tree64 / nodes512 declare none
+    assert bench.region_lanes(NS(lanes=2, R=4), bench.parse(["--lanes", "1"])) == 1
+    for wl, n in ((NS(lanes=2, R=4), "3"), (NS(R=4), "2"), (NS(lanes=2, R=4), "0")):
+        with pytest.raises(SystemExit):
+            bench.region_lanes(wl, bench.parse(["--lanes", n]))
+    b = bench.parse(["--lanes", "1"])
+    assert bench.sub_args(b, "protein").lanes == 1 and bench.sub_args(b, "protein_exact").lanes == 1
+    assert bench.sub_args(b, "tree64").lanes is None and bench.sub_args(b, "nodes512").lanes is None

@@ -35,6 +35,10 @@ def _bench(*args, expect_rc=0):
     (("--workload", "protein", "--tips", "--sites", "4099"), 1),
     (("--workload", "protein", "--dtype", "f32", "--sites", "4099"), 1),
     (("--workload", "nodes512", "--nodes", "6", "--sites", "4099"), 6),
+    (("--workload", "node", "--lanes", "1", "--sites", "4099"), 1),
+    (("--workload", "node", "--launch", "bound", "--sites", "4099"), 1),
+    (("--workload", "protein", "--lanes", "1", "--sites", "4099"), 1),
+    (("--workload", "protein", "--launch", "bound", "--valu", "--sites", "4099"), 1),
 ])
 def test_workload_lines_carry_oracle_windows(args, windows):
     d = _bench(*args)
@@ -43,6 +47,9 @@ def test_workload_lines_carry_oracle_windows(args, windows):
     assert c["check_windows"] == windows and c["windows_mismatched"] == 0
     assert c["region_start"] == "single rank"
     assert d["value"] > 0 and d["roofline"]["frac"] > 0
+    # node / protein steps alternate over 2 streams unless --lanes 1
+    want = 1 if "--lanes" in args or args[1] in ("tree64", "nodes512") else 2
+    assert c["lanes"] == want == d["roofline"]["lanes"]
 
 
 def test_default_invocation_f32_with_every_sub_record():
@@ -58,6 +65,8 @@ def test_default_invocation_f32_with_every_sub_record():
         assert c[k]["dtype"] == "f32"
     for p in (c["protein"], c["protein"]["exact"]):
         assert p["check"] == "ok" and p["check_windows"] == 1 and p["dtype"] == "f32"
+        assert p["lanes"] == 2
+    assert c["lanes"] == 2 and c["nodes512"]["lanes"] == 1 and c["tree64"]["lanes"] == 1
     assert "valu_fma" not in c["protein"]  # the VALU FMA form is f64 only
 
 

@@ -8,7 +8,9 @@ mixes launches of different sizes.  This groups the plfx dispatches by
 (kernel, grid, workgroup) and prints count / average / min / max duration,
 and -- for the longest run of back-to-back dispatches of one shape with no
 other dispatch between them (the timed graph's replay; the host-array leg's
-launches sit between copy blits) -- the average over that run alone.  One JSON document.
+launches sit between copy blits) -- the average over that run alone, and the
+run's span (first start to last end) per dispatch, the per-step time when
+dispatches overlap (bench.py lanes).  One JSON document.
 
   python3 tools/trace_by_grid.py KERNEL_TRACE_CSV [OUT_JSON]
 """
@@ -41,15 +43,31 @@ def main():
         # between them (no blit, no other kernel): the replayed graph of the timed
         # region, not the host-array leg's launches between its copies
         ids = [pos[id(r)] for r in rs]
-        best, cur = [0], [0]
+
+        def span_of(run):
+            # first start to last end: per dispatch, the per-step time when the
+            # bench's lanes keep two dispatches in flight (each then lasts ~2x
+            # it); equal to the run's average when they run one after another
+            return (max(int(rs[i]["End_Timestamp"]) for i in run)
+                    - min(int(rs[i]["Start_Timestamp"]) for i in run)) / 1e3
+
+        runs, cur = [], [0]
         for i in range(1, len(ids)):
-            cur = cur + [i] if ids[i] == ids[i - 1] + 1 else [i]
-            if len(cur) > len(best):
-                best = cur
+            if ids[i] == ids[i - 1] + 1:
+                cur.append(i)
+            else:
+                runs.append(cur)
+                cur = [i]
+        runs.append(cur)
+        # the longest run; among equally long ones the densest (a run that
+        # spans host synchronisations is not the replayed graph)
+        best = min(runs, key=lambda r: (-len(r), span_of(r)))
         run = [d[i] for i in best]
+        span = span_of(best)
         out.append({"kernel": name, "grid": grid, "workgroup": wg, "dispatches": len(d),
                     "avg_us": round(st.mean(d), 3), "min_us": round(min(d), 3), "max_us": round(max(d), 3),
-                    "longest_consecutive_run": len(run), "run_avg_us": round(st.mean(run), 3)})
+                    "longest_consecutive_run": len(run), "run_avg_us": round(st.mean(run), 3),
+                    "run_span_us_per_dispatch": round(span / len(run), 3)})
     doc = {"trace": path, "groups": out}
     s = json.dumps(doc, indent=1)
     if len(sys.argv) > 2:
