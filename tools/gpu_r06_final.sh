@@ -7,7 +7,8 @@
 #      shape by tools/trace_by_grid.py (the host-array leg launches the node
 #      kernel at other grids);
 #   3. the N = 2 command shape at FULL size on the one GPU (gloo ranks
-#      folded onto it; rates meaningless, checks and memory real).
+#      folded onto it; rates meaningless, checks and memory real);
+# preceded by the whole GPU test suite on the same tree.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r06_final
@@ -22,7 +23,7 @@ step() {  # name, limit, command...
   return 0
 }
 cd $R
-step pytest_bench 600 python3 -u -m pytest tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread
+step pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 step bench_driver 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5
 grep '^{' $OUT/bench_driver.log > $OUT/bench_driver.json
 cd /tmp && export TMPDIR=/tmp

@@ -8,7 +8,8 @@ mixes launches of different sizes.  This groups the plfx dispatches by
 (kernel, grid, workgroup) and prints count / average / min / max duration,
 and -- for the longest run of back-to-back dispatches of one shape with no
 other dispatch between them (the timed graph's replay; the host-array leg's
-launches sit between copy blits) -- the average over that run alone, and the
+launches sit between copy blits; a host synchronisation's idle gap also ends a
+run) -- the average over that run alone, and the
 run's span (first start to last end) per dispatch, the per-step time when
 dispatches overlap (bench.py lanes).  One JSON document.
 
@@ -51,13 +52,19 @@ def main():
             return (max(int(rs[i]["End_Timestamp"]) for i in run)
                     - min(int(rs[i]["Start_Timestamp"]) for i in run)) / 1e3
 
+        # a run ends at another dispatch between two of this shape, or at an
+        # idle gap over 20 us with none of them in flight (a host
+        # synchronisation: the bench's warm-up, its region, its second region)
         runs, cur = [], [0]
+        busy = int(rs[0]["End_Timestamp"])  # the current run's latest end
         for i in range(1, len(ids)):
-            if ids[i] == ids[i - 1] + 1:
+            start, end = int(rs[i]["Start_Timestamp"]), int(rs[i]["End_Timestamp"])
+            if ids[i] == ids[i - 1] + 1 and start - busy <= 20000:
                 cur.append(i)
+                busy = max(busy, end)
             else:
                 runs.append(cur)
-                cur = [i]
+                cur, busy = [i], end
         runs.append(cur)
         # the longest run; among equally long ones the densest (a run that
         # spans host synchronisations is not the replayed graph)
@@ -67,7 +74,10 @@ def main():
         out.append({"kernel": name, "grid": grid, "workgroup": wg, "dispatches": len(d),
                     "avg_us": round(st.mean(d), 3), "min_us": round(min(d), 3), "max_us": round(max(d), 3),
                     "longest_consecutive_run": len(run), "run_avg_us": round(st.mean(run), 3),
-                    "run_span_us_per_dispatch": round(span / len(run), 3)})
+                    "run_span_us_per_dispatch": round(span / len(run), 3),
+                    # every run of at least 10: [dispatches, span per dispatch]
+                    # (the bench's warm-up, timed region and second region)
+                    "runs": [[len(r), round(span_of(r) / len(r), 3)] for r in runs if len(r) >= 10]})
     doc = {"trace": path, "groups": out}
     s = json.dumps(doc, indent=1)
     if len(sys.argv) > 2:
