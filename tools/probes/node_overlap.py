@@ -18,6 +18,8 @@ steps captured in one HIP graph as the bench does:
   g2f     g2 the same way: the even-step graph launched first, the odd-step
           graph's stream waits on the start event, no join on the device
   h2f     g2f with step 0 launched directly and the even-step graph from step 2
+  g2c     g2f through the HIP API directly (ctypes hipGraphLaunch /
+          hipStreamWaitEvent / hipEventRecord: no torch replay() around it)
 --spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is touched.
 Each variant's event time per step around one replay and its host wall from
 before the launch to after the synchronize (what bench.py's `value` divides
@@ -110,12 +112,15 @@ def main():
                 return False
         return True
 
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
     bytes_step = bench.bytes_per_site(esz) * wl.n
     for K in [int(x) for x in o.steps.split(",")]:
         gs = {f"s{S}": graph(K, S) for S in (1, 2, 4)}
         gs["g2"] = (half(K, 0, main_s), half(K, 1, side[0]))
         gs["g2f"] = gs["g2"]
         gs["h2f"] = (half(K, 0, main_s, skip=2), gs["g2"][1])
+        gs["g2c"] = gs["g2"]
         res = {k: [] for k in list(gs) + ["e1", "e2", "e2n", "e2f"] if not o.only or k in o.only.split(",")}
         wall = {k: [] for k in res}
         ok = True
@@ -131,6 +136,25 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e1b = torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
+                if k == "g2c":
+                    for e, st_ in ((e0, main_s), (e1, main_s), (e1b, side[0])):
+                        e.record(st_)  # creates the HIP events
+                    torch.cuda.synchronize()
+                    ex = [C.c_void_p(int(g.raw_cuda_graph_exec())) for g in gs[k]]
+                    hm, hs = C.c_void_p(main_s.cuda_stream), C.c_void_p(side[0].cuda_stream)
+                    he0, he1, he1b = (C.c_void_p(e.cuda_event) for e in (e0, e1, e1b))
+                    t0 = time.perf_counter()
+                    hip.hipEventRecord(he0, hm)
+                    hip.hipGraphLaunch(ex[0], hm)
+                    hip.hipStreamWaitEvent(hs, he0, 0)
+                    hip.hipGraphLaunch(ex[1], hs)
+                    hip.hipEventRecord(he1, hm)
+                    hip.hipEventRecord(he1b, hs)
+                    hip.hipDeviceSynchronize()
+                    wall[k].append((time.perf_counter() - t0) * 1e6 / K)
+                    res[k].append(max(e0.elapsed_time(e1), e0.elapsed_time(e1b)) * 1e3 / K)
+                    ok = ok and same()
+                    continue
                 t0 = time.perf_counter()
                 e0.record(main_s)
                 if k == "e2n":
