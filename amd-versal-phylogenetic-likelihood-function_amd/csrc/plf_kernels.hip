@@ -126,8 +126,13 @@ hipError_t launch_cat(const DnaArgs &a, int max_blocks, hipStream_t s) {
   // leaves 5.33 trips per wave at 3/CU (a sixth trip for a third of the waves)
   // and exactly 8 at 2/CU -- 35.4 vs 35.8 us, and 68.4 vs 69.2 us at 2^21
   // (tools/ab_defer.hip@f9b3af3, tools/tune_f32.hip@f9b3af3; profiles/r02_tune_f32.log)
+  // With `streams` calls in flight each takes 1/streams of it: two f32 nodes
+  // on two streams at 256 blocks each run 0.773 of the HBM peak in 20-step
+  // regions vs 0.746 at 512 (tools/probes/node_grid_lanes_f32.sh,
+  // profiles/r06_probe_node_grid_lanes.log)
   const int64_t gx = grid_x((const void *)kernel, cache, kGridMul32, a.n, kWavesPerBlock * 16 * kU32,
-                            1, max_blocks > 0 ? max_blocks : kBlocksPerCu32 * cu_count());
+                            1, max_blocks > 0 ? max_blocks
+                                              : std::max(1, kBlocksPerCu32 * cu_count() / std::max(1, a.streams)));
   const int64_t gs = segment_grid(a, gx, kSegMinSites32);
   if (gs) kernel = &dev::plf_dna_kernel<T, kU32, kSum, kNt, kMinWaves, 3>;
   hipLaunchKernelGGL(kernel, dim3((unsigned)(gs ? gs : gx)), dim3(kBlock), 0, s, (const T *)a.x1,
@@ -140,8 +145,12 @@ template <bool kSum>
 hipError_t launch_pair(const DnaArgs &a, int max_blocks, hipStream_t s) {
   static int cache = 0;
   auto kernel = &dev::plf_dna_f64_pair_kernel<kU64, kSum, kMinWaves, kNtl64>;
+  // resident blocks / streams: two 2^20-site nodes in flight on two streams at
+  // 512 blocks each (16 trips per block) run 0.775 in 20-step regions and 0.80
+  // in 200-step ones, vs 0.750 / 0.778 at 1024 (8 trips); one node alone at
+  // 512 runs 0.64 (tools/probes/node_grid_lanes.sh, profiles/r06_probe_node_grid_lanes.log)
   const int64_t gx = grid_x((const void *)kernel, cache, kGridMul64, a.n, kWavesPerBlock * 16 * kU64,
-                            1, max_blocks);
+                            std::max(1, a.streams), max_blocks);
   const int64_t gs = segment_grid(a, gx, kSegMinSites64);
   if (gs) kernel = &dev::plf_dna_f64_pair_kernel<kU64, kSum, kMinWaves, kNtl64, 3>;
   hipLaunchKernelGGL(kernel, dim3((unsigned)(gs ? gs : gx)), dim3(kBlock), 0, s, (const double *)a.x1,
@@ -253,7 +262,11 @@ hipError_t launch_prot_mfma_t(const DnaArgs &a, int max_blocks, hipStream_t s,
   // the fixed stride is as fast or faster (tools/tune_prot64d.hip@f9b3af3,
   // profiles/r03_tune_protein_dyn.log)
   auto kernel = &dev::plf_prot_mfma_kernel<kSum, 2, kTips, false>;
-  const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
+  // resident blocks / streams (two 2^18-site nodes in flight: 256 blocks each,
+  // +1-2 %; the VALU protein kernels keep their full grid, which measured best
+  // with two in flight too -- tools/probes/prot_grid_lanes.sh,
+  // profiles/r06_probe_prot_grid_lanes.log)
+  const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, std::max(1, a.streams), max_blocks);
   auto launch = [&](auto k) {
     hipLaunchKernelGGL(k, dim3((unsigned)gx), dim3(kBlock), 0, s, (const double *)a.x1,
                        (const double *)a.x2, (double *)a.x3, (const double *)a.EV,

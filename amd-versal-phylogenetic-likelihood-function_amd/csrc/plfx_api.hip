@@ -64,6 +64,7 @@ struct plfx_ctx {
   int max_blocks = 0;               // grid cap for the grid-stride kernels (0 = resident blocks)
   int node_segments = -1;           // node kernels' XCD-segmented mapping: -1 by size, 0 off, 1 on
                                     // (PLFX_NODE_SEGMENTS; plf_kernels.hip use_segments)
+  int streams = 1;                  // one-node calls kept in flight (plfx_ctx_set_streams, PLFX_STREAMS)
   int fuse = 3;  // traverse: 3 six-level subtrees before 2's, 2 three-level subtrees +
                  // level pairs, 1 level pairs, 0 none (PLFX_FUSE)
   bool lazy_tables = false;         // PLFX_CTX_LAZY_TABLES
@@ -347,6 +348,7 @@ int plf_dev(plfx_ctx *ctx, const T *x1, const T *x2, T *x3, const T *EV, int64_t
   }
   PLFX_WS(ctx, s, w);
   plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, w->ws, n, ctx->node_segments};
+  a.streams = ctx->streams;
   hipError_t e = sizeof(T) == 4 ? plfx::launch_plf_dna_f32(a, ctx->max_blocks, s)
                                 : plfx::launch_plf_dna_f64(a, ctx->max_blocks, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "plf_dna launch");
@@ -637,6 +639,20 @@ int plfx_ctx_create_ex(int device, unsigned flags, plfx_ctx **out) {
       return PLFX_ERR_INVALID;
     }
   }
+  // PLFX_STREAMS: one-node calls kept in flight, "1".."8" (PLFX_STREAMS_MAX), empty
+  // = 1; anything else is refused like PLFX_NODE_SEGMENTS
+  const char *streams_env = std::getenv("PLFX_STREAMS");
+  if (streams_env && *streams_env) {
+    const char *env = streams_env;
+    static_assert(PLFX_STREAMS_MAX <= 9, "PLFX_STREAMS is parsed as one digit");
+    const int v = (env[0] >= '1' && env[0] <= '0' + PLFX_STREAMS_MAX && !env[1]) ? env[0] - '0' : 0;
+    if (!v) {
+      (void)hipStreamDestroy(ctx->stream);
+      delete ctx;
+      return PLFX_ERR_INVALID;
+    }
+    ctx->streams = v;
+  }
   // the workspace pool: kWsPool entries (reduction words zeroed before return,
   // tip/tip tables), and the tables' constant code arrays
   auto undo = [&](int code) {
@@ -758,6 +774,21 @@ int plfx_ctx_release_stream(plfx_ctx *ctx, void *stream) {
   return PLFX_OK;
 }
 
+int plfx_ctx_set_streams(plfx_ctx *ctx, int streams) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  if (streams < 1 || streams > PLFX_STREAMS_MAX)
+    return fail(ctx, PLFX_ERR_INVALID, "streams %d not in 1..%d", streams, PLFX_STREAMS_MAX);
+  ctx->streams = streams;
+  return PLFX_OK;
+}
+
+int plfx_ctx_streams(const plfx_ctx *ctx) {
+  if (!ctx) return PLFX_ERR_INVALID;
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  return ctx->streams;
+}
+
 int plfx_plf_f32(plfx_ctx *ctx, const float *x1, const float *x2, float *x3, const float *EV, int n,
                  const float *left, const float *right, const int *wgt, int *scalerIncrement) {
   PLFX_BIND(ctx);
@@ -815,6 +846,7 @@ int plfx_plf_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const void
   }
   PLFX_WS(ctx, s, w);
   plfx::DnaArgs a{x1, x2, x3, EV, left, right, wgt, scaler, scaler_sum, w->ws, n};
+  a.streams = ctx->streams;
   // f64 exact: the scalar-operand kernel (plf_prot_valu_exact.hip, 3 waves per
   // SIMD; +10 % over the LDS-matrix kernel, same bits) with or without PLFX_VALU
   const bool fma = (flags & PLFX_FMA) != 0;

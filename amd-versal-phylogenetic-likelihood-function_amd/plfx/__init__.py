@@ -39,6 +39,7 @@ F32, F64 = 0, 1
 EXPORTS = (
     "plfx_ctx_create", "plfx_ctx_create_ex", "plfx_ctx_destroy", "plfx_last_error", "plfx_get_version",
     "plfx_ctx_stream", "plfx_ctx_device", "plfx_ctx_synchronize", "plfx_ctx_release_stream",
+    "plfx_ctx_set_streams", "plfx_ctx_streams",
     "plfx_plf_f32", "plfx_plf_f64", "plfx_plf_dev_f32", "plfx_plf_dev_f64",
     "plfx_instance_run", "plfx_instance_run_host", "plfx_scaler_sum",
     "plfx_tb_alignments_per_instance", "plfx_tb_alignments_padding",
@@ -55,6 +56,7 @@ EXPORTS = (
 )
 MAX_STREAMS = 64   # PLFX_MAX_STREAMS
 WS_POOL = 8        # PLFX_WS_POOL
+STREAMS_MAX = 8    # PLFX_STREAMS_MAX
 STREAM_PER_THREAD = 2  # hipStreamPerThread
 SCHED_KEYS = ("deep6", "deep5", "deep4", "septets", "triples", "unfused", "launches")
 PMAT_STATE, PMAT_EIGEN = 0, 1
@@ -114,6 +116,8 @@ def load():
     L.plfx_ctx_device.argtypes = [vp]
     L.plfx_ctx_synchronize.argtypes = [vp]
     L.plfx_ctx_release_stream.argtypes = [vp, vp]
+    L.plfx_ctx_set_streams.argtypes = [vp, i32]
+    L.plfx_ctx_streams.argtypes = [vp]
     for s in ("f32", "f64"):
         getattr(L, f"plfx_plf_{s}").argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, C.POINTER(i32)]
         getattr(L, f"plfx_plf_dev_{s}").argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
@@ -220,6 +224,17 @@ class Context:
 
     def synchronize(self):
         self._check(self._L.plfx_ctx_synchronize(self.h))
+
+    @property
+    def streams(self):
+        """One-node calls kept in flight (plfx_ctx_streams)."""
+        return self._L.plfx_ctx_streams(self.h)
+
+    def set_streams(self, streams):
+        """Tell the context that `streams` one-node calls run at once, each on
+        its own stream (plfx_ctx_set_streams: the dense DNA node and f64
+        protein FMA kernels then launch the resident blocks / streams)."""
+        self._check(self._L.plfx_ctx_set_streams(self.h, int(streams)))
 
     def release_stream(self, stream):
         """Wait for `stream` and return its scaler-sum workspace to the pool

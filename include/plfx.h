@@ -113,9 +113,10 @@
 extern "C" {
 #endif
 
-#define PLFX_VERSION 10200 /* 1.2.0 */
+#define PLFX_VERSION 10300 /* 1.3.0 */
 #define PLFX_MAX_STREAMS 64 /* streams holding a workspace at a time, per context */
 #define PLFX_WS_POOL 8      /* workspaces allocated with the context */
+#define PLFX_STREAMS_MAX 8  /* plfx_ctx_set_streams */
 
 typedef enum {
   PLFX_OK = 0,
@@ -156,6 +157,23 @@ int plfx_ctx_synchronize(plfx_ctx *ctx);
  * pool.  PLFX_OK also when the stream holds none.  (Extension: the reference's
  * XRT queues are fixed per instance, host_mem.cpp:123-127.) */
 int plfx_ctx_release_stream(plfx_ctx *ctx, void *stream);
+/* One-node calls the caller keeps in flight at once, each on its own stream
+ * (default 1; PLFX_STREAMS=1..8 in the environment at context creation,
+ * empty = 1, anything else fails plfx_ctx_create with PLFX_ERR_INVALID).  The dense
+ * one-node DNA kernels (plfx_plf_dev_f32 / _f64, plfx_plf_dev_gen with 4
+ * states, and the host entries' chunks) and the f64 protein FMA kernel
+ * (plfx_plf_dev_gen, 20 states, PLFX_FMA) then launch the co-resident blocks
+ * / streams, so the calls in flight fill the GPU together and one call's
+ * drain overlaps the others' work: 2^20-site f64 nodes alternating over two
+ * streams run 0.80 of the HBM peak instead of 0.78 (0.75 one at a time),
+ * f32 0.81 instead of 0.77.  Same bits for any value.
+ * A call issued alone with streams > 1 runs on the smaller grid (0.64 for
+ * the f64 node at 2): set it to what is actually in flight.  Other entry
+ * points ignore it.  (Extension: the reference's instances run side by side,
+ * app/src/include.h:181-195.)  set: PLFX_ERR_INVALID outside 1..8; get: the
+ * value, or PLFX_ERR_INVALID for a null context. */
+int plfx_ctx_set_streams(plfx_ctx *ctx, int streams);
+int plfx_ctx_streams(const plfx_ctx *ctx);
 
 /* ---- (1) drop-in for plf(): host arrays, synchronous -------------------- */
 /* Same argument order and meaning as plf() (app/src/plf.h:1-5); `int&` is

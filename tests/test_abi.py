@@ -49,7 +49,7 @@ def test_python_binding_lists_all_exports():
 def test_version():
     import plfx
 
-    assert plfx.load().plfx_get_version() == 10200
+    assert plfx.load().plfx_get_version() == 10300
 
 
 def _cases():

@@ -257,6 +257,12 @@ def test_traffic_not_reported_under_dispatch_knobs(monkeypatch):
     assert "knob" not in bench.traffic_record(a, W())["traffic_note"]
     monkeypatch.setenv("PLFX_MAX_BLOCKS", "64")
     assert "PLFX_MAX_BLOCKS" in bench.traffic_record(a, W())["traffic_note"]
+    monkeypatch.delenv("PLFX_MAX_BLOCKS")
+    for v in ("", "1"):
+        monkeypatch.setenv("PLFX_STREAMS", v)
+        assert "knob" not in bench.traffic_record(a, W())["traffic_note"]
+    monkeypatch.setenv("PLFX_STREAMS", "2")
+    assert "PLFX_STREAMS" in bench.traffic_record(a, W())["traffic_note"]
 
 
 def test_pmc_tools_record_launch_shapes():

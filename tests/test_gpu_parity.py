@@ -381,6 +381,98 @@ def test_segment_grid_never_exceeds_block_cap(oracle, monkeypatch, cap):
     monkeypatch.delenv("PLFX_NODE_SEGMENTS")
 
 
+@pytest.mark.parametrize("streams", [2, 3])
+def test_streams_setting_grids_and_bits(oracle, monkeypatch, streams):
+    """plfx_ctx_set_streams (bench.py lanes): with `streams` one-node calls in
+    flight the dense DNA node kernels (f32, f64) and the f64 protein FMA
+    kernel launch the resident blocks / streams -- the captured grids say so
+    -- and give the same bits as with 1, also with `streams` calls running at
+    once on as many streams; other values and bad PLFX_STREAMS are refused."""
+    import torch
+
+    import plfx
+
+    c = plfx.Context(0)
+    try:
+        assert c.streams == 1
+        for bad in (0, plfx.STREAMS_MAX + 1, -1):
+            with pytest.raises(plfx.PlfxError):
+                c.set_streams(bad)
+        assert c.streams == 1
+        n = 1 << 20
+        for dtype in (np.float32, np.float64):
+            d = oracle.gen_hostmem(n, dtype, 23 + streams)
+            e3, esc, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"],
+                                       threads=16)
+            t = {k: torch_dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+            outs = [(torch.empty_like(t["x1"]), torch.empty(n, dtype=torch.uint8, device="cuda"),
+                     torch.zeros(1, dtype=torch.int64, device="cuda")) for _ in range(streams)]
+
+            def call(sh, o=outs[0]):
+                c.plf_dev(t["x1"], t["x2"], o[0], t["EV"], t["left"], t["right"], t["wgt"], o[1], o[2],
+                          stream=sh)
+
+            grids = {}
+            for k in (1, streams):
+                c.set_streams(k)
+                grids[k] = [g for g in _captured_grids(call) if g[0] and "plf_dna" in g[0]]
+                assert len(grids[k]) == 1, grids
+            assert grids[streams][0][1] == grids[1][0][1] // streams, grids
+            # `streams` calls at once, one per stream, on the smaller grids
+            sts = [torch.cuda.Stream() for _ in range(streams)]
+            torch.cuda.synchronize()
+            for o, st_ in zip(outs, sts):
+                call(st_.cuda_stream, o)
+            torch.cuda.synchronize()
+            for o in outs:
+                assert np.array_equal(bits(o[0].cpu().numpy()), bits(e3))
+                assert np.array_equal(o[1].cpu().numpy(), esc) and int(o[2].item()) == einc
+            for st_ in sts:
+                c.release_stream(st_)
+            c.set_streams(1)
+            del t, outs
+        # protein f64 FMA (matrix cores): same bits at 1 and `streams`
+        m = 1 << 18
+        g = torch.Generator(device="cuda")
+        g.manual_seed(5)
+        x1 = torch.rand(m * 80, dtype=torch.float64, device="cuda", generator=g)
+        x1.view(-1, 80)[0::4] *= 1e-14
+        x2 = torch.rand(m * 80, dtype=torch.float64, device="cuda", generator=g)
+        EV = torch.rand(400, dtype=torch.float64, device="cuda", generator=g) - 0.25
+        P = torch.rand(3200, dtype=torch.float64, device="cuda", generator=g)
+        res = {}
+        for k in (1, streams):
+            c.set_streams(k)
+            x3 = torch.empty_like(x1)
+            sc = torch.empty(m, dtype=torch.uint8, device="cuda")
+            ss = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+            def pcall(sh):
+                c.plf_dev_gen(x1, x2, x3, EV, P[:1600], P[1600:], 20, None, sc, ss, fma=True, stream=sh)
+
+            pg = [x for x in _captured_grids(pcall) if x[0] and "plf_prot_mfma" in x[0]]
+            assert len(pg) == 1, pg
+            res[k] = (pg[0][1], x3.cpu().numpy(), sc.cpu().numpy(), int(ss.item()))
+        assert res[streams][0] == res[1][0] // streams
+        assert np.array_equal(bits(res[1][1]), bits(res[streams][1]))
+        assert np.array_equal(res[1][2], res[streams][2]) and res[1][3] == res[streams][3] > 0
+    finally:
+        c.close()
+    monkeypatch.setenv("PLFX_STREAMS", str(streams))
+    c = plfx.Context(0)
+    assert c.streams == streams
+    c.close()
+    for bad in ("0", "9", "x", "12", " 2"):
+        monkeypatch.setenv("PLFX_STREAMS", bad)
+        with pytest.raises(Exception):
+            plfx.Context(0)
+    monkeypatch.setenv("PLFX_STREAMS", "")
+    c = plfx.Context(0)
+    assert c.streams == 1
+    c.close()
+    monkeypatch.delenv("PLFX_STREAMS")
+
+
 def test_plf_dev_repeated_calls_and_optional_outputs(ctx, oracle):
     """The in-kernel ticket reduction resets itself: back-to-back launches with
     different weights each report their own sum; outputs are optional."""

@@ -20,6 +20,7 @@ steps captured in one HIP graph as the bench does:
   h2f     g2f with step 0 launched directly and the even-step graph from step 2
   g2c     g2f through the HIP API directly (ctypes hipGraphLaunch /
           hipStreamWaitEvent / hipEventRecord: no torch replay() around it)
+  gc3,gc4 g2c over 3 / 4 lanes (--sets must be a multiple of the lanes)
 --spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is touched.
 Each variant's event time per step around one replay and its host wall from
 before the launch to after the synchronize (what bench.py's `value` divides
@@ -51,6 +52,7 @@ def main():
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--only", default="", help="comma-separated variants (default: all)")
     ap.add_argument("--spin", action="store_true")
+    ap.add_argument("--sets", type=int, default=4, help="buffer sets")
     o = ap.parse_args()
     if o.spin:
         import ctypes as C
@@ -59,7 +61,7 @@ def main():
     dev = torch.device("cuda", 0)
     esz = 8 if o.dtype == "f64" else 4
     tdt = torch.float64 if esz == 8 else torch.float32
-    a = bench.parse(["--steps", "20", "--warmup", "5", "--dtype", o.dtype])
+    a = bench.parse(["--steps", "20", "--warmup", "5", "--dtype", o.dtype, "--buffer-sets", str(o.sets)])
     ctx = plfx.Context(0, lazy_tables=True)
     wl = bench.NodeWorkload(ctx, a, dev, None, tdt, esz)
     main_s = torch.cuda.Stream(dev)
@@ -87,10 +89,10 @@ def main():
         torch.cuda.synchronize()
         return g
 
-    def half(K, parity, s, skip=0):
+    def half(K, parity, s, skip=0, L=2):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
-            for i in range(parity + skip, K, 2):
+            for i in range(parity + skip, K, L):
                 wl.step(i, s.cuda_stream)
         torch.cuda.synchronize()
         return g
@@ -121,6 +123,9 @@ def main():
         gs["g2f"] = gs["g2"]
         gs["h2f"] = (half(K, 0, main_s, skip=2), gs["g2"][1])
         gs["g2c"] = gs["g2"]
+        for L in (3, 4):
+            if f"gc{L}" in o.only.split(",") and o.sets % L == 0:
+                gs[f"gc{L}"] = tuple(half(K, l, ([main_s] + side)[l], L=L) for l in range(L))
         res = {k: [] for k in list(gs) + ["e1", "e2", "e2n", "e2f"] if not o.only or k in o.only.split(",")}
         wall = {k: [] for k in res}
         ok = True
@@ -136,23 +141,27 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e1b = torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
-                if k == "g2c":
-                    for e, st_ in ((e0, main_s), (e1, main_s), (e1b, side[0])):
-                        e.record(st_)  # creates the HIP events
+                if k in ("g2c", "gc3", "gc4"):
+                    lanes = [main_s] + side[:len(gs[k]) - 1]
+                    ends = [torch.cuda.Event(enable_timing=True) for _ in lanes]
+                    e0.record(main_s)  # creates the HIP events
+                    for e, st_ in zip(ends, lanes):
+                        e.record(st_)
                     torch.cuda.synchronize()
                     ex = [C.c_void_p(int(g.raw_cuda_graph_exec())) for g in gs[k]]
-                    hm, hs = C.c_void_p(main_s.cuda_stream), C.c_void_p(side[0].cuda_stream)
-                    he0, he1, he1b = (C.c_void_p(e.cuda_event) for e in (e0, e1, e1b))
+                    hl = [C.c_void_p(st_.cuda_stream) for st_ in lanes]
+                    he0 = C.c_void_p(e0.cuda_event)
                     t0 = time.perf_counter()
-                    hip.hipEventRecord(he0, hm)
-                    hip.hipGraphLaunch(ex[0], hm)
-                    hip.hipStreamWaitEvent(hs, he0, 0)
-                    hip.hipGraphLaunch(ex[1], hs)
-                    hip.hipEventRecord(he1, hm)
-                    hip.hipEventRecord(he1b, hs)
+                    hip.hipEventRecord(he0, hl[0])
+                    for j, (h, x) in enumerate(zip(hl, ex)):
+                        if j:
+                            hip.hipStreamWaitEvent(h, he0, 0)
+                        hip.hipGraphLaunch(x, h)
+                    for h, e in zip(hl, ends):
+                        hip.hipEventRecord(C.c_void_p(e.cuda_event), h)
                     hip.hipDeviceSynchronize()
                     wall[k].append((time.perf_counter() - t0) * 1e6 / K)
-                    res[k].append(max(e0.elapsed_time(e1), e0.elapsed_time(e1b)) * 1e3 / K)
+                    res[k].append(max(e0.elapsed_time(e) for e in ends) * 1e3 / K)
                     ok = ok and same()
                     continue
                 t0 = time.perf_counter()
