@@ -337,7 +337,7 @@ def test_region_lanes():
     buffer sets) alternate their steps over 2 streams by default; a workload
     without lanes, an odd set count or a count not dividing the sets is
     refused when asked for more; --lanes 1 is the single launch stream; the
-    sub-records keep --lanes only for protein."""
+    sub-records pass --lanes on to all but tree64."""
     from types import SimpleNamespace as NS
 
     a = bench.parse([])
@@ -350,4 +350,5 @@ def test_region_lanes():
             bench.region_lanes(wl, bench.parse(["--lanes", n]))
     b = bench.parse(["--lanes", "1"])
     assert bench.sub_args(b, "protein").lanes == 1 and bench.sub_args(b, "protein_exact").lanes == 1
-    assert bench.sub_args(b, "tree64").lanes is None and bench.sub_args(b, "nodes512").lanes is None
+    assert bench.sub_args(b, "tree64").lanes is None and bench.sub_args(b, "nodes512").lanes == 1
+    assert a.per_launch == 1 and bench.parse(["--per-launch", "32"]).per_launch == 32

@@ -35,6 +35,7 @@ def _bench(*args, expect_rc=0):
     (("--workload", "protein", "--tips", "--sites", "4099"), 1),
     (("--workload", "protein", "--dtype", "f32", "--sites", "4099"), 1),
     (("--workload", "nodes512", "--nodes", "6", "--sites", "4099"), 6),
+    (("--workload", "nodes512", "--nodes", "70", "--per-launch", "32", "--sites", "4099"), 70),
     (("--workload", "node", "--lanes", "1", "--sites", "4099"), 1),
     (("--workload", "node", "--launch", "bound", "--sites", "4099"), 1),
     (("--workload", "protein", "--lanes", "1", "--sites", "4099"), 1),
@@ -48,7 +49,7 @@ def test_workload_lines_carry_oracle_windows(args, windows):
     assert c["region_start"] == "single rank"
     assert d["value"] > 0 and d["roofline"]["frac"] > 0
     # node / protein steps alternate over 2 streams unless --lanes 1
-    want = 1 if "--lanes" in args or args[1] in ("tree64", "nodes512") else 2
+    want = 1 if "--lanes" in args or args[1] == "tree64" else 2
     assert c["lanes"] == want == d["roofline"]["lanes"]
 
 
@@ -66,7 +67,7 @@ def test_default_invocation_f32_with_every_sub_record():
     for p in (c["protein"], c["protein"]["exact"]):
         assert p["check"] == "ok" and p["check_windows"] == 1 and p["dtype"] == "f32"
         assert p["lanes"] == 2
-    assert c["lanes"] == 2 and c["nodes512"]["lanes"] == 1 and c["tree64"]["lanes"] == 1
+    assert c["lanes"] == 2 and c["nodes512"]["lanes"] == 2 and c["tree64"]["lanes"] == 1
     assert "valu_fma" not in c["protein"]  # the VALU FMA form is f64 only
 
 

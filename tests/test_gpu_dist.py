@@ -166,10 +166,12 @@ def _assert_checked(d, world, nodes):
     assert "not MFMA" in c["protein"]["valu_fma"]["workload"]
 
 
-def test_nodes512_full_size_windows(oracle):
+@pytest.mark.parametrize("per_launch", [1, 32])
+def test_nodes512_full_size_windows(oracle, per_launch):
     """BASELINE configs[3] at full size on one GPU, as bench.py times it: the
-    512 nodes x 2^20 f64 sites of bench.NodesWorkload (201 GB of CLVs) in its
-    16 interleaved 32-node launches.  A 1024-site window of every node is
+    512 nodes x 2^20 f64 sites of bench.NodesWorkload (201 GB of CLVs) in one
+    launch per node over two lanes (the default), and in 16 interleaved
+    32-node launches.  A 1024-site window of every node is
     checked bit for bit against the oracle on that window (x3 and scaler
     bytes; every 64th node also against the reference's own plf() in
     double), and every node's scaler sum is its N/4 rescaled sites."""
@@ -179,14 +181,20 @@ def test_nodes512_full_size_windows(oracle):
     import plfx
 
     n = 1 << 20
-    a = bench.parse(["--workload", "nodes512"])
+    a = bench.parse(["--workload", "nodes512", "--per-launch", str(per_launch)])
     assert a.nodes == 512 and a.sites == n
     dev = torch.device("cuda", 0)
     with plfx.Context(0) as ctx:
         wl = bench.NodesWorkload(ctx, a, dev, None, torch.float64, 8, 1, 0)
-        assert wl.cnt == 512 and len(wl.launchers) == 16
-        wl.step(0, torch.cuda.current_stream().cuda_stream)
+        assert wl.cnt == 512 and len(wl.launchers) == (512 if per_launch == 1 else 16)
+        assert wl.lanes == 2
+        lanes = [torch.cuda.Stream(), torch.cuda.Stream()]
+        ctx.set_streams(2)
         torch.cuda.synchronize()
+        for lane, st_ in enumerate(lanes):  # as the bench's lanes issue one step
+            wl.issue(0, lane, 2, st_.cuda_stream)
+        torch.cuda.synchronize()
+        ctx.set_streams(1)
         EV = wl.EV.cpu().numpy()
         ones = np.ones(1024, dtype=np.int32)
         for j, nd in enumerate(wl.nodes):
