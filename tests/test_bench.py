@@ -232,8 +232,9 @@ def test_launch_check_against_record_shapes():
     assert not ok and "dispatched as" in why
     ok, why = bench.launch_check(rec, [("_ZN4plfx3dev14plf_dna_kernelIfEEvv", 262144, 256)])
     assert not ok and "not dispatched" in why
-    assert bench.launch_check(None, [(mangled, 1, 1)])[0]          # old record: not checked
+    assert not bench.launch_check(None, [(mangled, 1, 1)])[0]      # old record: does not count
     assert bench.launch_check(rec, None)[0]                        # no graph: not checked
+    assert bench.launch_check(None, None)[0]
 
 
 def test_traffic_not_reported_under_dispatch_knobs(monkeypatch):
