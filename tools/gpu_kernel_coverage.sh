@@ -5,9 +5,11 @@
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/cov -o run --output-format csv -- \
-  python3 -m pytest $R/tests -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread \
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/cov -o run --output-format csv -- \
+  python3 -m pytest $R/tests -m gpu -x -q -p no:cacheprovider --timeout 400 --timeout-method thread \
   > $R/gpurun_out/cov.log 2>&1
 rc=$?
+# the per-dispatch trace is large (the merge back is capped): the stats suffice
+find $R/gpurun_out/cov -name "*kernel_trace.csv" -delete
 grep -E "passed|failed" $R/gpurun_out/cov.log | tail -1
 exit $rc

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Which product kernels a run launched: every kernel compiled into libplfx
-(from the device assembly of csrc/plf_kernels.hip, built here) against the
+(from the device assembly of every csrc/*.hip translation unit, built here) against the
 kernel names of a rocprofv3 --kernel-trace --stats run (e.g. the whole GPU
 test suite, tools/gpu_kernel_coverage.sh).
 
@@ -18,12 +18,15 @@ PKG = ROOT / "amd-versal-phylogenetic-likelihood-function_amd"
 
 
 def compiled_kernels():
+    names = set()
     with tempfile.TemporaryDirectory() as d:
-        asm = Path(d) / "k.s"
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                        "-ffp-contract=off", "--cuda-device-only", "-S", "-o", str(asm),
-                        str(PKG / "csrc" / "plf_kernels.hip")], check=True, capture_output=True)
-        names = sorted(set(re.findall(r"\.amdhsa_kernel (\S+)", asm.read_text())))
+        for src in sorted((PKG / "csrc").glob("*.hip")):  # every translation unit with kernels
+            asm = Path(d) / (src.stem + ".s")
+            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                            "-ffp-contract=off", "--cuda-device-only", "-S", "-o", str(asm), str(src)],
+                           check=True, capture_output=True)
+            names |= set(re.findall(r"\.amdhsa_kernel (\S+)", asm.read_text()))
+    names = sorted(names)
     dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True,
                          check=True).stdout.split("\n")
     return dict(zip(names, dem))
