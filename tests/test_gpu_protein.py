@@ -956,6 +956,27 @@ def test_protein_valu_fma_bits(ctx, oracle, n):
     assert fsc.sum() > 0 or n < 4
 
 
+@pytest.mark.parametrize("valu", [False, True])
+def test_protein_f64_optional_outputs(ctx, oracle, valu):
+    """The f64 FMA node without the scaler sum (and without scaler bytes or
+    weights): the kernels' no-sum instantiations, matrix-core and VALU, give
+    the same CLV bits and scaler bytes as with every output."""
+    import torch
+
+    n = 3001
+    x1, x2, EV, left, right, w = gen(n, np.float64, 77)
+    f3, fsc, _ = oracle.plf_generic(S, CAT, x1, x2, EV, left, right, w, fma=True)
+    t = [dev(a) for a in (x1, x2, EV, left, right)]
+    for wgt, with_sc in ((dev(w), True), (None, True), (None, False)):
+        x3 = torch.empty(V * n, dtype=torch.float64, device="cuda")
+        sc = torch.empty(n, dtype=torch.uint8, device="cuda") if with_sc else None
+        ctx.plf_dev_gen(t[0], t[1], x3, t[2], t[3], t[4], S, wgt, sc, None, n=n, fma=True, valu=valu)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(x3.cpu().numpy()), bits(f3))
+        if with_sc:
+            assert np.array_equal(sc.cpu().numpy(), fsc)
+
+
 def test_protein_valu_fma_signed_zeros_and_flags(ctx, oracle):
     """The VALU FMA chains start from +0.0 as the fma() restatement does, on
     inputs full of +-0.0 and underflowing products; PLFX_VALU is refused
