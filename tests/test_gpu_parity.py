@@ -459,9 +459,25 @@ def test_streams_setting_grids_and_bits(oracle, monkeypatch, streams):
     finally:
         c.close()
     monkeypatch.setenv("PLFX_STREAMS", str(streams))
+    monkeypatch.setenv("PLFX_NODE_SEGMENTS", "1")  # the XCD-segmented mapping on the smaller grid
     c = plfx.Context(0)
-    assert c.streams == streams
-    c.close()
+    monkeypatch.delenv("PLFX_NODE_SEGMENTS")
+    try:
+        assert c.streams == streams
+        n = 1 << 20
+        d = oracle.gen_hostmem(n, np.float64, 5)
+        e3, esc, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"], threads=16)
+        t = {k: torch_dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+        x3 = torch.empty_like(t["x1"])
+        sc = torch.empty(n, dtype=torch.uint8, device="cuda")
+        s = torch.zeros(1, dtype=torch.int64, device="cuda")
+        g = [x for x in _captured_grids(lambda sh: c.plf_dev(t["x1"], t["x2"], x3, t["EV"], t["left"], t["right"],
+                                                             t["wgt"], sc, s, stream=sh)) if x[0] and "plf_dna" in x[0]]
+        assert len(g) == 1 and g[0][1] % 8 == 0 and g[0][1] <= 1024 // streams, g
+        assert np.array_equal(bits(x3.cpu().numpy()), bits(e3))
+        assert np.array_equal(sc.cpu().numpy(), esc) and int(s.item()) == einc
+    finally:
+        c.close()
     for bad in ("0", "9", "x", "12", " 2"):
         monkeypatch.setenv("PLFX_STREAMS", bad)
         with pytest.raises(Exception):
