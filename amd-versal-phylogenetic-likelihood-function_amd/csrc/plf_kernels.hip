@@ -163,11 +163,12 @@ hipError_t launch_pair(const DnaArgs &a, int max_blocks, hipStream_t s) {
 template <bool kSum, int kTips>
 hipError_t launch_pair_batch(const dev::NodeBatch &b, int count, const double *EV,
                              const int32_t *wgt, int64_t n, unsigned long long *ws, int max_blocks,
-                             hipStream_t s, const double *tipvec) {
+                             hipStream_t s, const double *tipvec, int share = 1) {
   static int cache = 0;
   auto kernel = &dev::plf_dna_f64_pair_batch_kernel<kU64, kSum, kMinWaves, kNtl64, kTips>;
+  // share: batches the caller keeps in flight on as many streams (plfx_ctx_set_streams)
   const int64_t gx = grid_x((const void *)kernel, cache, kGridMul64, n, kWavesPerBlock * 16 * kU64,
-                            count, max_blocks);
+                            count * std::max(1, share), max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt, n,
                      ws, tipvec);
   return hipGetLastError();
@@ -176,11 +177,11 @@ hipError_t launch_pair_batch(const dev::NodeBatch &b, int count, const double *E
 template <typename T, bool kSum, int kTips>
 hipError_t launch_cat_batch(const dev::NodeBatch &b, int count, const T *EV, const int32_t *wgt,
                             int64_t n, unsigned long long *ws, int max_blocks, hipStream_t s,
-                            const T *tipvec) {
+                            const T *tipvec, int share = 1) {
   static int cache = 0;
   auto kernel = &dev::plf_dna_batch_kernel<T, kU32, kSum, kNt, kMinWaves, kTips>;
   const int64_t gx = grid_x((const void *)kernel, cache, kGridMul32, n, kWavesPerBlock * 16 * kU32,
-                            count, max_blocks);
+                            count * std::max(1, share), max_blocks);
   hipLaunchKernelGGL(kernel, dim3((unsigned)gx, (unsigned)count), dim3(kBlock), 0, s, b, EV, wgt, n,
                      ws, tipvec);
   return hipGetLastError();
@@ -668,7 +669,8 @@ hipError_t launch_plf_dna_f64(const DnaArgs &a, int max_blocks, hipStream_t s) {
 
 hipError_t launch_plf_dna_batch(int dtype, const NodeDescH *nodes, int count, const void *EV,
                                 const int32_t *wgt, int64_t n, unsigned long long *ws,
-                                int max_blocks, hipStream_t s, int tips, const void *tipvec) {
+                                int max_blocks, hipStream_t s, int tips, const void *tipvec,
+                                int share) {
   if (count < 1 || count > kMaxBatch || tips < 0 || tips > 2) return hipErrorInvalidValue;
   dev::NodeBatch b{};
   bool any_sum = false;
@@ -683,18 +685,18 @@ hipError_t launch_plf_dna_batch(int dtype, const NodeDescH *nodes, int count, co
   const double *TV64 = (const double *)tipvec;
   const float *TV32 = (const float *)tipvec;
   switch (key) {
-    case 0: return launch_cat_batch<float, false, 0>(b, count, E32, wgt, n, ws, max_blocks, s, TV32);
-    case 1: return launch_cat_batch<float, false, 1>(b, count, E32, wgt, n, ws, max_blocks, s, TV32);
-    case 2: return launch_cat_batch<float, false, 2>(b, count, E32, wgt, n, ws, max_blocks, s, TV32);
-    case 3: return launch_cat_batch<float, true, 0>(b, count, E32, wgt, n, ws, max_blocks, s, TV32);
-    case 4: return launch_cat_batch<float, true, 1>(b, count, E32, wgt, n, ws, max_blocks, s, TV32);
-    case 5: return launch_cat_batch<float, true, 2>(b, count, E32, wgt, n, ws, max_blocks, s, TV32);
-    case 6: return launch_pair_batch<false, 0>(b, count, E64, wgt, n, ws, max_blocks, s, TV64);
-    case 7: return launch_pair_batch<false, 1>(b, count, E64, wgt, n, ws, max_blocks, s, TV64);
-    case 8: return launch_pair_batch<false, 2>(b, count, E64, wgt, n, ws, max_blocks, s, TV64);
-    case 9: return launch_pair_batch<true, 0>(b, count, E64, wgt, n, ws, max_blocks, s, TV64);
-    case 10: return launch_pair_batch<true, 1>(b, count, E64, wgt, n, ws, max_blocks, s, TV64);
-    default: return launch_pair_batch<true, 2>(b, count, E64, wgt, n, ws, max_blocks, s, TV64);
+    case 0: return launch_cat_batch<float, false, 0>(b, count, E32, wgt, n, ws, max_blocks, s, TV32, share);
+    case 1: return launch_cat_batch<float, false, 1>(b, count, E32, wgt, n, ws, max_blocks, s, TV32, share);
+    case 2: return launch_cat_batch<float, false, 2>(b, count, E32, wgt, n, ws, max_blocks, s, TV32, share);
+    case 3: return launch_cat_batch<float, true, 0>(b, count, E32, wgt, n, ws, max_blocks, s, TV32, share);
+    case 4: return launch_cat_batch<float, true, 1>(b, count, E32, wgt, n, ws, max_blocks, s, TV32, share);
+    case 5: return launch_cat_batch<float, true, 2>(b, count, E32, wgt, n, ws, max_blocks, s, TV32, share);
+    case 6: return launch_pair_batch<false, 0>(b, count, E64, wgt, n, ws, max_blocks, s, TV64, share);
+    case 7: return launch_pair_batch<false, 1>(b, count, E64, wgt, n, ws, max_blocks, s, TV64, share);
+    case 8: return launch_pair_batch<false, 2>(b, count, E64, wgt, n, ws, max_blocks, s, TV64, share);
+    case 9: return launch_pair_batch<true, 0>(b, count, E64, wgt, n, ws, max_blocks, s, TV64, share);
+    case 10: return launch_pair_batch<true, 1>(b, count, E64, wgt, n, ws, max_blocks, s, TV64, share);
+    default: return launch_pair_batch<true, 2>(b, count, E64, wgt, n, ws, max_blocks, s, TV64, share);
   }
 }
 

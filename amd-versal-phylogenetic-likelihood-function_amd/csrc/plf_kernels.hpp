@@ -58,7 +58,7 @@ constexpr int kMaxBatch = 32;
 hipError_t launch_plf_dna_batch(int dtype, const NodeDescH *nodes, int count, const void *EV,
                                 const int32_t *wgt, int64_t n, unsigned long long *ws,
                                 int max_blocks, hipStream_t s, int tips = 0,
-                                const void *tipvec = nullptr);
+                                const void *tipvec = nullptr, int share = 1);
 // Tip/tip protein nodes from their 576-combination tables (plf_prot.hpp
 // prot_tiptip_gather_kernel): x3 / scaler / sum of each node gathered by code pair.
 struct ProtGatherDescH {

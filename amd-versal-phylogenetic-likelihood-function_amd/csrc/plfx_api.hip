@@ -484,7 +484,7 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
                int64_t n, const int32_t *wgt, hipStream_t s, int tips,
                const void *tipvec = nullptr, int states = 4, int flags = PLFX_EXACT,
                int *launches = nullptr, std::vector<TabRef> *tabs = nullptr,
-               const int *ids = nullptr) {
+               const int *ids = nullptr, int streams = 1) {
   if (tabs) tabs->clear();
   if (count < 0 || n < 0 || (count > 0 && (!nodes || !EV)))
     return fail(ctx, PLFX_ERR_INVALID, "bad batch arguments");
@@ -586,7 +586,7 @@ int batch_impl(plfx_ctx *ctx, int dtype, const plfx_node *nodes, int count, cons
     int c = 0;
     for (int i = j; i < count; i += L) sel[c++] = all[i];
     hipError_t e = plfx::launch_plf_dna_batch(dtype, L == 1 ? all : sel, c, EV, wgt, n, w->ws,
-                                              ctx->max_blocks, s, tips, tipvec);
+                                              ctx->max_blocks, s, tips, tipvec, streams);
     if (e != hipSuccess) return hip_fail(ctx, e, "plf batch launch");
     if (launches) ++*launches;
   }
@@ -924,7 +924,10 @@ int plfx_plf_batch_dev(plfx_ctx *ctx, int dtype, int states, const plfx_node *no
   if (dtype != PLFX_F32 && dtype != PLFX_F64) return fail(ctx, PLFX_ERR_INVALID, "bad dtype %d", dtype);
   if (states != 4 && states != 20)
     return fail(ctx, PLFX_ERR_UNSUPPORTED, "batched nodes: states=%d not built (4, 20)", states);
-  return batch_impl(ctx, dtype, nodes, count, EV, n, wgt, pick(ctx, stream), 0, nullptr, states);
+  // DNA batches share the resident grid with the batches of the other
+  // streams in flight (plfx_ctx_set_streams)
+  return batch_impl(ctx, dtype, nodes, count, EV, n, wgt, pick(ctx, stream), 0, nullptr, states,
+                    PLFX_EXACT, nullptr, nullptr, nullptr, ctx->streams);
 }
 
 int plfx_plf_tips_dev_gen(plfx_ctx *ctx, int dtype, int states, int flags, const uint8_t *tip1,

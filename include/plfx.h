@@ -163,13 +163,16 @@ int plfx_ctx_release_stream(plfx_ctx *ctx, void *stream);
  * one-node DNA kernels (plfx_plf_dev_f32 / _f64, plfx_plf_dev_gen with 4
  * states, and the host entries' chunks) and the f64 protein FMA kernel
  * (plfx_plf_dev_gen, 20 states, PLFX_FMA) then launch the co-resident blocks
- * / streams, so the calls in flight fill the GPU together and one call's
+ * / streams, and a DNA batch (plfx_plf_batch_dev) the share of them its
+ * nodes would take / streams, so the calls in flight fill the GPU together and one call's
  * drain overlaps the others' work: 2^20-site f64 nodes alternating over two
  * streams run 0.80 of the HBM peak instead of 0.78 (0.75 one at a time),
  * f32 0.81 instead of 0.77.  Same bits for any value.
  * A call issued alone with streams > 1 runs on the smaller grid (0.64 for
  * the f64 node at 2): set it to what is actually in flight.  Other entry
- * points ignore it.  (Extension: the reference's instances run side by side,
+ * points ignore it.  For many large nodes, one call per node over two streams
+ * beats batches (512 nodes of 2^20 f64 sites: 0.793 vs 0.775 for 32-node
+ * batches on two streams, 0.766 on one).  (Extension: the reference's instances run side by side,
  * app/src/include.h:181-195.)  set: PLFX_ERR_INVALID outside 1..8; get: the
  * value, or PLFX_ERR_INVALID for a null context. */
 int plfx_ctx_set_streams(plfx_ctx *ctx, int streams);
