@@ -431,6 +431,33 @@ def test_streams_setting_grids_and_bits(oracle, monkeypatch, streams):
                 c.release_stream(st_)
             c.set_streams(1)
             del t, outs
+        # a DNA batch (plfx_plf_batch_dev) shares the grid the same way (its
+        # own context: every captured stream keeps a pool workspace)
+        cb = plfx.Context(0)
+        try:
+            nb = 1 << 18
+            d = oracle.gen_hostmem(nb, np.float64, 31)
+            e3, esc, einc = oracle.plf(d["x1"], d["x2"], d["EV"], d["left"], d["right"], d["wgt"])
+            t = {k: torch_dev(d[k]) for k in ("x1", "x2", "EV", "left", "right", "wgt")}
+            bnodes = [dict(x1=t["x1"], x2=t["x2"], x3=torch.empty_like(t["x1"]), left=t["left"],
+                           right=t["right"], scaler=torch.empty(nb, dtype=torch.uint8, device="cuda"),
+                           scaler_sum=torch.zeros(1, dtype=torch.int64, device="cuda")) for _ in range(2)]
+            bgrid = {}
+            for k in (1, streams):
+                cb.set_streams(k)
+                g = [x for x in _captured_grids(lambda sh: cb.plf_batch_dev(bnodes, t["EV"], nb, t["wgt"],
+                                                                            stream=sh))
+                     if x[0] and "batch" in x[0]]
+                assert len(g) == 1, g
+                bgrid[k] = g[0][1]  # workgroups over both nodes
+                for nd in bnodes:
+                    assert np.array_equal(bits(nd["x3"].cpu().numpy()), bits(e3))
+                    assert np.array_equal(nd["scaler"].cpu().numpy(), esc)
+                    assert int(nd["scaler_sum"].item()) == einc
+            assert bgrid[streams] == (bgrid[1] // 2 // streams) * 2, bgrid
+            del t, bnodes
+        finally:
+            cb.close()
         # protein f64 FMA (matrix cores): same bits at 1 and `streams`
         m = 1 << 18
         g = torch.Generator(device="cuda")
