@@ -82,3 +82,15 @@ def test_corrupted_single_rank_line_fails():
         assert c[k]["check"] == "CHECK_FAILED" and c[k]["windows_mismatched"] == 1
     for p in (c["protein"], c["protein"]["valu_fma"], c["protein"]["exact"]):
         assert p["windows_mismatched"] == 1 and p["check"] == "CHECK_FAILED"
+
+
+def test_sweep_small_sites_one_and_two_lanes():
+    """bench.py --sweep: per-call cost at small site counts on one stream and
+    over two lanes (independent outputs), every path's outputs checked."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--sweep", "--sweep-sites", "1,1000,65537"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["check"] == "ok" and [row["sites"] for row in d["rows"]] == [1, 1000, 65537]
+    for row in d["rows"]:
+        assert row["check"] == "ok" and 0 < row["graph_two_lanes_us_per_call"] and 0 < row["graph_us_per_call"]
