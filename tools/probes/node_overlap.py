@@ -21,6 +21,10 @@ steps captured in one HIP graph as the bench does:
   g2c     g2f through the HIP API directly (ctypes hipGraphLaunch /
           hipStreamWaitEvent / hipEventRecord: no torch replay() around it)
   gc3,gc4 g2c over 3 / 4 lanes (--sets must be a multiple of the lanes)
+  g2h     g2c with the context told two calls are in flight
+          (plfx_ctx_set_streams 2: half grids; the bench's form)
+  g2e     g2h with the region's first and last steps at the full grid (they
+          run partly alone)
 --spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is touched.
 Each variant's event time per step around one replay and its host wall from
 before the launch to after the synchronize (what bench.py's `value` divides
@@ -97,6 +101,16 @@ def main():
         torch.cuda.synchronize()
         return g
 
+    def half_sched(K, parity, s, full=()):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for i in range(parity, K, 2):
+                ctx.set_streams(1 if i in full else 2)
+                wl.step(i, s.cuda_stream)
+        ctx.set_streams(1)
+        torch.cuda.synchronize()
+        return g
+
     def run_g2(pair):
         ga, gb = pair
         side[0].wait_stream(main_s)
@@ -123,6 +137,10 @@ def main():
         gs["g2f"] = gs["g2"]
         gs["h2f"] = (half(K, 0, main_s, skip=2), gs["g2"][1])
         gs["g2c"] = gs["g2"]
+        if "g2h" in o.only.split(","):
+            gs["g2h"] = (half_sched(K, 0, main_s), half_sched(K, 1, side[0]))
+        if "g2e" in o.only.split(","):
+            gs["g2e"] = (half_sched(K, 0, main_s, (0, K - 1)), half_sched(K, 1, side[0], (0, K - 1)))
         for L in (3, 4):
             if f"gc{L}" in o.only.split(",") and o.sets % L == 0:
                 gs[f"gc{L}"] = tuple(half(K, l, ([main_s] + side)[l], L=L) for l in range(L))
@@ -141,7 +159,7 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e1b = torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
-                if k in ("g2c", "gc3", "gc4"):
+                if k in ("g2c", "gc3", "gc4", "g2h", "g2e"):
                     lanes = [main_s] + side[:len(gs[k]) - 1]
                     ends = [torch.cuda.Event(enable_timing=True) for _ in lanes]
                     e0.record(main_s)  # creates the HIP events
