@@ -18,7 +18,7 @@ namespace dev {
 // kExact: plf()'s separate multiply and add in its order (bit-identical to
 // the exact LDS kernel and to plf()'s double loop); else every multiply-add
 // fused (bit-identical to the matrix-core kernels and the fma restatement).
-template <bool kSum, bool kExact, int kRows, int kCols>
+template <bool kSum, bool kExact, int kRows, int kCols, bool kPrefetch = true>
 __device__ __forceinline__ void prot_valu_body(const double *__restrict__ x1, const double *__restrict__ x2,
                                                double *__restrict__ x3, const double *__restrict__ EV,
                                                const double *__restrict__ left,
@@ -84,26 +84,28 @@ __device__ __forceinline__ void prot_valu_body(const double *__restrict__ x1, co
   const double *PL = left + c * S * S, *PR = right + c * S * S;
   const int64_t stride = (int64_t)gridDim.x * 64;
   constexpr int K = PT::kChunks / kBlock;
-  V pf[K];  // the next child tile in flight
-  if ((int64_t)blockIdx.x * 64 < n) tile_fetch<double>(x1, (int64_t)blockIdx.x * 64, n, pf);
+  V pf[K];  // the next child tile in flight (kPrefetch)
+  if (kPrefetch && (int64_t)blockIdx.x * 64 < n) tile_fetch<double>(x1, (int64_t)blockIdx.x * 64, n, pf);
   for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += stride) {
     double U[S];
     const int64_t sq = base + lane < n ? base + lane : n - 1;
     const int wsite = kSum ? wgt_at(wgt, sq, ws) : 0;
     {
       double a[S];
+      if constexpr (!kPrefetch) tile_fetch<double>(x1, base, n, pf);
       tile_put<double>(tile, pf);
       __syncthreads();
-      tile_fetch<double>(x2, base, n, pf);  // this trip's x2 while phase 1 runs
+      if constexpr (kPrefetch) tile_fetch<double>(x2, base, n, pf);  // this trip's x2 while phase 1 runs
       row_read<double>(tile, lane, c, a);
       __syncthreads();
       dot(PL, a, [&](int k, double u) { U[k] = u; });
     }
     {
       double b[S];
+      if constexpr (!kPrefetch) tile_fetch<double>(x2, base, n, pf);
       tile_put<double>(tile, pf);
       __syncthreads();
-      if (base + stride < n) tile_fetch<double>(x1, base + stride, n, pf);  // the next trip's x1
+      if (kPrefetch && base + stride < n) tile_fetch<double>(x1, base + stride, n, pf);  // the next trip's x1
       row_read<double>(tile, lane, c, b);
       __syncthreads();
       dot(PR, b, [&](int k, double u) { U[k] = U[k] * u; });  // prod[k] = umpL[k] * umpR[k]
