@@ -33,7 +33,6 @@
 
 #include <algorithm>
 #include <cstdint>
-#include <cstdlib>
 
 #include "plf_kernels.hpp"
 #include "plf_prot_valu.hpp"
@@ -51,19 +50,6 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
   prot_valu_body<kSum, false, kRows, kCols>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum);
 }
 
-// A/B (PLFX_VALU_NOPF=1): the child tiles fetched right before their use, no
-// tile in flight in registers during the phases (fewer VGPRs, no spill)
-template <bool kSum, int kRows, int kCols, int kMinW>
-__global__ void __launch_bounds__(kBlock, kMinW)
-plf_prot_valu_fma_nopf_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
-                              double *__restrict__ x3, const double *__restrict__ EV,
-                              const double *__restrict__ left, const double *__restrict__ right,
-                              const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                              unsigned long long *ws, int64_t *scaler_sum) {
-  prot_valu_body<kSum, false, kRows, kCols, false>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws,
-                                                   scaler_sum);
-}
-
 }  // namespace dev
 
 namespace {
@@ -74,12 +60,11 @@ constexpr int kValuRows = 5, kValuCols = 2, kValuMinW = 3;
 
 template <bool kSum>
 hipError_t launch_valu_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  static const bool nopf = [] {
-    const char *e = std::getenv("PLFX_VALU_NOPF");
-    return e && e[0] == '1';
-  }();
-  auto kernel = nopf ? &dev::plf_prot_valu_fma_nopf_kernel<kSum, kValuRows, kValuCols, kValuMinW>
-                     : &dev::plf_prot_valu_fma_kernel<kSum, kValuRows, kValuCols, kValuMinW>;
+  // the next child tile stays in flight in registers during the phases (168
+  // VGPRs, 21 spilled): fetching it right before use instead (no spill) is
+  // +0.5 % with two streams in flight but -3 % alone
+  // (profiles/r06_probe_valu_nopf.log, plf_prot_valu.hip@95468ac)
+  auto kernel = &dev::plf_prot_valu_fma_kernel<kSum, kValuRows, kValuCols, kValuMinW>;
   static int resident = 0;
   if (!resident) {
     int dev = 0, cus = 0, per_cu = 0;

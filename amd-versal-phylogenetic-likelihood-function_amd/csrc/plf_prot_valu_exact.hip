@@ -11,7 +11,6 @@
 
 #include <algorithm>
 #include <cstdint>
-#include <cstdlib>
 
 #include "plf_kernels.hpp"
 #include "plf_prot_valu.hpp"
@@ -26,17 +25,10 @@ plf_prot_valu_exact_kernel(const double *__restrict__ x1, const double *__restri
                            const double *__restrict__ left, const double *__restrict__ right,
                            const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
                            unsigned long long *ws, int64_t *scaler_sum) {
-  prot_valu_body<kSum, true, kRows, kCols>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum);
-}
-
-// A/B (PLFX_VALU_NOPF=1): the child tiles fetched right before their use
-template <bool kSum, int kRows, int kCols, int kMinW>
-__global__ void __launch_bounds__(kBlock, kMinW)
-plf_prot_valu_exact_nopf_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
-                                double *__restrict__ x3, const double *__restrict__ EV,
-                                const double *__restrict__ left, const double *__restrict__ right,
-                                const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                                unsigned long long *ws, int64_t *scaler_sum) {
+  // kPrefetch = false: each child tile fetched right before its phase, none
+  // held in registers across a phase -- 149 VGPRs and no spill instead of
+  // 168 with 23 spilled: +1-2 % alone and with two streams in flight
+  // (profiles/r06_probe_valu_nopf.log, plf_prot_valu_exact.hip@95468ac)
   prot_valu_body<kSum, true, kRows, kCols, false>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws,
                                                   scaler_sum);
 }
@@ -47,12 +39,7 @@ namespace {
 
 template <bool kSum, int kRows, int kCols, int kMinW>
 hipError_t launch_k(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  static const bool nopf = [] {
-    const char *e = std::getenv("PLFX_VALU_NOPF");
-    return e && e[0] == '1';
-  }();
-  auto kernel = nopf ? &dev::plf_prot_valu_exact_nopf_kernel<kSum, kRows, kCols, kMinW>
-                     : &dev::plf_prot_valu_exact_kernel<kSum, kRows, kCols, kMinW>;
+  auto kernel = &dev::plf_prot_valu_exact_kernel<kSum, kRows, kCols, kMinW>;
   static int resident = 0;
   if (!resident) {
     int dev = 0, cus = 0, per_cu = 0;
