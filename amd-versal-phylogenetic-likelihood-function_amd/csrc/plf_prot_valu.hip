@@ -33,7 +33,6 @@
 
 #include <algorithm>
 #include <cstdint>
-#include <cstdlib>
 
 #include "plf_kernels.hpp"
 #include "plf_prot_valu.hpp"
@@ -51,19 +50,6 @@ plf_prot_valu_fma_kernel(const double *__restrict__ x1, const double *__restrict
   prot_valu_body<kSum, false, kRows, kCols>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws, scaler_sum);
 }
 
-// A/B (PLFX_VALU_LDSX=1): the child's row read from the LDS tile per column
-// chunk instead of held in registers for the phase
-template <bool kSum, int kRows, int kCols, int kMinW>
-__global__ void __launch_bounds__(kBlock, kMinW)
-plf_prot_valu_fma_ldsx_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
-                              double *__restrict__ x3, const double *__restrict__ EV,
-                              const double *__restrict__ left, const double *__restrict__ right,
-                              const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                              unsigned long long *ws, int64_t *scaler_sum) {
-  prot_valu_body<kSum, false, kRows, kCols, true, true>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws,
-                                                        scaler_sum);
-}
-
 }  // namespace dev
 
 namespace {
@@ -77,13 +63,10 @@ hipError_t launch_valu_t(const DnaArgs &a, int max_blocks, hipStream_t s) {
   // the next child tile stays in flight in registers during the phases (168
   // VGPRs, 21 spilled): fetching it right before use instead (no spill) is
   // +0.5 % with two streams in flight but -3 % alone
-  // (profiles/r06_probe_valu_nopf.log, plf_prot_valu.hip@95468ac)
-  static const bool ldsx = [] {
-    const char *e = std::getenv("PLFX_VALU_LDSX");
-    return e && e[0] == '1';
-  }();
-  auto kernel = ldsx ? &dev::plf_prot_valu_fma_ldsx_kernel<kSum, kValuRows, kValuCols, kValuMinW>
-                     : &dev::plf_prot_valu_fma_kernel<kSum, kValuRows, kValuCols, kValuMinW>;
+  // (plf_prot_valu.hip@95468ac), and reading the child's row from the LDS
+  // tile per column chunk (2 spilled) -2 % / -6 % (plf_prot_valu.hpp@d4b0f72;
+  // profiles/r06_probe_valu_nopf.log)
+  auto kernel = &dev::plf_prot_valu_fma_kernel<kSum, kValuRows, kValuCols, kValuMinW>;
   static int resident = 0;
   if (!resident) {
     int dev = 0, cus = 0, per_cu = 0;

@@ -18,7 +18,7 @@ namespace dev {
 // kExact: plf()'s separate multiply and add in its order (bit-identical to
 // the exact LDS kernel and to plf()'s double loop); else every multiply-add
 // fused (bit-identical to the matrix-core kernels and the fma restatement).
-template <bool kSum, bool kExact, int kRows, int kCols, bool kPrefetch = true, bool kLdsX = false>
+template <bool kSum, bool kExact, int kRows, int kCols, bool kPrefetch = true>
 __device__ __forceinline__ void prot_valu_body(const double *__restrict__ x1, const double *__restrict__ x2,
                                                double *__restrict__ x3, const double *__restrict__ EV,
                                                const double *__restrict__ left,
@@ -81,58 +81,6 @@ __device__ __forceinline__ void prot_valu_body(const double *__restrict__ x1, co
       for (int j = 0; j < kRows; j++) fn(gk * kRows + j, u[j]);
     }
   };
-  // kLdsX: the child's row read from the LDS tile per 2-column chunk
-  auto dot_lds = [&](const double *P, const V *r, auto &&fn) {
-#pragma unroll
-    for (int gk = 0; gk < S / kRows; gk++) {
-      const double *G = P + gk * kRows * S;
-      double u[kRows], cur[kRows][kCols], nxt[kRows][kCols];
-#pragma unroll
-      for (int j = 0; j < kRows; j++)
-#pragma unroll
-        for (int q = 0; q < kCols; q++) cur[j][q] = G[j * S + q];
-#pragma unroll
-      for (int lc = 0; lc < S; lc += kCols) {
-        if (lc + kCols < S) {
-#pragma unroll
-          for (int j = 0; j < kRows; j++)
-#pragma unroll
-            for (int q = 0; q < kCols; q++) nxt[j][q] = G[j * S + lc + kCols + q];
-        }
-        double xq[kCols];
-        if constexpr (kLdsX) {
-          static_assert(kCols == 2, "kLdsX reads one f64x2 per 2-column chunk");
-          const V t = r[lc / 2];
-          xq[0] = t.x;
-          xq[1] = t.y;
-        }
-#pragma unroll
-        for (int q = 0; q < kCols; q++) {
-          if constexpr (kExact) {
-            // plf()'s separate roundings: all kRows products, then all kRows
-            // adds (chains start at the first product, as the exact kernel's)
-            double pr[kRows];
-#pragma unroll
-            for (int j = 0; j < kRows; j++) pr[j] = xq[q] * cur[j][q];
-            pin_chains(pr);
-#pragma unroll
-            for (int j = 0; j < kRows; j++) u[j] = lc + q == 0 ? pr[j] : u[j] + pr[j];
-          } else {
-#pragma unroll
-            for (int j = 0; j < kRows; j++)
-              u[j] = __builtin_fma(xq[q], cur[j][q], lc + q == 0 ? 0.0 : u[j]);
-          }
-        }
-        pin_chains(u);
-#pragma unroll
-        for (int j = 0; j < kRows; j++)
-#pragma unroll
-          for (int q = 0; q < kCols; q++) cur[j][q] = nxt[j][q];
-      }
-#pragma unroll
-      for (int j = 0; j < kRows; j++) fn(gk * kRows + j, u[j]);
-    }
-  };
   const double *PL = left + c * S * S, *PR = right + c * S * S;
   const int64_t stride = (int64_t)gridDim.x * 64;
   constexpr int K = PT::kChunks / kBlock;
@@ -148,16 +96,9 @@ __device__ __forceinline__ void prot_valu_body(const double *__restrict__ x1, co
       tile_put<double>(tile, pf);
       __syncthreads();
       if constexpr (kPrefetch) tile_fetch<double>(x2, base, n, pf);  // this trip's x2 while phase 1 runs
-      if constexpr (kLdsX) {
-        (void)a;
-        dot_lds(PL, tile + lane * PT::kStride + c * (PT::kChunksPerSite / 4),
-                [&](int k, double u) { U[k] = u; });
-        __syncthreads();
-      } else {
-        row_read<double>(tile, lane, c, a);
-        __syncthreads();
-        dot(PL, a, [&](int k, double u) { U[k] = u; });
-      }
+      row_read<double>(tile, lane, c, a);
+      __syncthreads();
+      dot(PL, a, [&](int k, double u) { U[k] = u; });
     }
     {
       double b[S];
@@ -165,16 +106,9 @@ __device__ __forceinline__ void prot_valu_body(const double *__restrict__ x1, co
       tile_put<double>(tile, pf);
       __syncthreads();
       if (kPrefetch && base + stride < n) tile_fetch<double>(x1, base + stride, n, pf);  // the next trip's x1
-      if constexpr (kLdsX) {
-        (void)b;
-        dot_lds(PR, tile + lane * PT::kStride + c * (PT::kChunksPerSite / 4),
-                [&](int k, double u) { U[k] = U[k] * u; });
-        __syncthreads();
-      } else {
-        row_read<double>(tile, lane, c, b);
-        __syncthreads();
-        dot(PR, b, [&](int k, double u) { U[k] = U[k] * u; });  // prod[k] = umpL[k] * umpR[k]
-      }
+      row_read<double>(tile, lane, c, b);
+      __syncthreads();
+      dot(PR, b, [&](int k, double u) { U[k] = U[k] * u; });  // prod[k] = umpL[k] * umpR[k]
     }
     // phase 3: O[l] = sum_k U[k] * EV[k][l], fused, from +0.0
     double O[S];

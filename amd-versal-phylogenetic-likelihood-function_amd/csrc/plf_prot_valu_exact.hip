@@ -11,7 +11,6 @@
 
 #include <algorithm>
 #include <cstdint>
-#include <cstdlib>
 
 #include "plf_kernels.hpp"
 #include "plf_prot_valu.hpp"
@@ -34,31 +33,13 @@ plf_prot_valu_exact_kernel(const double *__restrict__ x1, const double *__restri
                                                   scaler_sum);
 }
 
-// A/B (PLFX_VALU_LDSX=1): the tile prefetch kept, the child's row read from
-// the LDS tile per column chunk instead of held in registers
-template <bool kSum, int kRows, int kCols, int kMinW>
-__global__ void __launch_bounds__(kBlock, kMinW)
-plf_prot_valu_exact_ldsx_kernel(const double *__restrict__ x1, const double *__restrict__ x2,
-                                double *__restrict__ x3, const double *__restrict__ EV,
-                                const double *__restrict__ left, const double *__restrict__ right,
-                                const int32_t *__restrict__ wgt, uint8_t *__restrict__ scaler, int64_t n,
-                                unsigned long long *ws, int64_t *scaler_sum) {
-  prot_valu_body<kSum, true, kRows, kCols, true, true>(x1, x2, x3, EV, left, right, wgt, scaler, n, ws,
-                                                       scaler_sum);
-}
-
 }  // namespace dev
 
 namespace {
 
 template <bool kSum, int kRows, int kCols, int kMinW>
 hipError_t launch_k(const DnaArgs &a, int max_blocks, hipStream_t s) {
-  static const bool ldsx = [] {
-    const char *e = std::getenv("PLFX_VALU_LDSX");
-    return e && e[0] == '1';
-  }();
-  auto kernel = ldsx ? &dev::plf_prot_valu_exact_ldsx_kernel<kSum, kRows, kCols, kMinW>
-                     : &dev::plf_prot_valu_exact_kernel<kSum, kRows, kCols, kMinW>;
+  auto kernel = &dev::plf_prot_valu_exact_kernel<kSum, kRows, kCols, kMinW>;
   static int resident = 0;
   if (!resident) {
     int dev = 0, cus = 0, per_cu = 0;
