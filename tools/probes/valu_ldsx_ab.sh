@@ -4,6 +4,8 @@
 # vs read from the LDS tile per 2-column chunk (PLFX_VALU_LDSX=1: 2 spilled),
 # the tile prefetch kept; the VALU tests with the switch on; two lanes
 # alternated three times, then one stream.
+# The PLFX_VALU_LDSX switch exists only in the library built from @d4b0f72 (the A/B
+# code was removed after it); run this against a checkout of that commit.
 set -u
 mkdir -p gpurun_out/r06_ldsx
 PLFX_VALU_LDSX=1 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_protein.py -x -q -k valu --timeout 240 --timeout-method thread > gpurun_out/r06_ldsx/pytest.log 2>&1 || { tail -20 gpurun_out/r06_ldsx/pytest.log; exit 1; }

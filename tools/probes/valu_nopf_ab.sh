@@ -3,6 +3,8 @@
 # with the next child tile in flight in registers (product: 168 VGPRs, 21-23
 # spilled) vs fetched right before use (PLFX_VALU_NOPF=1: 142-164 VGPRs, no
 # spill), two lanes, 2^18 sites, 200 steps after 300 warm-up, alternated 3x.
+# The PLFX_VALU_NOPF switch exists only in the library built from @95468ac (the A/B
+# code was removed after it); run this against a checkout of that commit.
 set -u
 mkdir -p gpurun_out/r06_nopf
 one() {  # name, env value, args...
