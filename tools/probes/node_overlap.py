@@ -25,6 +25,8 @@ steps captured in one HIP graph as the bench does:
           (plfx_ctx_set_streams 2: half grids; the bench's form)
   g2e     g2h with the region's first and last steps at the full grid (they
           run partly alone)
+  g2n     g2h without lane 1's wait on the start event: each lane records its
+          own start event; device time from the earlier start to the later end
 --spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is touched.
 Each variant's event time per step around one replay and its host wall from
 before the launch to after the synchronize (what bench.py's `value` divides
@@ -139,6 +141,8 @@ def main():
         gs["g2c"] = gs["g2"]
         if "g2h" in o.only.split(","):
             gs["g2h"] = (half_sched(K, 0, main_s), half_sched(K, 1, side[0]))
+        if "g2n" in o.only.split(","):
+            gs["g2n"] = (half_sched(K, 0, main_s), half_sched(K, 1, side[0]))
         if "g2e" in o.only.split(","):
             gs["g2e"] = (half_sched(K, 0, main_s, (0, K - 1)), half_sched(K, 1, side[0], (0, K - 1)))
         for L in (3, 4):
@@ -159,6 +163,30 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e1b = torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
+                if k == "g2n":
+                    e0b = torch.cuda.Event(enable_timing=True)
+                    ends = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                    lanes = [main_s, side[0]]
+                    for e, st_ in ((e0, main_s), (e0b, side[0])):
+                        e.record(st_)
+                    for e, st_ in zip(ends, lanes):
+                        e.record(st_)
+                    torch.cuda.synchronize()
+                    ex = [C.c_void_p(int(g.raw_cuda_graph_exec())) for g in gs[k]]
+                    hl = [C.c_void_p(st_.cuda_stream) for st_ in lanes]
+                    starts = [C.c_void_p(e0.cuda_event), C.c_void_p(e0b.cuda_event)]
+                    t0 = time.perf_counter()
+                    for h, x, es in zip(hl, ex, starts):
+                        hip.hipEventRecord(es, h)
+                        hip.hipGraphLaunch(x, h)
+                    for h, e in zip(hl, ends):
+                        hip.hipEventRecord(C.c_void_p(e.cuda_event), h)
+                    hip.hipDeviceSynchronize()
+                    wall[k].append((time.perf_counter() - t0) * 1e6 / K)
+                    first = e0 if e0.elapsed_time(e0b) >= 0 else e0b
+                    res[k].append(max(first.elapsed_time(e) for e in ends) * 1e3 / K)
+                    ok = ok and same()
+                    continue
                 if k in ("g2c", "gc3", "gc4", "g2h", "g2e"):
                     lanes = [main_s] + side[:len(gs[k]) - 1]
                     ends = [torch.cuda.Event(enable_timing=True) for _ in lanes]
