@@ -235,7 +235,16 @@ hipError_t launch_prot_t(const DnaArgs &a, int max_blocks, hipStream_t s, const 
   if constexpr (kFma) {
     static int cache = 0;
     auto kernel = &dev::plf_prot_mfma32_kernel<kSum, 3, kTips>;
-    const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, max_blocks);
+    // with `streams` calls in flight: the resident blocks per CU / streams,
+    // rounded UP to whole blocks per CU (3 per CU -> 2 at two streams: 0.743-
+    // 0.746 vs 0.728-0.730 at the full grid and 0.737 at 1.5 per CU;
+    // profiles/r06_probe_prot_grid_lanes.log)
+    int cap = max_blocks;
+    if (cap <= 0 && a.streams > 1) {
+      const int cus = cu_count(), per_cu = std::max(1, resident_blocks((const void *)kernel, cache) / cus);
+      cap = cus * ((per_cu + a.streams - 1) / a.streams);
+    }
+    const int64_t gx = grid_x((const void *)kernel, cache, 1, a.n, 64, 1, cap);
     hipLaunchKernelGGL(kernel, dim3((unsigned)gx), dim3(kBlock), 0, s, (const T *)a.x1,
                        (const T *)a.x2, (T *)a.x3, (const T *)a.EV, (const T *)a.left,
                        (const T *)a.right, a.wgt, a.scaler, a.n, a.ws, a.scaler_sum, tipvec);

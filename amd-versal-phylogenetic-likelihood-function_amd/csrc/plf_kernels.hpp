@@ -23,7 +23,7 @@ struct DnaArgs {
   int segments = -1;        // node kernels' XCD-segmented site mapping: -1 by size, 0 off,
                             // 1 on (plf_kernels.hip use_segments; PLFX_NODE_SEGMENTS)
   int streams = 1;          // one-node calls the caller keeps in flight (plfx_ctx_set_streams):
-                            // the dense DNA node kernels and the f64 protein FMA kernel
+                            // the dense DNA node kernels and the protein FMA kernels
                             // take the co-resident blocks / streams
 };
 

@@ -161,9 +161,9 @@ int plfx_ctx_release_stream(plfx_ctx *ctx, void *stream);
  * (default 1; PLFX_STREAMS=1..8 in the environment at context creation,
  * empty = 1, anything else fails plfx_ctx_create with PLFX_ERR_INVALID).  The dense
  * one-node DNA kernels (plfx_plf_dev_f32 / _f64, plfx_plf_dev_gen with 4
- * states, and the host entries' chunks) and the f64 protein FMA kernel
- * (plfx_plf_dev_gen, 20 states, PLFX_FMA) then launch the co-resident blocks
- * / streams, and a DNA batch (plfx_plf_batch_dev) the share of them its
+ * states, and the host entries' chunks) and the protein FMA kernels
+ * (plfx_plf_dev_gen, 20 states, PLFX_FMA; f32 rounds up to whole blocks per
+ * CU) then launch the co-resident blocks / streams, and a DNA batch (plfx_plf_batch_dev) the share of them its
  * nodes would take / streams, so the calls in flight fill the GPU together and one call's
  * drain overlaps the others' work: 2^20-site f64 nodes alternating over two
  * streams run 0.80 of the HBM peak instead of 0.78 (0.75 one at a time),

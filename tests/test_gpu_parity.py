@@ -483,6 +483,27 @@ def test_streams_setting_grids_and_bits(oracle, monkeypatch, streams):
         assert res[streams][0] == res[1][0] // streams
         assert np.array_equal(bits(res[1][1]), bits(res[streams][1]))
         assert np.array_equal(res[1][2], res[streams][2]) and res[1][3] == res[streams][3] > 0
+        # protein f32 FMA: whole blocks per CU, rounded up (3 per CU -> 2 at 2 streams)
+        x1f, x2f = x1.float(), x2.float()
+        EVf, Pf = EV.float(), P.float()
+        resf = {}
+        for k in (1, streams):
+            c.set_streams(k)
+            x3 = torch.empty_like(x1f)
+            sc = torch.empty(m, dtype=torch.uint8, device="cuda")
+            ss = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+            def fcall(sh):
+                c.plf_dev_gen(x1f, x2f, x3, EVf, Pf[:1600], Pf[1600:], 20, None, sc, ss, fma=True, stream=sh)
+
+            fg = [x for x in _captured_grids(fcall) if x[0] and "plf_prot_mfma32" in x[0]]
+            assert len(fg) == 1, fg
+            resf[k] = (fg[0][1], x3.cpu().numpy(), sc.cpu().numpy(), int(ss.item()))
+        ncu = torch.cuda.get_device_properties(0).multi_processor_count
+        per_cu = resf[1][0] // ncu
+        assert resf[streams][0] == ncu * -(-per_cu // streams)
+        assert np.array_equal(bits(resf[1][1]), bits(resf[streams][1]))
+        assert np.array_equal(resf[1][2], resf[streams][2]) and resf[1][3] == resf[streams][3] > 0
     finally:
         c.close()
     monkeypatch.setenv("PLFX_STREAMS", str(streams))
